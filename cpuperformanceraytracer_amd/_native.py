@@ -1,0 +1,115 @@
+"""ctypes binding of libpt_mi355.so (include/pt_mi355.h).
+
+The product path is the HIP library only: if it cannot be loaded, or no GPU is present, every
+render call raises -- there is no CPU fallback (the CPU restatement under oracle/ is a test
+checker and is never imported here).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+from .build import LIB as _LIB_PATH
+
+PT_OK = 0
+PT_EINVAL = -1
+PT_EHIP = -2
+PT_ENOMEM = -3
+PT_ESTATE = -4
+
+PT_LAYOUT_INTERLEAVED = 0
+PT_LAYOUT_PLANAR8 = 1
+PT_LAYOUT_TILED_PLANAR8 = 2
+
+PT_FLAG_DEFER_READBACK = 1
+
+# Every symbol include/pt_mi355.h declares (tests/test_abi.py checks they are all exported).
+EXPORTED_SYMBOLS = (
+    "pt_init", "pt_shutdown", "pt_last_error", "pt_default_config", "pt_set_frame", "pt_get_frame",
+    "pt_render_scalar", "pt_render_simd", "pt_render_simd_tiled", "pt_render_tile", "pt_begin_frame",
+    "pt_readback", "pt_render_device", "pt_count_device",
+)
+
+
+class PtConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("num_bounces", ctypes.c_int32),
+                ("samples_per_frame", ctypes.c_int32), ("flags", ctypes.c_uint32),
+                ("ambient", ctypes.c_float * 3)]
+
+
+class PtBufferInfo(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("num_channels", ctypes.c_int32)]
+
+
+class PtTileInfo(ctypes.Structure):
+    _fields_ = [("tile_x", ctypes.c_int32), ("tile_y", ctypes.c_int32),
+                ("tile_width", ctypes.c_int32), ("tile_height", ctypes.c_int32),
+                ("tile_min_x", ctypes.c_int32), ("tile_max_x", ctypes.c_int32),
+                ("tile_min_y", ctypes.c_int32), ("tile_max_y", ctypes.c_int32)]
+
+
+class PtDeviceJob(ctypes.Structure):
+    _fields_ = [("buf", ctypes.c_void_p), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("row_start", ctypes.c_int32), ("row_stride", ctypes.c_int32), ("nrows", ctypes.c_int32),
+                ("layout", ctypes.c_int32), ("frame_first", ctypes.c_uint32), ("nframes", ctypes.c_int32),
+                ("num_bounces", ctypes.c_int32)]
+
+
+class PtWorkCounts(ctypes.Structure):
+    _fields_ = [("segments", ctypes.c_uint64), ("lane_slots", ctypes.c_uint64),
+                ("samples", ctypes.c_uint64), ("escaped", ctypes.c_uint64)]
+
+
+class PtError(RuntimeError):
+    def __init__(self, code: int, what: str, detail: str):
+        super().__init__(f"{what} failed (rc={code}): {detail}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib_path() -> Path:
+    return Path(os.environ.get("PT_MI355_LIB", str(_LIB_PATH)))
+
+
+def load() -> ctypes.CDLL:
+    """Load libpt_mi355.so (build it first with cpuperformanceraytracer_amd.build)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not path.exists():
+        raise FileNotFoundError(f"{path} not built: run `python -m cpuperformanceraytracer_amd.build`")
+    L = ctypes.CDLL(str(path))
+    i32, u32, vp = ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p
+    sig = {
+        "pt_init": (i32, [ctypes.POINTER(PtConfig)]),
+        "pt_shutdown": (None, []),
+        "pt_last_error": (ctypes.c_char_p, []),
+        "pt_default_config": (None, [ctypes.POINTER(PtConfig)]),
+        "pt_set_frame": (i32, [u32]),
+        "pt_get_frame": (u32, []),
+        "pt_render_scalar": (i32, [vp, i32, i32, i32]),
+        "pt_render_simd": (i32, [vp, i32, i32, i32]),
+        "pt_render_simd_tiled": (i32, [vp, i32, i32, i32, i32, i32, i32, i32]),
+        "pt_render_tile": (i32, [ctypes.POINTER(PtBufferInfo), ctypes.POINTER(PtTileInfo)]),
+        "pt_begin_frame": (i32, []),
+        "pt_readback": (i32, [vp]),
+        "pt_render_device": (i32, [ctypes.POINTER(PtDeviceJob), vp]),
+        "pt_count_device": (i32, [ctypes.POINTER(PtDeviceJob), vp, ctypes.POINTER(PtWorkCounts)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != PT_OK:
+        detail = load().pt_last_error().decode(errors="replace")
+        raise PtError(rc, what, detail)

@@ -1,0 +1,80 @@
+"""Build the native libraries in-tree (they travel to the GPU box with the repo snapshot).
+
+  libpt_mi355.so  -- the product: HIP kernels for gfx950 + the C ABI (include/pt_mi355.h) + the
+                     reference-named C++ entry points (include/demofox_path_tracing_mi355.h).
+
+Compile flags that carry the parity contract (DESIGN.md "Numerics"):
+  -ffp-contract=off                           no a*b+c fusion (the reference's MSVC /fp:precise)
+  -fhip-fp32-correctly-rounded-divide-sqrt    IEEE f32 '/' and sqrtf, like x86 SSE
+  -fno-gpu-flush-denormals-to-zero            keep f32 denormals, like x86 SSE
+  no -ffast-math                              NaN/inf/ordering semantics of the C++ source
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIB = PKG / "libpt_mi355.so"
+ARCH = os.environ.get("PT_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["pt_kernel.hip", "pt_scene.cpp", "pt_capi.cpp", "pt_dropin.cpp"]
+HEADERS = ["pt_kernel.h", "pt_scene.h", "pt_sincosf.h"]
+PARITY_FLAGS = [
+    "-ffp-contract=off",
+    "-fhip-fp32-correctly-rounded-divide-sqrt",
+    "-fno-gpu-flush-denormals-to-zero",
+]
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (ROCm required to build libpt_mi355.so)")
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def build_lib(force: bool = False, verbose: bool = False) -> Path:
+    deps = [CSRC / s for s in SOURCES + HEADERS] + [ROOT / "include" / "pt_mi355.h",
+                                                     ROOT / "include" / "demofox_path_tracing_mi355.h",
+                                                     Path(__file__)]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           *PARITY_FLAGS, f"-I{ROOT / 'include'}", f"-I{CSRC}",
+           "-Wall", "-Wno-unused-function",
+           *[str(CSRC / s) for s in SOURCES], "-o", str(LIB) + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(str(LIB) + ".tmp", LIB)
+    return LIB
+
+
+def build_oracle(verbose: bool = False) -> None:
+    """Test infrastructure: the C restatement (oracle/liboracle.so) and, when the reference is
+    present in this container, its own scalar build (oracle/_ref/).  Building the checker is not
+    using it: the product never loads either."""
+    subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
+    ref = Path("/root/reference/CPUPerformanceRayTracer")
+    if ref.exists():
+        subprocess.run([str(ROOT / "oracle" / "build_ref.sh")], check=True,
+                       stdout=None if verbose else subprocess.DEVNULL)
+
+
+if __name__ == "__main__":
+    build_lib(force="--force" in sys.argv, verbose=True)
+    build_oracle(verbose=True)
+    print(LIB)

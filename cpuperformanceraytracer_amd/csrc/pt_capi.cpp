@@ -1,0 +1,363 @@
+// pt_capi.cpp -- the C ABI of libpt_mi355.so (include/pt_mi355.h): validation, frame state,
+// host<->device buffer mirroring, and dispatch to the HIP kernels (pt_kernel.hip).
+//
+// Reference behaviour mirrored here (paths relative to CPUPerformanceRayTracer/):
+//   - frame counter: `static f32 iFrame; iFrame += 1` before rendering (scalar.cpp:798-799,
+//     simd.cpp:483-484, simd_tiled.cpp:547);
+//   - settings checks of ApplicationState::CheckValidSettings (Application.cpp:36-94), returned
+//     as PT_EINVAL instead of __debugbreak();
+//   - the caller owns the host buffer, the call returns after it is updated (Application.cpp:474).
+#include "pt_kernel.h"
+#include "../../include/pt_mi355.h"
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+namespace {
+
+struct State {
+    bool inited = false;
+    pt_config cfg{};
+    hipStream_t stream = nullptr;
+    PtScene scene{};
+    uint32_t frame = 0;                 // value of the reference's static iFrame
+    // device mirror of the caller's host accumulator (host-buffer entry points)
+    float* dbuf = nullptr;
+    size_t dbuf_cap = 0;
+    const float* mirror_host = nullptr; // host buffer the mirror currently represents
+    size_t mirror_bytes = 0;
+    bool mirror_valid = false;          // deferred mode: device copy is authoritative
+    unsigned long long* dcounters = nullptr;
+};
+
+State g;
+char g_err[512] = "no error";
+
+int fail(int code, const char* fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) return fail(PT_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr uint32_t kMaxFrame = 1u << 24;   // iFrame is an f32 counter: exact below 2^24
+
+int ensure_init()
+{
+    if (g.inited) return PT_OK;
+    return pt_init(nullptr);
+}
+
+int ensure_dbuf(size_t bytes)
+{
+    if (bytes <= g.dbuf_cap) return PT_OK;
+    if (g.dbuf) {
+        HIP_TRY(hipStreamSynchronize(g.stream));
+        HIP_TRY(hipFree(g.dbuf));
+        g.dbuf = nullptr;
+        g.dbuf_cap = 0;
+    }
+    if (hipMalloc(&g.dbuf, bytes) != hipSuccess) {
+        g.dbuf = nullptr;
+        return fail(PT_ENOMEM, "hipMalloc(%zu) failed", bytes);
+    }
+    g.dbuf_cap = bytes;
+    g.mirror_valid = false;
+    return PT_OK;
+}
+
+// Make the device mirror hold the host buffer [0, bytes).  In deferred mode an already valid
+// mirror of the same buffer is authoritative and nothing is copied.
+int stage_in(const float* host, size_t bytes, size_t off, size_t len)
+{
+    const bool deferred = (g.cfg.flags & PT_FLAG_DEFER_READBACK) != 0;
+    if (g.mirror_host != host || g.mirror_bytes != bytes) g.mirror_valid = false;
+    int rc = ensure_dbuf(bytes);
+    if (rc) return rc;
+    if (deferred && g.mirror_valid) return PT_OK;
+    if (deferred) {   // first deferred touch: the whole buffer becomes device-resident
+        off = 0;
+        len = bytes;
+    }
+    HIP_TRY(hipMemcpyAsync((char*)g.dbuf + off, (const char*)host + off, len, hipMemcpyHostToDevice, g.stream));
+    g.mirror_host = host;
+    g.mirror_bytes = bytes;
+    g.mirror_valid = deferred;
+    return PT_OK;
+}
+
+int stage_out(float* host, size_t off, size_t len)
+{
+    if (!(g.cfg.flags & PT_FLAG_DEFER_READBACK))
+        HIP_TRY(hipMemcpyAsync((char*)host + off, (const char*)g.dbuf + off, len, hipMemcpyDeviceToHost, g.stream));
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    return PT_OK;
+}
+
+int check_frame_budget(uint32_t add)
+{
+    if ((uint64_t)g.frame + add >= kMaxFrame)
+        return fail(PT_EINVAL, "frame counter %u + %u exceeds the exact f32 range 2^24", g.frame, add);
+    return PT_OK;
+}
+
+PtJob base_job(float* buf, int32_t w, int32_t h)
+{
+    PtJob j{};
+    j.buf = buf;
+    j.width = w;
+    j.height = h;
+    j.col0 = 0;
+    j.ncols = w;
+    j.row_start = 0;
+    j.row_stride = 1;
+    j.nrows = h;
+    j.layout = PT_LAYOUT_INTERLEAVED;
+    j.tile_w = j.tile_h = 0;
+    j.frame_first = g.frame + 1;
+    j.nframes = g.cfg.samples_per_frame;
+    j.num_bounces = g.cfg.num_bounces;
+    j.env = nullptr;
+    j.env_w = j.env_h = 0;
+    j.counters = nullptr;
+    return j;
+}
+
+int launch(const PtJob& j, hipStream_t st, bool count)
+{
+    hipError_t e = pt_launch_render(j, g.scene, st, count);
+    if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
+    return PT_OK;
+}
+
+int check_frame_args(const float* buf, int32_t w, int32_t h, int32_t nc)
+{
+    if (!buf) return fail(PT_EINVAL, "null buffer");
+    if (w <= 0 || h <= 0) return fail(PT_EINVAL, "invalid size %dx%d", w, h);
+    if (nc != 3) return fail(PT_EINVAL, "NumChannels must be 3 (RGB f32), got %d", nc);
+    if ((int64_t)w * h > (int64_t)1 << 30) return fail(PT_EINVAL, "image too large");
+    return PT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void pt_default_config(pt_config* c)
+{
+    if (!c) return;
+    memset(c, 0, sizeof(*c));
+    c->device = 0;
+    c->num_bounces = 4;          // c_numBounces, scalar.cpp:19
+    c->samples_per_frame = 1;    // NUM_SAMPLES_PER_FRAME, global_preprocessor_flags.h:30
+    c->flags = 0;
+    c->ambient[0] = c->ambient[1] = c->ambient[2] = 0.1f;   // scalar.cpp:307
+}
+
+int pt_init(const pt_config* cfg)
+{
+    pt_config c;
+    if (cfg) c = *cfg;
+    else pt_default_config(&c);
+    if (c.num_bounces < 0 || c.num_bounces > 1024) return fail(PT_EINVAL, "num_bounces %d out of range", c.num_bounces);
+    if (c.samples_per_frame < 1 || c.samples_per_frame > 65536)
+        return fail(PT_EINVAL, "samples_per_frame %d out of range", c.samples_per_frame);
+    if (g.inited) pt_shutdown();
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (c.device < 0 || c.device >= ndev) return fail(PT_EHIP, "device %d not available (%d devices)", c.device, ndev);
+    HIP_TRY(hipSetDevice(c.device));
+    HIP_TRY(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
+    if (hipMalloc(&g.dcounters, PT_CNT_N * sizeof(unsigned long long)) != hipSuccess)
+        return fail(PT_ENOMEM, "hipMalloc(counters) failed");
+    g.cfg = c;
+    pt_build_demofox_scene(&g.scene, c.ambient);
+    g.frame = 0;
+    g.inited = true;
+    return PT_OK;
+}
+
+void pt_shutdown(void)
+{
+    if (!g.inited) return;
+    (void)hipSetDevice(g.cfg.device);
+    if (g.stream) (void)hipStreamSynchronize(g.stream);
+    if (g.dbuf) (void)hipFree(g.dbuf);
+    if (g.dcounters) (void)hipFree(g.dcounters);
+    if (g.stream) (void)hipStreamDestroy(g.stream);
+    g = State{};
+}
+
+const char* pt_last_error(void) { return g_err; }
+
+int pt_set_frame(uint32_t frame)
+{
+    if (frame >= kMaxFrame) return fail(PT_EINVAL, "frame %u >= 2^24", frame);
+    g.frame = frame;
+    return PT_OK;
+}
+
+uint32_t pt_get_frame(void) { return g.frame; }
+
+int pt_render_scalar(float* buf, int32_t w, int32_t h, int32_t nc)
+{
+    int rc;
+    if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
+    if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
+    const size_t bytes = (size_t)w * h * 3 * sizeof(float);
+    if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
+    PtJob j = base_job(g.dbuf, w, h);
+    if ((rc = launch(j, g.stream, false))) return rc;
+    g.frame += (uint32_t)g.cfg.samples_per_frame;
+    return stage_out(buf, 0, bytes);
+}
+
+int pt_render_simd(float* buf, int32_t w, int32_t h, int32_t nc)
+{
+    int rc;
+    if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
+    if (w % 8) return fail(PT_EINVAL, "image width %d must be a multiple of 8 (SIMD lane width)", w);
+    if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
+    const size_t bytes = (size_t)w * h * 3 * sizeof(float);
+    if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
+    PtJob j = base_job(g.dbuf, w, h);
+    j.layout = PT_LAYOUT_PLANAR8;
+    if ((rc = launch(j, g.stream, false))) return rc;
+    g.frame += (uint32_t)g.cfg.samples_per_frame;
+    return stage_out(buf, 0, bytes);
+}
+
+int pt_render_simd_tiled(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty, int32_t tw, int32_t th, int32_t nc)
+{
+    int rc;
+    if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
+    // CheckValidSettings (Application.cpp:36-94) + the tile cover DemofoxRenderSimdTiled assumes
+    if (ntx <= 0 || nty <= 0 || tw <= 0 || th <= 0) return fail(PT_EINVAL, "invalid tiling");
+    if (tw % 8) return fail(PT_EINVAL, "tile width %d must be a multiple of 8 (SIMD lane width)", tw);
+    if (w % 8) return fail(PT_EINVAL, "image width %d must be a multiple of 8", w);
+    if (w % ntx || h % nty) return fail(PT_EINVAL, "image %dx%d not divisible into %dx%d tiles", w, h, ntx, nty);
+    if (ntx * tw != w || nty * th != h) return fail(PT_EINVAL, "tiles %dx(%d) x %dx(%d) do not cover %dx%d", ntx, tw, nty, th, w, h);
+    if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
+    const size_t bytes = (size_t)w * h * 3 * sizeof(float);
+    if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
+    PtJob j = base_job(g.dbuf, w, h);
+    j.layout = PT_LAYOUT_TILED_PLANAR8;
+    j.tile_w = tw;
+    j.tile_h = th;
+    if ((rc = launch(j, g.stream, false))) return rc;
+    g.frame += (uint32_t)g.cfg.samples_per_frame;
+    return stage_out(buf, 0, bytes);
+}
+
+int pt_begin_frame(void)
+{
+    int rc;
+    if ((rc = ensure_init())) return rc;
+    if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
+    g.frame += (uint32_t)g.cfg.samples_per_frame;
+    return PT_OK;
+}
+
+int pt_render_tile(const pt_buffer_info* b, const pt_tile_info* t)
+{
+    int rc;
+    if (!b || !t) return fail(PT_EINVAL, "null tile/buffer info");
+    if ((rc = check_frame_args(b->data, b->width, b->height, b->num_channels)) || (rc = ensure_init())) return rc;
+    const int32_t tw = t->tile_width, th = t->tile_height;
+    if (tw <= 0 || th <= 0 || tw % 8) return fail(PT_EINVAL, "tile width %d must be a positive multiple of 8", tw);
+    if (t->tile_x < 0 || t->tile_y < 0) return fail(PT_EINVAL, "negative tile index");
+    if (t->tile_min_x != t->tile_x * tw || t->tile_max_x != t->tile_min_x + tw - 1 ||
+        t->tile_min_y != t->tile_y * th || t->tile_max_y != t->tile_min_y + th - 1)
+        return fail(PT_EINVAL, "tile bounds inconsistent with (TileX, TileY, TileWidth, TileHeight)");
+    if (t->tile_max_x >= b->width || t->tile_max_y >= b->height) return fail(PT_EINVAL, "tile outside the buffer");
+    if (b->width % tw) return fail(PT_EINVAL, "buffer width %d not a multiple of tile width %d", b->width, tw);
+    if (g.frame < (uint32_t)g.cfg.samples_per_frame)
+        return fail(PT_ESTATE, "RenderTile before the first frame was started (pt_begin_frame)");
+    const size_t bytes = (size_t)b->width * b->height * 3 * sizeof(float);
+    // simd_tiled.cpp:499-502: the tile is one contiguous slice
+    const size_t off = ((size_t)t->tile_y * th * b->width * 3 + (size_t)t->tile_x * tw * th * 3) * sizeof(float);
+    const size_t len = (size_t)tw * th * 3 * sizeof(float);
+    if ((rc = stage_in(b->data, bytes, off, len))) return rc;
+    PtJob j = base_job(g.dbuf, b->width, b->height);
+    j.layout = PT_LAYOUT_TILED_PLANAR8;
+    j.tile_w = tw;
+    j.tile_h = th;
+    j.col0 = t->tile_min_x;
+    j.ncols = tw;
+    j.row_start = t->tile_min_y;
+    j.nrows = th;
+    j.frame_first = g.frame - (uint32_t)g.cfg.samples_per_frame + 1;
+    if ((rc = launch(j, g.stream, false))) return rc;
+    return stage_out(b->data, off, len);
+}
+
+int pt_readback(float* buf)
+{
+    if (!g.inited || !g.dbuf || !g.mirror_valid || buf != g.mirror_host)
+        return fail(PT_ESTATE, "no deferred device accumulator for this buffer");
+    HIP_TRY(hipMemcpyAsync(buf, g.dbuf, g.mirror_bytes, hipMemcpyDeviceToHost, g.stream));
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    return PT_OK;
+}
+
+static int device_job(const pt_device_job* dj, PtJob* j)
+{
+    if (!dj || !dj->buf) return fail(PT_EINVAL, "null device job/buffer");
+    if (dj->width <= 0 || dj->height <= 0 || dj->nrows < 0 || dj->row_stride <= 0 || dj->row_start < 0)
+        return fail(PT_EINVAL, "invalid device job geometry");
+    if (dj->nrows > 0 && dj->row_start + (int64_t)(dj->nrows - 1) * dj->row_stride >= dj->height)
+        return fail(PT_EINVAL, "row shard exceeds the image height");
+    if (dj->layout != PT_LAYOUT_INTERLEAVED && dj->layout != PT_LAYOUT_PLANAR8)
+        return fail(PT_EINVAL, "device jobs support the interleaved and planar8 layouts");
+    if (dj->layout == PT_LAYOUT_PLANAR8 && dj->width % 8) return fail(PT_EINVAL, "planar8 needs width % 8 == 0");
+    if (dj->frame_first < 1 || dj->nframes < 0 || (uint64_t)dj->frame_first + (uint64_t)dj->nframes > kMaxFrame)
+        return fail(PT_EINVAL, "frame range [%u, +%d) invalid", dj->frame_first, dj->nframes);
+    if (dj->num_bounces < 0 || dj->num_bounces > 1024) return fail(PT_EINVAL, "num_bounces out of range");
+    *j = base_job(dj->buf, dj->width, dj->height);
+    j->row_start = dj->row_start;
+    j->row_stride = dj->row_stride;
+    j->nrows = dj->nrows;
+    j->layout = dj->layout;
+    j->frame_first = dj->frame_first;
+    j->nframes = dj->nframes;
+    j->num_bounces = dj->num_bounces;
+    return PT_OK;
+}
+
+int pt_render_device(const pt_device_job* dj, void* stream)
+{
+    int rc;
+    PtJob j;
+    if ((rc = ensure_init()) || (rc = device_job(dj, &j))) return rc;
+    return launch(j, (hipStream_t)stream, false);
+}
+
+int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
+{
+    int rc;
+    PtJob j;
+    if (!out) return fail(PT_EINVAL, "null counts");
+    if ((rc = ensure_init()) || (rc = device_job(dj, &j))) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(g.dcounters, 0, PT_CNT_N * sizeof(unsigned long long), st));
+    j.counters = g.dcounters;
+    if ((rc = launch(j, st, true))) return rc;
+    unsigned long long h[PT_CNT_N];
+    HIP_TRY(hipMemcpyAsync(h, g.dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    out->segments = h[PT_CNT_SEGMENTS];
+    out->lane_slots = h[PT_CNT_LANE_SLOTS];
+    out->samples = h[PT_CNT_SAMPLES];
+    out->escaped = h[PT_CNT_ESCAPED];
+    return PT_OK;
+}
+
+}  // extern "C"

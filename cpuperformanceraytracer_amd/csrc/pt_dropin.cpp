@@ -1,0 +1,39 @@
+// pt_dropin.cpp -- the reference's renderer entry points (C++ linkage, same signatures) forwarding
+// to the C ABI.  See include/demofox_path_tracing_mi355.h.
+#include "../../include/demofox_path_tracing_mi355.h"
+#include <stdio.h>
+#include <stdlib.h>
+
+static void pt_check(int rc, const char* what)
+{
+    if (rc == PT_OK) return;
+    fprintf(stderr, "%s: %s (rc=%d)\n", what, pt_last_error(), rc);
+    abort();   // the reference __debugbreak()s on invalid settings (Application.cpp:59,69,79,89)
+}
+
+void DemofoxRenderScalar(f32* BufferOut, i32 Width, i32 Height, i32 NumChannels)
+{
+    pt_check(pt_render_scalar(BufferOut, Width, Height, NumChannels), "DemofoxRenderScalar");
+}
+
+void DemofoxRenderSimd(f32* BufferOut, i32 Width, i32 Height, i32 NumChannels)
+{
+    pt_check(pt_render_simd(BufferOut, Width, Height, NumChannels), "DemofoxRenderSimd");
+}
+
+void DemofoxRenderSimdTiled(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY,
+                            i32 TileWidth, i32 TileHeight, i32 NumChannels)
+{
+    pt_check(pt_render_simd_tiled(BufferOut, BufferWidth, BufferHeight, NumTilesX, NumTilesY, TileWidth, TileHeight,
+                                  NumChannels),
+             "DemofoxRenderSimdTiled");
+}
+
+void RenderTile(RenderBufferInfo& BufferInfo, RenderTileInfo& TileInfo)
+{
+    const pt_buffer_info b = {BufferInfo.BufferDataPtr, BufferInfo.BufferWidth, BufferInfo.BufferHeight,
+                              BufferInfo.NumChannels};
+    const pt_tile_info t = {TileInfo.TileX,    TileInfo.TileY,    TileInfo.TileWidth, TileInfo.TileHeight,
+                            TileInfo.TileMinX, TileInfo.TileMaxX, TileInfo.TileMinY,  TileInfo.TileMaxY};
+    pt_check(pt_render_tile(&b, &t), "RenderTile");
+}

@@ -1,0 +1,41 @@
+// pt_kernel.h -- launch interface between the C-ABI layer (pt_capi.cpp) and the HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "pt_scene.h"
+
+// Output layouts of the reference's frame functions (include/pt_mi355.h documents each).
+enum PtLayout : int32_t {
+    PT_LAYOUT_INTERLEAVED = 0,    // DemofoxRenderScalar: [(row*W + x)*3 + ch]
+    PT_LAYOUT_PLANAR8 = 1,        // DemofoxRenderSimd:   per 8-px group [R x8][G x8][B x8]
+    PT_LAYOUT_TILED_PLANAR8 = 2,  // RenderTile:          tile-major, planar8 inside each tile row
+};
+
+// Work counters written by the COUNT build (one atomic per wave at exit).
+enum PtCounter : int {
+    PT_CNT_SEGMENTS = 0,     // TestSceneTrace calls over all lanes (useful work)
+    PT_CNT_LANE_SLOTS = 1,   // 64 x trace-loop iterations over all waves (issued lane-slots)
+    PT_CNT_SAMPLES = 2,      // primary samples finished
+    PT_CNT_ESCAPED = 3,      // paths that ended on a miss
+    PT_CNT_N = 4,
+};
+
+struct PtJob {
+    float* buf;                 // device accumulator (layout below)
+    int32_t width, height;      // iResolution (full image)
+    int32_t col0, ncols;        // pixel columns [col0, col0 + ncols)
+    int32_t row_start;          // first global row Y (row 0 = top of image)
+    int32_t row_stride;         // global-row step between consecutive buffer rows
+    int32_t nrows;              // buffer rows rendered
+    int32_t layout;             // PtLayout
+    int32_t tile_w, tile_h;     // PT_LAYOUT_TILED_PLANAR8 only
+    uint32_t frame_first;       // iFrame of the first accumulated frame (>= 1)
+    int32_t nframes;            // frames accumulated in order (spp of this launch)
+    int32_t num_bounces;        // c_numBounces
+    const float* env;           // device env map (H x W x 3), nullptr => ambient
+    int32_t env_w, env_h;
+    unsigned long long* counters;  // PT_CNT_N u64, COUNT build only
+};
+
+// Enqueue one render launch on `stream`.  Returns hipSuccess or the launch error.
+hipError_t pt_launch_render(const PtJob& job, const PtScene& scene, hipStream_t stream, bool count);

@@ -1,0 +1,96 @@
+// pt_sincosf.h -- sinf/cosf on the GPU, bit-identical to the host libm the reference calls.
+//
+// RandomUnitVector (demofox_path_tracing_scalar.cpp:42-50) evaluates cos(a) and sin(a) on an f32
+// a in [0, 2*pi].  Under MSVC -- the reference's platform -- those unqualified calls resolve to
+// the float overloads (cosf/sinf); with the image's glibc 2.35 they are glibc's sinf/cosf, whose
+// algorithm evaluates in double: a Cody-Waite-free "fast" reduction by pi/2 (exact enough below
+// 120) and two short double polynomials, rounded once to f32.  Every double op below is IEEE
+// (mul/fma) on both x86-64 and gfx950, so reproducing the same ops with the same constants and
+// the same fused multiply-adds gives the same f32, bit for bit.  This replaces OCML's sinf/cosf,
+// whose results differ by an ulp on a fraction of inputs and would flip hit/miss decisions.
+//
+// Verified exhaustively on every f32 in [0, 2*pi*1.0001] against the host libm in
+// tests/test_sincosf.py (tests/native/check_sincosf.cpp compiles THIS header for the host).
+// Domain: |y| < 120 (the reference's argument never leaves [0, 2*pi]; larger |y| is rejected by
+// the caller's construction, not handled here).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define PT_HD __host__ __device__ __forceinline__
+#else
+#define PT_HD static inline
+#include <math.h>
+#endif
+
+namespace pt {
+
+// glibc 2.35 __sincosf_table[0] (sysdeps/ieee754/flt-32), read from the image's libm.so.6:
+//   hpi_inv = 2/pi * 2^24, hpi = pi/2, cosine c0..c4, sine s1..s3.  Table [1] differs only in the
+//   sign of c0..c4, i.e. cos_poly_T1 == -cos_poly_T0 exactly (round-to-nearest is sign-symmetric).
+constexpr double kHpiInv = 0x1.45f306dc9c883p+23;
+constexpr double kHpi = 0x1.921fb54442d18p+0;
+constexpr double kC0 = 0x1p0;
+constexpr double kC1 = -0x1.ffffffd0c621cp-2;
+constexpr double kC2 = 0x1.55553e1068f19p-5;
+constexpr double kC3 = -0x1.6c087e89a359dp-10;
+constexpr double kC4 = 0x1.99343027bf8c3p-16;
+constexpr double kS1 = -0x1.555545995a603p-3;
+constexpr double kS2 = 0x1.1107605230bc4p-7;
+constexpr double kS3 = -0x1.994eb3774cf24p-13;
+
+PT_HD uint32_t f32_bits(float f)
+{
+#if defined(__HIPCC__)
+    return __builtin_bit_cast(uint32_t, f);
+#else
+    uint32_t u;
+    __builtin_memcpy(&u, &f, 4);
+    return u;
+#endif
+}
+
+// Both results of one argument (the reduction is shared; each output equals the separate call).
+PT_HD void sincosf_glibc(float y, float* s_out, float* c_out)
+{
+    const uint32_t top = (f32_bits(y) >> 20) & 0x7ffu;   // abstop12
+    if (top < 0x398u) {                                   // |y| < 2^-12: sinf = y, cosf = 1
+        *s_out = y;
+        *c_out = 1.0f;
+        return;
+    }
+    double x = (double)y;
+    int n = 0;
+    if (top >= 0x3f4u) {                                  // |y| >= 0.75 (abstop12(pio4f)): reduce
+        const double r = x * kHpiInv;
+        n = ((int32_t)r + 0x800000) >> 24;
+        x = __builtin_fma(-(double)n, kHpi, x);
+    }
+    const double sg = ((n + 1) & 2) ? -1.0 : 1.0;        // sign[n & 3] = {1,-1,-1,1}
+    const double xs = x * sg;
+    const double x2 = x * x;
+    // sine polynomial (sinf_poly, even n)
+    const double x3 = xs * x2;
+    const double s1 = __builtin_fma(x2, kS3, kS2);
+    const double x7 = x3 * x2;
+    const double ss = __builtin_fma(x3, kS1, xs);
+    const float sp = (float)__builtin_fma(x7, s1, ss);
+    // cosine polynomial (sinf_poly, odd n), table selected by n & 2
+    const double x4 = x2 * x2;
+    const double c2 = __builtin_fma(x2, kC4, kC3);
+    const double c1 = __builtin_fma(x2, kC1, kC0);
+    const double x6 = x4 * x2;
+    const double cc = __builtin_fma(x4, kC2, c1);
+    float cp = (float)__builtin_fma(x6, c2, cc);
+    if (n & 2) cp = -cp;
+    // sinf uses poly(n), cosf uses poly(n ^ 1)
+    if (n & 1) {
+        *s_out = cp;
+        *c_out = sp;
+    } else {
+        *s_out = sp;
+        *c_out = cp;
+    }
+}
+
+}  // namespace pt

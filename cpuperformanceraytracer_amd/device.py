@@ -1,0 +1,64 @@
+"""Device-resident rendering on torch tensors (HBM in, HBM out; the bench and multi-GPU path).
+
+PyTorch is plumbing here: it owns the device allocation and the stream; the work is the HIP
+kernel in libpt_mi355.so, reached through pt_render_device / pt_count_device.
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import _native as N
+
+_backend_device = None
+
+
+def ensure_backend(device_index: int, num_bounces: int = 4) -> None:
+    """Initialise libpt_mi355 on `device_index` (the torch device of this rank)."""
+    global _backend_device
+    if _backend_device == device_index:
+        return
+    from .renderer import init
+    init(num_bounces=num_bounces, device=device_index)
+    _backend_device = device_index
+
+
+def _job(buf, width: int, height: int, row_start: int, row_stride: int, nrows: int, frame_first: int,
+         nframes: int, num_bounces: int, layout: int) -> N.PtDeviceJob:
+    import torch
+    if not isinstance(buf, torch.Tensor) or buf.device.type != "cuda":
+        raise N.PtError(N.PT_EINVAL, "render_device", "buf must be a device (cuda/hip) tensor")
+    if buf.dtype != torch.float32 or not buf.is_contiguous():
+        raise N.PtError(N.PT_EINVAL, "render_device", "buf must be contiguous float32")
+    if buf.numel() < nrows * width * 3:
+        raise N.PtError(N.PT_EINVAL, "render_device", f"buf holds {buf.numel()} < {nrows}x{width}x3 floats")
+    ensure_backend(buf.device.index if buf.device.index is not None else torch.cuda.current_device(), num_bounces)
+    return N.PtDeviceJob(buf.data_ptr(), width, height, row_start, row_stride, nrows, layout, frame_first,
+                         nframes, num_bounces)
+
+
+def _stream(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def render_device(buf, width: int, height: int, *, frame_first: int, nframes: int, num_bounces: int,
+                  row_start: int = 0, row_stride: int = 1, nrows: int | None = None,
+                  layout: int = N.PT_LAYOUT_INTERLEAVED, stream=None) -> None:
+    """Accumulate frames [frame_first, frame_first+nframes) of global rows row_start + k*row_stride
+    (k < nrows) into `buf` (nrows x width x 3 f32, in HBM).  Asynchronous on `stream`."""
+    nrows = height if nrows is None else nrows
+    job = _job(buf, width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces, layout)
+    N.check(N.load().pt_render_device(ctypes.byref(job), _stream(stream)), "pt_render_device")
+
+
+def count_device(buf, width: int, height: int, *, frame_first: int, nframes: int, num_bounces: int,
+                 row_start: int = 0, row_stride: int = 1, nrows: int | None = None,
+                 layout: int = N.PT_LAYOUT_INTERLEAVED, stream=None) -> dict:
+    """Like render_device (it does render into buf) but also counts the work: traced segments,
+    issued lane-slots, samples, escaped paths.  Synchronous."""
+    nrows = height if nrows is None else nrows
+    job = _job(buf, width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces, layout)
+    out = N.PtWorkCounts()
+    N.check(N.load().pt_count_device(ctypes.byref(job), _stream(stream), ctypes.byref(out)), "pt_count_device")
+    return {"segments": out.segments, "lane_slots": out.lane_slots, "samples": out.samples, "escaped": out.escaped}

@@ -1,0 +1,133 @@
+"""Host-side mirror of the reference renderer interface, backed by libpt_mi355.so.
+
+Same names, argument meaning and error behaviour as the reference's frame functions
+(paths relative to /root/reference/CPUPerformanceRayTracer/):
+
+  DemofoxRenderScalar(BufferOut, Width, Height, NumChannels)      demofox_path_tracing_scalar.h:7
+  DemofoxRenderSimd(BufferOut, Width, Height, NumChannels)        demofox_path_tracing_simd.h:7
+  DemofoxRenderSimdTiled(BufferOut, W, H, NTX, NTY, TW, TH, NC)   demofox_path_tracing_simd_tiled.h:7
+  RenderBufferInfo / RenderTileInfo / RenderTile(info, tile)      demofox_path_tracing_simd_tiled.cpp:473-535
+
+`BufferOut` is a float32 numpy array (the host render target of Application.cpp:142-151).  Each
+frame call advances the frame counter first (the reference's `static f32 iFrame`) and returns after
+the buffer holds the running average -- bit-identical to the reference's scalar path.  Invalid
+settings raise PtError (the reference __debugbreak()s, Application.cpp:36-94).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _native as N
+
+
+def _buf(a: np.ndarray, width: int, height: int, num_channels: int) -> int:
+    if not isinstance(a, np.ndarray) or a.dtype != np.float32 or not a.flags["C_CONTIGUOUS"]:
+        raise N.PtError(N.PT_EINVAL, "buffer", "BufferOut must be a C-contiguous float32 numpy array")
+    if not a.flags["WRITEABLE"]:
+        raise N.PtError(N.PT_EINVAL, "buffer", "BufferOut must be writeable")
+    if width > 0 and height > 0 and num_channels > 0 and a.size < width * height * num_channels:
+        raise N.PtError(N.PT_EINVAL, "buffer", f"BufferOut holds {a.size} floats < {width}x{height}x{num_channels}")
+    return a.ctypes.data
+
+
+def init(num_bounces: int = 4, samples_per_frame: int = 1, ambient=(0.1, 0.1, 0.1), device: int = 0,
+         defer_readback: bool = False) -> None:
+    """(Re)initialise the backend: the runtime form of the reference's compile-time settings
+    (c_numBounces scalar.cpp:19, NUM_SAMPLES_PER_FRAME global_preprocessor_flags.h:30).
+    Resets the frame counter to 0, like a fresh process of the reference."""
+    L = N.load()
+    c = N.PtConfig()
+    L.pt_default_config(ctypes.byref(c))
+    c.device = device
+    c.num_bounces = num_bounces
+    c.samples_per_frame = samples_per_frame
+    c.flags = N.PT_FLAG_DEFER_READBACK if defer_readback else 0
+    for i in range(3):
+        c.ambient[i] = float(ambient[i])
+    N.check(L.pt_init(ctypes.byref(c)), "pt_init")
+
+
+def shutdown() -> None:
+    N.load().pt_shutdown()
+
+
+def set_frame(frame: int) -> None:
+    """Set the value of the reference's static iFrame (the next frame call renders frame+1)."""
+    N.check(N.load().pt_set_frame(frame), "pt_set_frame")
+
+
+def get_frame() -> int:
+    return int(N.load().pt_get_frame())
+
+
+def readback(BufferOut: np.ndarray) -> None:
+    """defer_readback mode: copy the HBM-resident accumulator into BufferOut."""
+    N.check(N.load().pt_readback(_buf(BufferOut, 0, 0, 0)), "pt_readback")
+
+
+def DemofoxRenderScalar(BufferOut: np.ndarray, Width: int, Height: int, NumChannels: int) -> None:
+    N.check(N.load().pt_render_scalar(_buf(BufferOut, Width, Height, NumChannels), Width, Height, NumChannels),
+            "DemofoxRenderScalar")
+
+
+def DemofoxRenderSimd(BufferOut: np.ndarray, Width: int, Height: int, NumChannels: int) -> None:
+    N.check(N.load().pt_render_simd(_buf(BufferOut, Width, Height, NumChannels), Width, Height, NumChannels),
+            "DemofoxRenderSimd")
+
+
+def DemofoxRenderSimdTiled(BufferOut: np.ndarray, BufferWidth: int, BufferHeight: int, NumTilesX: int,
+                           NumTilesY: int, TileWidth: int, TileHeight: int, NumChannels: int) -> None:
+    N.check(N.load().pt_render_simd_tiled(_buf(BufferOut, BufferWidth, BufferHeight, NumChannels), BufferWidth,
+                                          BufferHeight, NumTilesX, NumTilesY, TileWidth, TileHeight, NumChannels),
+            "DemofoxRenderSimdTiled")
+
+
+@dataclass
+class RenderBufferInfo:
+    """demofox_path_tracing_simd_tiled.cpp:473-479"""
+    BufferDataPtr: np.ndarray
+    BufferWidth: int
+    BufferHeight: int
+    NumChannels: int
+
+
+@dataclass
+class RenderTileInfo:
+    """demofox_path_tracing_simd_tiled.cpp:481-487"""
+    TileX: int
+    TileY: int
+    TileWidth: int
+    TileHeight: int
+    TileMinX: int
+    TileMaxX: int
+    TileMinY: int
+    TileMaxY: int
+
+
+def BeginFrame() -> None:
+    """Advance the frame counter once without rendering (what DemofoxRenderSimdTiled does before
+    fanning out RenderTile calls, simd_tiled.cpp:547)."""
+    N.check(N.load().pt_begin_frame(), "pt_begin_frame")
+
+
+def RenderTile(BufferInfo: RenderBufferInfo, TileInfo: RenderTileInfo) -> None:
+    """Render one tile at the current frame into its tile-major slice (simd_tiled.cpp:489-535)."""
+    b = N.PtBufferInfo(_buf(BufferInfo.BufferDataPtr, BufferInfo.BufferWidth, BufferInfo.BufferHeight,
+                            BufferInfo.NumChannels),
+                       BufferInfo.BufferWidth, BufferInfo.BufferHeight, BufferInfo.NumChannels)
+    t = N.PtTileInfo(TileInfo.TileX, TileInfo.TileY, TileInfo.TileWidth, TileInfo.TileHeight,
+                     TileInfo.TileMinX, TileInfo.TileMaxX, TileInfo.TileMinY, TileInfo.TileMaxY)
+    N.check(N.load().pt_render_tile(ctypes.byref(b), ctypes.byref(t)), "RenderTile")
+
+
+def make_tiles(width: int, height: int, num_tiles_x: int, num_tiles_y: int):
+    """The tile list DemofoxRenderSimdTiled walks (simd_tiled.cpp:549-571)."""
+    tw, th = width // num_tiles_x, height // num_tiles_y
+    tiles = []
+    for tx in range(num_tiles_x):
+        for ty in range(num_tiles_y):
+            tiles.append(RenderTileInfo(tx, ty, tw, th, tx * tw, tx * tw + tw - 1, ty * th, ty * th + th - 1))
+    return tiles

@@ -1,0 +1,36 @@
+// include/demofox_path_tracing_mi355.h -- reference-shaped C++ surface of libpt_mi355.so.
+//
+// Same names, signatures and C++ linkage as the reference's renderer headers, so a reference host
+// (Application.cpp:474 style) links against libpt_mi355.so instead of compiling the CPU renderer:
+//   demofox_path_tracing_scalar.h:7      void DemofoxRenderScalar(f32*, i32, i32, i32)
+//   demofox_path_tracing_simd.h:7        void DemofoxRenderSimd(f32*, i32, i32, i32)
+//   demofox_path_tracing_simd_tiled.h:7  void DemofoxRenderSimdTiled(f32*, i32, i32, i32, i32, i32, i32, i32)
+//   demofox_path_tracing_simd_tiled.cpp:473-489  RenderBufferInfo, RenderTileInfo, RenderTile(&, &)
+// Like the reference (which __debugbreak()s on bad settings), these have no error return: on
+// failure they print pt_last_error() to stderr and abort().
+#pragma once
+#include <stdint.h>
+#include "pt_mi355.h"
+
+typedef float f32;
+typedef int32_t i32;
+
+struct RenderBufferInfo {
+    f32* BufferDataPtr;
+    i32 BufferWidth;
+    i32 BufferHeight;
+    i32 NumChannels;
+};
+
+struct RenderTileInfo {
+    i32 TileX, TileY;
+    i32 TileWidth, TileHeight;
+    i32 TileMinX, TileMaxX;
+    i32 TileMinY, TileMaxY;
+};
+
+void DemofoxRenderScalar(f32* BufferOut, i32 Width, i32 Height, i32 NumChannels);
+void DemofoxRenderSimd(f32* BufferOut, i32 Width, i32 Height, i32 NumChannels);
+void DemofoxRenderSimdTiled(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY,
+                            i32 TileWidth, i32 TileHeight, i32 NumChannels);
+void RenderTile(RenderBufferInfo& BufferInfo, RenderTileInfo& TileInfo);

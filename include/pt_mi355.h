@@ -1,0 +1,117 @@
+/* include/pt_mi355.h -- C ABI of the MI355X (gfx950) path-tracing backend, libpt_mi355.so.
+ *
+ * Drop-in boundary for the reference's per-pixel path-tracing hot path
+ * (torgeiba/CPUPerformanceRayTracer; file:line below are relative to CPUPerformanceRayTracer/).
+ * Plain C types only: pointers, sizes, POD structs.  Every function returns PT_OK (0) or a
+ * negative PT_E* code; pt_last_error() then describes the failure (the reference has no error
+ * returns -- it __debugbreak()s, Application.cpp:59,69,79,89 -- see the C++ wrappers in
+ * demofox_path_tracing_mi355.h for the reference-shaped, abort-on-error surface).
+ *
+ * Semantics: results are bit-identical to the reference's scalar path
+ * (demofox_path_tracing_scalar.cpp) for the same (pixel, frame): same Wang-hash seed, same f32
+ * operations in the same order, glibc-identical sinf/cosf.  Frame state mirrors the reference's
+ * `static f32 iFrame` (scalar.cpp:798-799): each frame call first increments it, then renders
+ * with it; the first call renders frame 1.
+ *
+ * Threading: like the reference (static state, not re-entrant) -- call from one host thread.
+ */
+#ifndef PT_MI355_H
+#define PT_MI355_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_OK 0
+#define PT_EINVAL (-1)   /* invalid argument / settings (CheckValidSettings, Application.cpp:36-94) */
+#define PT_EHIP (-2)     /* HIP runtime error (no device, launch failure, ...)                     */
+#define PT_ENOMEM (-3)   /* device allocation failed                                               */
+#define PT_ESTATE (-4)   /* call out of order (e.g. readback without a deferred buffer)            */
+
+/* Buffer layouts written by the reference's three frame functions. */
+#define PT_LAYOUT_INTERLEAVED 0    /* DemofoxRenderScalar: RGB of pixel (X,Y) at 3*(Y*W+X)+c          */
+#define PT_LAYOUT_PLANAR8 1        /* DemofoxRenderSimd (simd.cpp:496-511): per row, per 8 pixels    */
+                                   /*   [R0..R7][G0..G7][B0..B7]                                      */
+#define PT_LAYOUT_TILED_PLANAR8 2  /* RenderTile (simd_tiled.cpp:499-531): tile-major, planar8 rows   */
+
+#define PT_FLAG_DEFER_READBACK 1u  /* keep the accumulator in HBM between frame calls: no H2D/D2H;    */
+                                   /* the host buffer is refreshed only by pt_readback().            */
+
+/* Runtime form of the reference's compile-time configuration (global_preprocessor_flags.h and the
+ * file-scope constants of demofox_path_tracing_scalar.cpp:6-25). */
+typedef struct pt_config {
+    int32_t device;              /* HIP device ordinal                                             */
+    int32_t num_bounces;         /* c_numBounces (scalar.cpp:19); reference default 4              */
+    int32_t samples_per_frame;   /* NUM_SAMPLES_PER_FRAME (flags.h:30): frames accumulated per call */
+    uint32_t flags;              /* PT_FLAG_*                                                      */
+    float ambient[3];            /* miss radiance (scalar.cpp:307), reference default 0.1          */
+} pt_config;
+
+/* Mirrors of RenderBufferInfo / RenderTileInfo (demofox_path_tracing_simd_tiled.cpp:473-487). */
+typedef struct pt_buffer_info {
+    float* data;                 /* BufferDataPtr (host memory, W*H*NumChannels f32)               */
+    int32_t width, height, num_channels;
+} pt_buffer_info;
+
+typedef struct pt_tile_info {
+    int32_t tile_x, tile_y;
+    int32_t tile_width, tile_height;
+    int32_t tile_min_x, tile_max_x;
+    int32_t tile_min_y, tile_max_y;
+} pt_tile_info;
+
+/* Device-resident job: the buffer already lives in HBM (bench, multi-GPU shards).  Renders the
+ * global rows Y = row_start + k*row_stride, k in [0, nrows), of a width x height image into a
+ * compact buffer of nrows rows, accumulating frames frame_first .. frame_first+nframes-1. */
+typedef struct pt_device_job {
+    float* buf;                  /* device pointer                                                  */
+    int32_t width, height;
+    int32_t row_start, row_stride, nrows;
+    int32_t layout;              /* PT_LAYOUT_INTERLEAVED or PT_LAYOUT_PLANAR8                      */
+    uint32_t frame_first;        /* >= 1                                                            */
+    int32_t nframes;
+    int32_t num_bounces;
+} pt_device_job;
+
+/* Work counters of pt_count_device(). */
+typedef struct pt_work_counts {
+    uint64_t segments;           /* TestSceneTrace calls (traced ray segments)                     */
+    uint64_t lane_slots;         /* 64 x loop iterations issued per wave, summed over waves        */
+    uint64_t samples;            /* primary samples (pixels x frames)                              */
+    uint64_t escaped;            /* paths that ended on a miss                                     */
+} pt_work_counts;
+
+/* --- lifecycle -------------------------------------------------------------------------------- */
+int pt_init(const pt_config* cfg);            /* NULL => defaults; (re)initialises the backend      */
+void pt_shutdown(void);
+const char* pt_last_error(void);
+void pt_default_config(pt_config* cfg);
+int pt_set_frame(uint32_t frame);             /* set the static iFrame value (next call: frame+1)  */
+uint32_t pt_get_frame(void);
+
+/* --- drop-in frame entry points (host buffers; synchronous: the buffer is updated on return) --- */
+/* replaces DemofoxRenderScalar, demofox_path_tracing_scalar.h:7 / .cpp:785-820 */
+int pt_render_scalar(float* buf, int32_t width, int32_t height, int32_t num_channels);
+/* replaces DemofoxRenderSimd, demofox_path_tracing_simd.h:7 / .cpp:468-514 (planar8 layout) */
+int pt_render_simd(float* buf, int32_t width, int32_t height, int32_t num_channels);
+/* replaces DemofoxRenderSimdTiled, demofox_path_tracing_simd_tiled.h:7 / .cpp:537-574 */
+int pt_render_simd_tiled(float* buf, int32_t width, int32_t height, int32_t num_tiles_x, int32_t num_tiles_y,
+                         int32_t tile_width, int32_t tile_height, int32_t num_channels);
+/* replaces RenderTile, demofox_path_tracing_simd_tiled.cpp:489-535 (renders at the current frame,
+ * does not advance it; only the tile's contiguous slice of the buffer is transferred) */
+int pt_render_tile(const pt_buffer_info* buffer, const pt_tile_info* tile);
+/* advance the frame counter once (DemofoxRenderSimdTiled :547) without rendering -- for hosts that
+ * fan RenderTile calls out themselves (the v4 / simt_pooled pattern) */
+int pt_begin_frame(void);
+/* PT_FLAG_DEFER_READBACK: copy the device accumulator of `buf` back into it */
+int pt_readback(float* buf);
+
+/* --- device-resident entry points -------------------------------------------------------------- */
+int pt_render_device(const pt_device_job* job, void* hip_stream);      /* async on hip_stream     */
+int pt_count_device(const pt_device_job* job, void* hip_stream, pt_work_counts* out); /* sync;    */
+                                  /* renders like pt_render_device AND counts the work it did     */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,56 @@
+#!/usr/bin/env bash
+# oracle/build_ref.sh -- TEST INFRASTRUCTURE ONLY.
+#
+# Builds the reference's own scalar path tracer (unmodified, compiled where it lies under
+# /root/reference) into oracle/_ref/ so it can (a) generate the golden fixtures in tests/golden
+# and (b) serve as the "reference" CPU baseline in bench.py.  Nothing from the reference is
+# copied into the repository: the one generated header (a selection of mathlib.h's own scalar
+# lines, see below) lives in a temporary directory that is deleted on exit, and only the
+# compiled binary/.so land in oracle/_ref/ (git-ignored).
+#
+# Why a generated header: the reference's full mathlib.h only compiles under MSVC (it overloads
+# operators on __m256 and calls SVML).  demofox_path_tracing_scalar.cpp only needs mathlib.h's
+# scalar f32xN subset, so we extract exactly those line ranges and add
+# `using std::{sqrt,abs,cos,sin,tan};`: MSVC's <cmath> declares the float overloads of these in
+# the global namespace, so the reference's unqualified calls on f32 (scalar.cpp:46-48,122,126,
+# 169,173,338) are sqrtf/fabsf/cosf/sinf/tanf under MSVC.  libstdc++'s <cmath> only has the double
+# versions globally: without the using-declarations GCC binds abs(float) to abs(int) (5 pixels
+# differ) and cos/sin/tan to double precision (a different rounding of x, y and
+# the camera distance).  The float overloads here resolve to glibc's sinf/cosf/tanf.
+# `-I-` stops GCC from searching the reference directory first for "mathlib.h".
+#
+# Flags: -O2 -ffp-contract=off  (MSVC /fp:precise does not contract a*b+c).
+set -euo pipefail
+REF=${REF:-/root/reference/CPUPerformanceRayTracer}
+HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
+OUT="$HERE/_ref"
+if [ ! -f "$REF/demofox_path_tracing_scalar.cpp" ]; then
+    echo "build_ref.sh: reference not present at $REF -- skipping (prebuilt files are used)" >&2
+    exit 0
+fi
+mkdir -p "$OUT"
+GEN="$(mktemp -d "${TMPDIR:-/tmp}/ptref.XXXXXX")"
+trap 'rm -rf "$GEN"' EXIT
+M="$REF/mathlib.h"
+{
+    echo '#pragma once'
+    echo '#include "utils.h"'
+    echo '#include <cmath>'
+    echo 'using std::sqrt; using std::abs; using std::cos; using std::sin; using std::tan;'
+    awk 'NR>=12&&NR<=72' "$M"              # f32x2/3/4 structs + add/sub/mul/div/dot/fmadd
+    awk 'NR==415||NR==436||NR==437' "$M"   # (comment) + sroot/rsroot(f32)
+    awk 'NR>=582&&NR<=619' "$M"            # scalar operator+ - * /
+    awk 'NR>=723&&NR<=726' "$M"            # len(f32xN)
+    awk 'NR>=729&&NR<=731' "$M"            # (comments)
+    awk 'NR>=749&&NR<=751' "$M"            # normalize(f32xN)
+    awk 'NR==763||NR==768' "$M"            # lerp, cross(f32x3)
+} > "$GEN/mathlib.h"
+CXX=${CXX:-g++}
+FLAGS="-std=c++17 -O2 -ffp-contract=off -fPIC -w"
+INC="-I$GEN -I- -I$GEN -I$REF"
+$CXX $FLAGS $INC -c "$REF/demofox_path_tracing_scalar.cpp" -o "$GEN/scalar.o" 2>/dev/null
+$CXX $FLAGS -c "$HERE/ref_driver.cpp" -o "$GEN/drv.o"
+$CXX $FLAGS -DREF_DRIVER_MAIN -c "$HERE/ref_driver.cpp" -o "$GEN/drv_main.o"
+$CXX -shared -o "$OUT/libref_scalar.so" "$GEN/scalar.o" "$GEN/drv.o" -lm
+$CXX -o "$OUT/ref_scalar" "$GEN/scalar.o" "$GEN/drv_main.o" -lm
+echo "build_ref.sh: built $OUT/libref_scalar.so and $OUT/ref_scalar"

@@ -1,0 +1,75 @@
+/* oracle/pt_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C, written from scratch) of the reference's scalar diffuse+emissive
+ * path tracer, demofox_path_tracing_scalar.cpp (paths relative to
+ * /root/reference/CPUPerformanceRayTracer/).  It is the parity checker for the HIP product path:
+ * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.
+ *
+ * Pinning: bit-identical to the reference's own scalar code (compiled unmodified by
+ * oracle/build_ref.sh) on the committed golden fixtures in tests/golden/ (f32, xz)
+ * (256x256, 1 and 8 frames, 4 bounces) -- see tests/test_oracle.py.
+ *
+ * Generalisations beyond the reference's compile-time constants (each is a loop bound or a
+ * constant the reference hard-codes, the arithmetic is unchanged):
+ *   - num_bounces           (c_numBounces, scalar.cpp:19; 4 in the reference, 8 in configs 2-5)
+ *   - frame_first, nframes  (the static iFrame, scalar.cpp:798-799; nframes calls in a row)
+ *   - row_start/row_stride  (render a row-interleaved shard of the image with GLOBAL pixel
+ *                            coordinates, so every shard is bit-identical to the full image)
+ *   - env                   (miss radiance = equirectangular env sample, the textured variant
+ *                            demofox_path_tracing_simt_textured.cpp:408 -> texture.cpp:101-139;
+ *                            NOT pinned by a reference run: that file needs SVML)
+ */
+#ifndef PT_ORACLE_H
+#define PT_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pto_env {
+    const float* data;   /* Height x Width x 3 f32, row 0 = bottom (stbi flip-on-load, asset_loading.cpp:12) */
+    int32_t width;
+    int32_t height;
+} pto_env;
+
+typedef struct pto_params {
+    int32_t width, height;        /* iResolution                                            */
+    int32_t row_start;            /* first global row (Y, row 0 = top)                     */
+    int32_t row_stride;           /* global row step between consecutive buffer rows       */
+    int32_t nrows;                /* rows in the buffer                                     */
+    uint32_t frame_first;         /* iFrame of the first accumulated frame (>= 1)           */
+    int32_t nframes;              /* frames accumulated in order                            */
+    int32_t num_bounces;          /* c_numBounces                                           */
+    float ambient[3];             /* miss radiance when env == NULL (scalar.cpp:307: 0.1)   */
+    const pto_env* env;           /* NULL => constant ambient                                */
+    int32_t nthreads;             /* host threads (row-cyclic); <= 1 => single thread        */
+} pto_params;
+
+/* Flop accounting (SURVEY.md §8d convention: 1 per fp32 add/sub/mul/div/sqrt/compare executed by
+ * the scalar reference; negation/abs/moves 0; frame- or scene-constant work excluded;
+ * sin/cos/atan2/asin counted separately as transcendentals). */
+typedef struct pto_counts {
+    uint64_t samples;        /* primary samples (pixels x frames)                 */
+    uint64_t segments;       /* TestSceneTrace calls                              */
+    uint64_t flops_sample;   /* camera ray + accumulate, per sample               */
+    uint64_t flops_segment;  /* scene trace + shading, per segment                */
+    uint64_t transcendentals;
+    uint64_t escaped;        /* paths that ended on a miss                        */
+} pto_counts;
+
+/* Render into buf (nrows x width x 3 f32, interleaved RGB, accumulating in place).  0 on success. */
+int pto_render(float* buf, const pto_params* p);
+/* Same, single-threaded, counting work (slower; for deriving the roofline constants). */
+int pto_render_counted(float* buf, const pto_params* p, pto_counts* counts);
+
+/* Known-answer hooks. */
+uint32_t pto_wang_hash(uint32_t* state);                  /* scalar.cpp:27-35  */
+float pto_randomf(uint32_t* state);                        /* scalar.cpp:37-40  */
+void pto_random_unit_vector(uint32_t* state, float out3[3]);/* scalar.cpp:42-50 */
+uint32_t pto_seed(uint32_t x, uint32_t y, uint32_t frame); /* scalar.cpp:332    */
+void pto_env_sample(const pto_env* env, const float dir[3], float out3[3]); /* texture.cpp:101-139 */
+
+#ifdef __cplusplus
+}
+#endif
+#endif

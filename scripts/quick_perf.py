@@ -1,0 +1,25 @@
+"""Quick device timing of the headline workload (1920x1080, 8 spp, 8 bounces); dev tool."""
+import sys, time, json
+from pathlib import Path
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import torch
+from cpuperformanceraytracer_amd.device import render_device, count_device
+W, H, S, B = 1920, 1080, 8, 8
+if len(sys.argv) > 1:
+    W, H, S, B = map(int, sys.argv[1:5])
+buf = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
+cnt = count_device(buf, W, H, frame_first=1, nframes=S, num_bounces=B)
+for i in range(3):
+    render_device(buf, W, H, frame_first=1 + S * (i + 1), nframes=S, num_bounces=B)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+K = 10
+e0.record()
+for i in range(K):
+    render_device(buf, W, H, frame_first=1 + S * (i + 4), nframes=S, num_bounces=B)
+e1.record(); torch.cuda.synchronize()
+ms = e0.elapsed_time(e1) / K
+print(json.dumps({"W": W, "H": H, "spp": S, "B": B, "ms_per_launch": ms,
+                  "primary_samples_per_s": W * H * S / ms * 1e3, "ray_samples_per_s": W * H * S * B / ms * 1e3,
+                  "segments_per_sample": cnt["segments"] / cnt["samples"],
+                  "simd_eff": cnt["segments"] / cnt["lane_slots"], "counts": cnt}))

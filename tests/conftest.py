@@ -1,0 +1,52 @@
+"""Shared fixtures.  `-m gpu` tests need a real MI355X and call the product through its C ABI;
+everything else runs on CPU (oracle vs golden fixtures, host logic, ABI exports, gloo sharding)."""
+from __future__ import annotations
+
+import json
+import lzma
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+GOLDEN = ROOT / "tests" / "golden"
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X, gfx950) and libpt_mi355.so")
+
+
+@pytest.fixture(scope="session")
+def manifest() -> dict:
+    return json.loads((GOLDEN / "manifest.json").read_text())
+
+
+def load_golden(name: str) -> np.ndarray:
+    m = json.loads((GOLDEN / "manifest.json").read_text())["cases"][name]
+    raw = lzma.decompress((GOLDEN / f"{name}.f32.xz").read_bytes())
+    return np.frombuffer(raw, dtype="<f4").reshape(m["height"], m["width"], 3).copy()
+
+
+@pytest.fixture(scope="session")
+def golden():
+    return load_golden
+
+
+def bits_equal(a: np.ndarray, b: np.ndarray) -> bool:
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    return a.shape == b.shape and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def mismatch_report(a: np.ndarray, b: np.ndarray) -> str:
+    a = np.asarray(a, np.float32).reshape(-1, 3)
+    b = np.asarray(b, np.float32).reshape(-1, 3)
+    bad = np.nonzero((a.view(np.uint32) != b.view(np.uint32)).any(1))[0]
+    if len(bad) == 0:
+        return "identical"
+    d = np.abs(a[bad].astype(np.float64) - b[bad]).max(1)
+    return f"{len(bad)} of {len(a)} pixels differ; first {bad[:5].tolist()}, max |d| {d.max():.3g}"

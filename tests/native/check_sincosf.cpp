@@ -1,0 +1,46 @@
+// tests/native/check_sincosf.cpp -- exhaustive host check of the product's pt::sincosf_glibc
+// (cpuperformanceraytracer_amd/csrc/pt_sincosf.h, compiled here for the host) against the host
+// libm sinf/cosf that the oracle and the reference call.  Usage: check_sincosf [lo hi] (floats).
+// Prints "checked N mismatches M" and exits non-zero on any mismatch.
+#include "../../cpuperformanceraytracer_amd/csrc/pt_sincosf.h"
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+int main(int argc, char** argv)
+{
+    float lo = 0.0f, hi = 6.2831855f * 1.0001f;
+    if (argc == 3) { lo = std::strtof(argv[1], nullptr); hi = std::strtof(argv[2], nullptr); }
+    uint32_t u0, u1;
+    std::memcpy(&u0, &lo, 4);
+    std::memcpy(&u1, &hi, 4);
+    unsigned nt = std::thread::hardware_concurrency();
+    if (nt == 0 || nt > 16) nt = 8;
+    std::atomic<uint64_t> bad{0}, cnt{0};
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            uint64_t b = 0, c = 0;
+            for (uint64_t u = (uint64_t)u0 + t; u <= u1; u += nt) {
+                float f, s, co;
+                uint32_t uu = (uint32_t)u;
+                std::memcpy(&f, &uu, 4);
+                pt::sincosf_glibc(f, &s, &co);
+                const float rs = sinf(f), rc = cosf(f);
+                if (std::memcmp(&s, &rs, 4) || std::memcmp(&co, &rc, 4)) {
+                    if (b < 4) std::printf("mismatch %a: sin %a/%a cos %a/%a\n", f, s, rs, co, rc);
+                    ++b;
+                }
+                ++c;
+            }
+            bad += b;
+            cnt += c;
+        });
+    for (auto& x : th) x.join();
+    std::printf("checked %llu mismatches %llu\n", (unsigned long long)cnt.load(), (unsigned long long)bad.load());
+    return bad.load() ? 1 : 0;
+}

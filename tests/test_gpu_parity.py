@@ -1,0 +1,180 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference goldens and the CPU oracle.
+
+Bar: BIT-EXACT.  The kernel performs the reference's f32 operations in the reference's order with
+single rounding, and sin/cos with glibc's algorithm (DESIGN.md "Numerics"), so every pixel must
+equal the reference's scalar path (demofox_path_tracing_scalar.cpp) bit for bit.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import bits_equal, load_golden, mismatch_report
+from layouts import planar8_to_interleaved, tiled_to_interleaved
+from oracle import pyoracle
+
+pytestmark = pytest.mark.gpu
+
+import cpuperformanceraytracer_amd as pt  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def fresh_backend():
+    pt.init(num_bounces=4)
+    yield
+
+
+@pytest.mark.parametrize("name", ["g1_256x256_f1", "g2_256x256_f8", "g3_200x120_f3", "g4_64x64_f32"])
+def test_scalar_matches_reference_goldens(manifest, name):
+    """configs[0] and friends: DemofoxRenderScalar called F times on a zeroed buffer."""
+    c = manifest["cases"][name]
+    buf = np.zeros((c["height"], c["width"], 3), np.float32)
+    for _ in range(c["frames"]):
+        pt.DemofoxRenderScalar(buf, c["width"], c["height"], 3)
+    assert pt.get_frame() == c["frames"]
+    g = load_golden(name)
+    assert bits_equal(buf, g), mismatch_report(buf, g)
+
+
+def test_samples_per_frame_batches_frames(golden):
+    """One call accumulating 8 frames == 8 calls of 1 frame (the in-kernel lerp chain)."""
+    pt.init(num_bounces=4, samples_per_frame=8)
+    buf = np.zeros((256, 256, 3), np.float32)
+    pt.DemofoxRenderScalar(buf, 256, 256, 3)
+    assert pt.get_frame() == 8
+    assert bits_equal(buf, golden("g2_256x256_f8"))
+
+
+def test_deferred_readback(golden):
+    pt.init(num_bounces=4, defer_readback=True)
+    buf = np.zeros((256, 256, 3), np.float32)
+    for _ in range(8):
+        pt.DemofoxRenderScalar(buf, 256, 256, 3)
+    assert not buf.any()          # nothing copied back yet
+    pt.readback(buf)
+    assert bits_equal(buf, golden("g2_256x256_f8"))
+
+
+@pytest.mark.parametrize("w,h,frames", [(1920, 1080, 1), (1920, 1080, 8), (333, 97, 5)])
+def test_eight_bounces_vs_oracle(w, h, frames):
+    """configs[1] shape (1920x1080, 8 bounces, 8 spp) at full size against the CPU oracle."""
+    pt.init(num_bounces=8, samples_per_frame=frames)
+    buf = np.zeros((h, w, 3), np.float32)
+    pt.DemofoxRenderScalar(buf, w, h, 3)
+    ref = pyoracle.render(w, h, nframes=frames, num_bounces=8)
+    assert bits_equal(buf, ref), mismatch_report(buf, ref)
+
+
+def test_large_frame_index_vs_oracle():
+    """Progressive accumulation deep into a run: frames 1000001..1000003 on a prior image."""
+    pt.init(num_bounces=8)
+    w, h = 160, 96
+    start = pyoracle.render(w, h, frame_first=1, nframes=2, num_bounces=8)
+    buf = start.copy()
+    pt.set_frame(1_000_000)
+    for _ in range(3):
+        pt.DemofoxRenderScalar(buf, w, h, 3)
+    ref = pyoracle.render(w, h, frame_first=1_000_001, nframes=3, num_bounces=8, buf=start.copy())
+    assert bits_equal(buf, ref), mismatch_report(buf, ref)
+
+
+def test_simd_layout_planar8():
+    w, h = 256, 128
+    buf = np.zeros(w * h * 3, np.float32)
+    for _ in range(2):
+        pt.DemofoxRenderSimd(buf, w, h, 3)
+    ref = pyoracle.render(w, h, nframes=2, num_bounces=4)
+    img = planar8_to_interleaved(buf, w, h)
+    assert bits_equal(img, ref), mismatch_report(img, ref)
+
+
+def test_simd_tiled_layout():
+    w, h, ntx, nty = 320, 240, 4, 5
+    tw, th = w // ntx, h // nty
+    buf = np.zeros(w * h * 3, np.float32)
+    for _ in range(2):
+        pt.DemofoxRenderSimdTiled(buf, w, h, ntx, nty, tw, th, 3)
+    ref = pyoracle.render(w, h, nframes=2, num_bounces=4)
+    img = tiled_to_interleaved(buf, w, h, tw, th)
+    assert bits_equal(img, ref), mismatch_report(img, ref)
+
+
+def test_render_tile_fanout_matches_tiled():
+    """The host fans RenderTile calls out itself (simt_pooled / v4 pattern)."""
+    w, h, ntx, nty = 320, 240, 10, 15
+    buf = np.zeros(w * h * 3, np.float32)
+    tiles = pt.make_tiles(w, h, ntx, nty)
+    info = pt.RenderBufferInfo(buf, w, h, 3)
+    for _ in range(2):
+        pt.BeginFrame()
+        for t in reversed(tiles):               # order must not matter
+            pt.RenderTile(info, t)
+    ref = pyoracle.render(w, h, nframes=2, num_bounces=4)
+    img = tiled_to_interleaved(buf, w, h, w // ntx, h // nty)
+    assert bits_equal(img, ref), mismatch_report(img, ref)
+
+
+def test_invalid_settings_raise():
+    from cpuperformanceraytracer_amd._native import PtError
+    buf = np.zeros(100 * 64 * 3, np.float32)
+    with pytest.raises(PtError):
+        pt.DemofoxRenderSimd(buf, 100, 64, 3)          # width % 8 != 0
+    pt.DemofoxRenderSimdTiled(buf, 96, 64, 3, 4, 32, 16, 3)       # valid: 3 x 32 by 4 x 16
+    with pytest.raises(PtError):
+        pt.DemofoxRenderSimdTiled(buf, 96, 64, 2, 4, 48, 16, 3 + 1)  # NumChannels 4
+    with pytest.raises(PtError):
+        pt.DemofoxRenderSimdTiled(buf, 88, 64, 2, 4, 44, 16, 3)     # tile width 44 % 8 != 0
+    with pytest.raises(PtError):
+        pt.DemofoxRenderSimdTiled(buf, 96, 64, 5, 4, 16, 16, 3)     # 96 % 5 != 0
+    with pytest.raises(PtError):
+        pt.DemofoxRenderScalar(buf, 8, 8, 4)            # NumChannels must be 3
+    with pytest.raises(PtError):
+        pt.DemofoxRenderScalar(np.zeros(10, np.float64), 2, 2, 3)
+
+
+def test_empty_and_single_pixel():
+    buf = np.zeros((1, 1, 3), np.float32)
+    pt.DemofoxRenderScalar(buf, 1, 1, 3)
+    ref = pyoracle.render(1, 1, nframes=1, num_bounces=4)
+    assert bits_equal(buf, ref)
+
+
+# ---------------------------------------------------------------- device-resident path -------
+torch = pytest.importorskip("torch")
+
+
+def _dev_render(w, h, frames, bounces, **kw):
+    from cpuperformanceraytracer_amd.device import render_device
+    nrows = kw.get("nrows", h)
+    buf = torch.zeros(nrows * w * 3, dtype=torch.float32, device="cuda")
+    render_device(buf, w, h, frame_first=kw.pop("frame_first", 1), nframes=frames, num_bounces=bounces, **kw)
+    torch.cuda.synchronize()
+    return buf.cpu().numpy().reshape(nrows, w, 3)
+
+
+def test_device_row_shards_equal_full_image():
+    """Row-interleaved shards (the multi-GPU partition) reproduce the full image bit for bit."""
+    w, h, f, b = 640, 360, 4, 8
+    full = _dev_render(w, h, f, b)
+    ref = pyoracle.render(w, h, nframes=f, num_bounces=b)
+    assert bits_equal(full, ref), mismatch_report(full, ref)
+    G = 3
+    rebuilt = np.zeros_like(full)
+    for r in range(G):
+        n = len(range(r, h, G))
+        rebuilt[r::G] = _dev_render(w, h, f, b, row_start=r, row_stride=G, nrows=n)
+    assert bits_equal(rebuilt, full)
+
+
+def test_device_counts_match_oracle_counts():
+    """Device-counted traced segments == the oracle's (identical paths => identical counts)."""
+    from cpuperformanceraytracer_amd.device import count_device
+    w, h, f, b = 256, 256, 2, 8
+    buf = torch.zeros(h * w * 3, dtype=torch.float32, device="cuda")
+    cnt = count_device(buf, w, h, frame_first=1, nframes=f, num_bounces=b)
+    img, oc = pyoracle.render_counted(w, h, nframes=f, num_bounces=b)
+    assert bits_equal(buf.cpu().numpy().reshape(h, w, 3), img)
+    assert cnt["samples"] == oc["samples"] == w * h * f
+    assert cnt["segments"] == oc["segments"]
+    assert cnt["escaped"] == oc["escaped"]
+    assert cnt["lane_slots"] >= cnt["segments"]
