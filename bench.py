@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X path-tracing hot path (BASELINE.json metric and configs).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+         --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (configs[1]): 1920x1080, 8 spp, 8 bounces, the demofox quad+sphere scene,
+diffuse+emissive.  One STEP = one launch that accumulates 8 more frames (8 spp) into the
+HBM-resident f32 accumulator of every pixel -- bit-identical to 8 calls of the reference's
+DemofoxRenderScalar.  Frames advance step to step like the reference's progressive render.
+
+N > 1 (weak scaling): every rank renders its own 1920x1080 worth of rows of a 1920 x (1080*N)
+image (rows interleaved, shard.py); after the K steps the sub-images are gathered to rank 0 over
+RCCL (the job's only exchange, inside the timed region, also reported separately).
+
+Printed (rank 0, one JSON line): the BASELINE metric (ray-samples/s = pixels x spp x bounces / s),
+ms per step, a roofline object for the render kernel (algorithmic FP32 FLOP/s against the 157.3
+TFLOP/s FP32 vector peak; HBM traffic from the committed rocprofv3 PMC pass), and the CPU baseline
+(the oracle's C restatement of the reference scalar path on this host's cores, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "ray-samples/sec (pixels×spp×bounces) at 1920×1080; ms/frame"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2_1080p")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=8, help="frames of the CPU baseline sample")
+    return ap.parse_args()
+
+
+def cpu_baseline(wl, frames: int) -> dict:
+    """The oracle (C restatement of demofox_path_tracing_scalar.cpp, bit-identical to it) timed on
+    this host's cores on a bounded sample of the same workload; plus the reference's own scalar
+    build (oracle/_ref, c_numBounces=4 compiled in) single-threaded for calibration."""
+    from oracle import pyoracle
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    cores = max(1, min(16, ncpu))
+    pyoracle.render(64, 64, nframes=1, num_bounces=wl.num_bounces, nthreads=cores)   # warm
+    t0 = time.perf_counter()
+    pyoracle.render(wl.width, wl.height, frame_first=1, nframes=frames, num_bounces=wl.num_bounces, nthreads=cores)
+    dt = time.perf_counter() - t0
+    samples = wl.width * wl.height * frames
+    out = {"value": samples * wl.num_bounces / dt, "unit": "ray-samples/s", "cores": cores, "kind": "port",
+           "sample": f"{wl.width}x{wl.height}, {frames} frames (spp), {wl.num_bounces} bounces, "
+                     f"oracle/pt_oracle.c (gcc -O2, {cores} threads, row-cyclic); {dt:.2f} s wall",
+           "primary_samples_per_s": samples / dt, "host_cpus_visible": ncpu,
+           "cpu_model": _cpu_model()}
+    ref = ROOT / "oracle" / "_ref" / "libref_scalar.so"
+    if ref.exists():
+        import ctypes
+        import numpy as np
+        L = ctypes.CDLL(str(ref))
+        L.ref_render_scalar.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        w, h = 640, 360
+        buf = np.zeros((h, w, 3), np.float32)
+        t0 = time.perf_counter()
+        L.ref_render_scalar(buf.ctypes.data, w, h, 1)
+        dt = time.perf_counter() - t0
+        out["reference_scalar"] = {"primary_samples_per_s": w * h / dt, "ray_samples_per_s": w * h * 4 / dt,
+                                   "cores": 1, "sample": f"{w}x{h}, 1 frame, 4 bounces (compiled-in "
+                                   "c_numBounces), DemofoxRenderScalar built unmodified by oracle/build_ref.sh"}
+    return out
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def load_traffic(kernel_substr: str = "pt_render_kernel"):
+    """Per-launch HBM bytes of the render kernel from the committed rocprofv3 PMC summary."""
+    p = ROOT / "profiles" / "pmc_summary.json"
+    if not p.exists():
+        return None, None
+    d = json.loads(p.read_text())
+    return d.get("hbm_bytes_per_launch"), d.get("source")
+
+
+def main() -> None:
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from cpuperformanceraytracer_amd import roofline as RL
+    from cpuperformanceraytracer_amd.config import CONFIGS
+    from cpuperformanceraytracer_amd.device import count_device, ensure_backend, render_device
+    from cpuperformanceraytracer_amd.shard import gather_rows, max_rows, rows_of
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            sys.exit("run N>1 under torch.distributed.run (one process per GPU)")
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+    wl = CONFIGS[args.workload]
+    W, H, S, B = wl.width, wl.height, wl.spp, wl.num_bounces
+    Hg = H * world                                   # weak scaling: H rows per rank
+    row_start, row_stride, nrows = rows_of(rank, world, Hg)
+    mr = max_rows(world, Hg)
+    ensure_backend(dev.index, B)
+
+    buf = torch.zeros(mr * W * 3, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    frame = 1
+
+    def step(f):
+        render_device(buf, W, Hg, frame_first=f, nframes=S, num_bounces=B, row_start=row_start,
+                      row_stride=row_stride, nrows=nrows, stream=stream)
+
+    for _ in range(args.warmup):
+        step(frame)
+        frame += S
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    timed_first = frame
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev[k][0].record(stream)
+        step(frame)
+        ev[k][1].record(stream)
+        frame += S
+    gather_ms = 0.0
+    if world > 1:
+        g0 = torch.cuda.Event(enable_timing=True)
+        g1 = torch.cuda.Event(enable_timing=True)
+        g0.record(stream)
+        full = gather_rows(buf, W, Hg, rank, world)
+        g1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = [a.elapsed_time(b) for a, b in ev]
+    if world > 1:
+        gather_ms = g0.elapsed_time(g1)
+        t = torch.tensor([elapsed, gather_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, gather_ms = float(t[0]), float(t[1])
+        if rank == 0:
+            assert full is not None and full.shape == (Hg, W, 3)
+
+    # Exact work of the timed launches (deterministic: same frames, counted on a scratch buffer).
+    scratch = torch.zeros_like(buf)
+    segs = samples = slots = 0
+    for k in range(K):
+        c = count_device(scratch, W, Hg, frame_first=timed_first + k * S, nframes=S, num_bounces=B,
+                         row_start=row_start, row_stride=row_stride, nrows=nrows, stream=stream)
+        segs += c["segments"]
+        samples += c["samples"]
+        slots += c["lane_slots"]
+    del scratch
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    ms_step = elapsed * 1e3 / K
+    total_ray_samples = W * H * S * B * K * world
+    value = total_ray_samples / elapsed
+    avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
+    flops_launch = RL.launch_flops(segs, samples) / K
+    achieved_tf = flops_launch / avg_kernel_s / 1e12
+    hbm_launch, traffic_src = load_traffic()
+    res = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "ray-samples/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (the reference's fixed demofox quad+sphere scene; no dataset)",
+        "config": {"workload": wl.name, "width": W, "height": H, "spp": S, "bounces": B,
+                   "image_rows_total": Hg, "parallelism": f"rows interleaved x{world}" if world > 1 else "single GPU",
+                   "step": f"one launch accumulating {S} frames (spp) of every pixel in HBM"},
+        "primary_samples_per_s": W * H * S * K * world / elapsed,
+        "ms_per_frame_8spp": ms_step,
+        "traced_segments_per_s": segs * world / (avg_kernel_s * K),
+        "segments_per_sample": segs / samples,
+        "simd_lane_efficiency": segs / slots if slots else None,
+        "kernel_ms_avg": avg_kernel_s * 1e3,
+        "kernel_ms_min": min(kernel_ms),
+        "roofline": {
+            "bound": "valu",
+            "achieved": achieved_tf,
+            "peak": RL.PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved_tf / RL.PEAK_FP32_TFLOPS,
+            "traffic": hbm_launch,
+            "kernel": "pt_render_kernel<INTERLEAVED>",
+            "flops_per_launch": flops_launch,
+            "flop_model": f"segments x {RL.F_SEGMENT} + samples x {RL.F_SAMPLE} (roofline.py)",
+            "algorithmic_bytes_per_launch": RL.BYTES_PER_PIXEL_PER_LAUNCH * W * H,
+            "hbm_achieved_gbps": RL.BYTES_PER_PIXEL_PER_LAUNCH * W * H / avg_kernel_s / 1e9,
+            "hbm_peak_gbps": RL.PEAK_HBM_GBPS,
+            "traffic_source": traffic_src,
+        },
+    }
+    if world > 1:
+        res["gather_ms"] = gather_ms
+    if world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(wl, args.cpu_frames)
+    print(json.dumps(res))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

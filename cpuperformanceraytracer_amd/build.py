@@ -24,7 +24,7 @@ LIB = PKG / "libpt_mi355.so"
 ARCH = os.environ.get("PT_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["pt_kernel.hip", "pt_scene.cpp", "pt_capi.cpp", "pt_dropin.cpp"]
-HEADERS = ["pt_kernel.h", "pt_scene.h", "pt_sincosf.h"]
+HEADERS = ["pt_kernel.h", "pt_scene.h", "pt_sincosf.h", "pt_exactmath.h"]
 PARITY_FLAGS = [
     "-ffp-contract=off",
     "-fhip-fp32-correctly-rounded-divide-sqrt",

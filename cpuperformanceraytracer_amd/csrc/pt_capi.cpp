@@ -20,6 +20,7 @@ struct State {
     pt_config cfg{};
     hipStream_t stream = nullptr;
     PtScene scene{};
+    PtScene* dscene = nullptr;          // device copy of `scene`
     uint32_t frame = 0;                 // value of the reference's static iFrame
     // device mirror of the caller's host accumulator (host-buffer entry points)
     float* dbuf = nullptr;
@@ -128,12 +129,13 @@ PtJob base_job(float* buf, int32_t w, int32_t h)
     j.env = nullptr;
     j.env_w = j.env_h = 0;
     j.counters = nullptr;
+    j.scene = g.dscene;
     return j;
 }
 
 int launch(const PtJob& j, hipStream_t st, bool count)
 {
-    hipError_t e = pt_launch_render(j, g.scene, st, count);
+    hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
     return PT_OK;
 }
@@ -180,6 +182,8 @@ int pt_init(const pt_config* cfg)
         return fail(PT_ENOMEM, "hipMalloc(counters) failed");
     g.cfg = c;
     pt_build_demofox_scene(&g.scene, c.ambient);
+    if (hipMalloc(&g.dscene, sizeof(PtScene)) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc(scene) failed");
+    HIP_TRY(hipMemcpy(g.dscene, &g.scene, sizeof(PtScene), hipMemcpyHostToDevice));
     g.frame = 0;
     g.inited = true;
     return PT_OK;
@@ -192,6 +196,7 @@ void pt_shutdown(void)
     if (g.stream) (void)hipStreamSynchronize(g.stream);
     if (g.dbuf) (void)hipFree(g.dbuf);
     if (g.dcounters) (void)hipFree(g.dcounters);
+    if (g.dscene) (void)hipFree(g.dscene);
     if (g.stream) (void)hipStreamDestroy(g.stream);
     g = State{};
 }

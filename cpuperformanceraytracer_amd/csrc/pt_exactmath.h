@@ -1,0 +1,58 @@
+// pt_exactmath.h -- correctly rounded f32 reciprocal / division / square root in fewer VALU
+// instructions than the compiler's general IEEE expansions, for the operand ranges the path
+// tracer produces.  Bit-identical to IEEE '/' and sqrtf wherever they are used (proofs and
+// exhaustive GPU checks: tests/native/exactmath_probe.hip, tests/test_gpu_exactmath.py).
+//
+// Why: on gfx950 the compiler's correctly rounded f32 division costs ~17 v_add-equivalents of
+// issue time and sqrtf ~23 (scripts/valu_microbench.hip), because they handle every
+// input class (denormals via scaling, inf/nan fix-ups).  The path tracer's divisors and radicands
+// are normal numbers in a known range, and outside it only the SIGN or ORDER of the result
+// matters to the reference (it is compared against 0.01 / the running best and discarded), so a
+// guarded fast path keeps bit-exactness where the value is used.
+#pragma once
+#include <stdint.h>
+
+namespace pt {
+
+__device__ __forceinline__ float rcp_approx(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float sqrt_approx(float x) { return __builtin_amdgcn_sqrtf(x); }
+
+// RN(1/x) for |x| in [2^-125, 2^125]: hardware reciprocal (<= 1 ulp) + one Newton-Raphson step
+// with exact-residual FMA.  Outside that range callers must not rely on the value.
+__device__ __forceinline__ float rcp_rn(float x)
+{
+    float r = rcp_approx(x);
+    const float e = __builtin_fmaf(-x, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    return r;
+}
+
+// RN(a/b) given y = RN(1/b) (Markstein: with y the correctly rounded reciprocal and a faithful
+// first quotient, the exact-remainder correction yields the correctly rounded quotient).  Two
+// corrections: the first makes the quotient faithful, the second rounds it correctly.  Valid when
+// b, a and a/b are normal and no intermediate overflows.
+__device__ __forceinline__ float div_rn(float a, float b, float y)
+{
+    float q = a * y;
+    float r = __builtin_fmaf(-q, b, a);
+    q = __builtin_fmaf(r, y, q);
+    r = __builtin_fmaf(-q, b, a);
+    return __builtin_fmaf(r, y, q);
+}
+
+// RN(sqrt(x)) for normal x >= 2^-100: hardware square root then a neighbour check with exact
+// FMA residuals (a correctly rounded root s satisfies (s - ulp/2)^2 < x < (s + ulp/2)^2).
+__device__ __forceinline__ float sqrt_rn(float x)
+{
+    const float s = sqrt_approx(x);
+    const float s_dn = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, s) - 1u);
+    const float s_up = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, s) + 1u);
+    const float r_dn = __builtin_fmaf(-s_dn, s, x);   // x - s_dn*s  (> 0 iff x > s_dn*s)
+    const float r_up = __builtin_fmaf(-s_up, s, x);   // x - s_up*s
+    float res = s;
+    res = (r_dn <= 0.0f) ? s_dn : res;
+    res = (r_up > 0.0f) ? s_up : res;
+    return res;
+}
+
+}  // namespace pt

@@ -22,6 +22,7 @@ enum PtCounter : int {
 
 struct PtJob {
     float* buf;                 // device accumulator (layout below)
+    const PtScene* scene;       // device scene table (pt_scene.h)
     int32_t width, height;      // iResolution (full image)
     int32_t col0, ncols;        // pixel columns [col0, col0 + ncols)
     int32_t row_start;          // first global row Y (row 0 = top of image)
@@ -38,4 +39,4 @@ struct PtJob {
 };
 
 // Enqueue one render launch on `stream`.  Returns hipSuccess or the launch error.
-hipError_t pt_launch_render(const PtJob& job, const PtScene& scene, hipStream_t stream, bool count);
+hipError_t pt_launch_render(const PtJob& job, hipStream_t stream, bool count);

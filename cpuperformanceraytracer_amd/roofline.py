@@ -1,0 +1,33 @@
+"""Roofline constants for the path-tracing kernel (DESIGN.md "Roofline").
+
+Algorithmic work is counted the way SURVEY.md §8d defines it: 1 FLOP per fp32 add, sub, mul,
+div, sqrt or compare that the reference's SCALAR path executes (demofox_path_tracing_scalar.cpp),
+negation/abs/moves 0, scene- and frame-constant work excluded (vertex translation, quad normals,
+camera distance, aspect ratio, 1/(iFrame+1)), sin/cos counted separately as transcendentals.
+
+The per-segment figure depends on which early exits of TestQuadTrace/TestSphereTrace a ray takes,
+so it is an average measured by the instrumented CPU restatement over a sample of the benchmark
+workload (tests/test_flops.py re-derives it and checks these constants).  The number of traced
+segments itself is counted exactly on the device for every benchmarked launch
+(pt_count_device), so   FLOP/launch = segments * F_SEGMENT + samples * F_SAMPLE.
+"""
+
+# Mean fp32 FLOP per traced segment (one TestSceneTrace + shading), 1920x1080, 8 bounces,
+# rows 0::8 and 3::8, frames 1-2 (426.85 / 426.64); 3840x2160 rows 5::16 gives 426.68.
+F_SEGMENT = 426.8
+# FLOP per primary sample: camera ray (20) + the c_numRendersPerFrame=1 scale/add (6) +
+# the progressive lerp (9) = 35, exact (no data dependence).
+F_SAMPLE = 35.0
+# Transcendentals (cosf + sinf) per traced segment: 2 per bounce that continues.
+T_SEGMENT = 1.14
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters").
+PEAK_FP32_TFLOPS = 157.3   # FP32 vector (= FP32 MFMA) peak, FMA counted as 2
+PEAK_HBM_GBPS = 8000.0     # HBM3E spec peak (6.29 TB/s measured copy)
+
+# Algorithmic HBM bytes: the accumulator is read once and written once per launch.
+BYTES_PER_PIXEL_PER_LAUNCH = 24
+
+
+def launch_flops(segments: int, samples: int) -> float:
+    return segments * F_SEGMENT + samples * F_SAMPLE

@@ -18,6 +18,7 @@ int main(int argc, char** argv)
     uint32_t u0, u1;
     std::memcpy(&u0, &lo, 4);
     std::memcpy(&u1, &hi, 4);
+    if (u0 > u1) { uint32_t t = u0; u0 = u1; u1 = t; }   // negative ranges: bit order reverses
     unsigned nt = std::thread::hardware_concurrency();
     if (nt == 0 || nt > 16) nt = 8;
     std::atomic<uint64_t> bad{0}, cnt{0};

@@ -1,0 +1,26 @@
+"""Re-derive the roofline constants (cpuperformanceraytracer_amd/roofline.py) with the instrumented
+oracle and check the committed values: F_SAMPLE exactly, F_SEGMENT within 0.5 % on samples of the
+benchmark workload (the per-segment count depends on which early exits rays take)."""
+from __future__ import annotations
+
+import pytest
+
+from cpuperformanceraytracer_amd import roofline as RL
+from oracle import pyoracle
+
+
+@pytest.mark.parametrize("w,h,rs,st,nr,frames", [(1920, 1080, 0, 8, 135, 1), (1920, 1080, 3, 8, 135, 2),
+                                                  (3840, 2160, 5, 16, 135, 1)])
+def test_flop_constants(w, h, rs, st, nr, frames):
+    _, c = pyoracle.render_counted(w, h, row_start=rs, row_stride=st, nrows=nr, nframes=frames, num_bounces=8)
+    assert c["samples"] == w * nr * frames
+    assert c["flops_sample"] == RL.F_SAMPLE * c["samples"]
+    f_seg = c["flops_segment"] / c["segments"]
+    assert abs(f_seg - RL.F_SEGMENT) / RL.F_SEGMENT < 0.005, f_seg
+    assert abs(c["transcendentals"] / c["segments"] - RL.T_SEGMENT) < 0.02
+
+
+def test_counted_render_equals_plain_render():
+    img, _ = pyoracle.render_counted(64, 48, nframes=2, num_bounces=8)
+    ref = pyoracle.render(64, 48, nframes=2, num_bounces=8)
+    assert (img.view("u4") == ref.view("u4")).all()

@@ -1,0 +1,99 @@
+"""The oracle (oracle/pt_oracle.c) is pinned to the reference before it is trusted as a checker.
+
+  * bit-identical to the golden fixtures, which the reference's own scalar code produced
+    (tests/golden/make_golden.py via oracle/build_ref.sh);
+  * the reference's Wang-hash known answers;
+  * when the reference is present (this container), bit-identical to a live run of it;
+  * its generalisations (row shards, frame offsets, multi-frame batches, bounce count) reduce to
+    the reference's call pattern.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import bits_equal, load_golden, mismatch_report
+from oracle import pyoracle
+
+
+@pytest.mark.parametrize("name", ["g1_256x256_f1", "g2_256x256_f8", "g3_200x120_f3", "g4_64x64_f32"])
+def test_oracle_matches_reference_golden(manifest, name):
+    c = manifest["cases"][name]
+    img = pyoracle.render(c["width"], c["height"], frame_first=c["frame_first"], nframes=c["frames"],
+                          num_bounces=c["num_bounces"])
+    g = load_golden(name)
+    assert bits_equal(img, g), mismatch_report(img, g)
+
+
+def test_golden_integrity(manifest):
+    import hashlib
+    for name, c in manifest["cases"].items():
+        g = load_golden(name)
+        assert hashlib.sha256(g.astype("<f4").tobytes()).hexdigest() == c["sha256"], name
+        assert np.isfinite(g).all()
+
+
+def test_golden_known_pixels():
+    """SURVEY.md §8c sample pixels of G1 (row, col): (0,0) is the 1/2-weighted ambient 0.05."""
+    g = load_golden("g1_256x256_f1")
+    assert np.all(g[0, 0] == np.float32(0.05))
+    assert g.max() <= 10.05 + 1e-6
+
+
+def test_wang_hash_kats(manifest):
+    for seed, seq in manifest["kat_wang_hash"].items():
+        assert pyoracle.wang_hash_sequence(int(seed), len(seq)) == seq
+
+
+def test_seed_formula(manifest):
+    k = manifest["kat_seed"]
+    assert pyoracle.seed(k["x"], k["y"], k["frame"]) == k["seed"]
+    # wrapping u32 arithmetic at large coordinates / frames
+    assert pyoracle.seed(7679, 4319, 16_000_000) == ((7679 * 1973 + 4319 * 9277 + 16_000_000 * 26699) & 0xFFFFFFFF) | 1
+
+
+def test_random_unit_vectors_are_unit():
+    v = pyoracle.random_unit_vector(12345, 1000).astype(np.float64)
+    assert np.allclose(np.linalg.norm(v, axis=1), 1.0, atol=1e-6)
+
+
+@pytest.mark.skipif(not pyoracle.ref_available(), reason="reference build (oracle/_ref) not present")
+@pytest.mark.parametrize("w,h,frames", [(96, 64, 2), (17, 33, 3)])
+def test_oracle_matches_live_reference(tmp_path, w, h, frames):
+    ref = pyoracle.ref_render(w, h, frames, tmp_path)
+    img = pyoracle.render(w, h, nframes=frames, num_bounces=4)
+    assert bits_equal(img, ref), mismatch_report(img, ref)
+
+
+def test_row_shards_are_bit_identical_to_full_image():
+    w, h, f, b = 120, 77, 2, 8
+    full = pyoracle.render(w, h, nframes=f, num_bounces=b)
+    for G in (2, 3, 8):
+        for r in range(G):
+            n = len(range(r, h, G))
+            part = pyoracle.render(w, h, nframes=f, num_bounces=b, row_start=r, row_stride=G, nrows=n)
+            assert bits_equal(part, full[r::G])
+
+
+def test_frame_batches_compose():
+    """frames 1..5 in one call == 1..2 then 3..5 on the same buffer (the lerp chain)."""
+    w, h = 64, 40
+    one = pyoracle.render(w, h, frame_first=1, nframes=5, num_bounces=8)
+    two = pyoracle.render(w, h, frame_first=1, nframes=2, num_bounces=8)
+    two = pyoracle.render(w, h, frame_first=3, nframes=3, num_bounces=8, buf=two)
+    assert bits_equal(one, two)
+
+
+def test_thread_count_does_not_change_result():
+    a = pyoracle.render(100, 60, nframes=2, num_bounces=8, nthreads=1)
+    b = pyoracle.render(100, 60, nframes=2, num_bounces=8, nthreads=7)
+    assert bits_equal(a, b)
+
+
+def test_zero_bounces_and_empty():
+    img = pyoracle.render(32, 16, nframes=1, num_bounces=0)
+    assert np.isfinite(img).all()
+    empty = pyoracle.render(32, 16, nframes=0, num_bounces=4)
+    assert not empty.any()
+    with pytest.raises(ValueError):
+        pyoracle.render(32, 16, frame_first=0)
