@@ -29,6 +29,8 @@ struct State {
     size_t mirror_bytes = 0;
     bool mirror_valid = false;          // deferred mode: device copy is authoritative
     unsigned long long* dcounters = nullptr;
+    unsigned int* dqueue = nullptr;     // ring of kQueueSlots tile-queue counters
+    unsigned queue_next = 0;
 };
 
 State g;
@@ -50,6 +52,7 @@ int fail(int code, const char* fmt, ...)
     } while (0)
 
 constexpr uint32_t kMaxFrame = 1u << 24;   // iFrame is an f32 counter: exact below 2^24
+constexpr unsigned kQueueSlots = 256;      // launches in flight that may share the ring
 
 int ensure_init()
 {
@@ -133,8 +136,9 @@ PtJob base_job(float* buf, int32_t w, int32_t h)
     return j;
 }
 
-int launch(const PtJob& j, hipStream_t st, bool count)
+int launch(PtJob j, hipStream_t st, bool count)
 {
+    j.queue = g.dqueue + (g.queue_next++ % kQueueSlots);
     hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
     return PT_OK;
@@ -180,6 +184,8 @@ int pt_init(const pt_config* cfg)
     HIP_TRY(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
     if (hipMalloc(&g.dcounters, PT_CNT_N * sizeof(unsigned long long)) != hipSuccess)
         return fail(PT_ENOMEM, "hipMalloc(counters) failed");
+    if (hipMalloc(&g.dqueue, kQueueSlots * sizeof(unsigned)) != hipSuccess)
+        return fail(PT_ENOMEM, "hipMalloc(queue) failed");
     g.cfg = c;
     pt_build_demofox_scene(&g.scene, c.ambient);
     if (hipMalloc(&g.dscene, sizeof(PtScene)) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc(scene) failed");
@@ -197,6 +203,7 @@ void pt_shutdown(void)
     if (g.dbuf) (void)hipFree(g.dbuf);
     if (g.dcounters) (void)hipFree(g.dcounters);
     if (g.dscene) (void)hipFree(g.dscene);
+    if (g.dqueue) (void)hipFree(g.dqueue);
     if (g.stream) (void)hipStreamDestroy(g.stream);
     g = State{};
 }
@@ -362,6 +369,7 @@ int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
     out->lane_slots = h[PT_CNT_LANE_SLOTS];
     out->samples = h[PT_CNT_SAMPLES];
     out->escaped = h[PT_CNT_ESCAPED];
+    out->primary = h[PT_CNT_PRIMARY];
     return PT_OK;
 }
 

@@ -17,7 +17,8 @@ enum PtCounter : int {
     PT_CNT_LANE_SLOTS = 1,   // 64 x trace-loop iterations over all waves (issued lane-slots)
     PT_CNT_SAMPLES = 2,      // primary samples finished
     PT_CNT_ESCAPED = 3,      // paths that ended on a miss
-    PT_CNT_N = 4,
+    PT_CNT_PRIMARY = 4,      // camera-ray segments traced (one per pixel)
+    PT_CNT_N = 5,
 };
 
 struct PtJob {
@@ -36,6 +37,7 @@ struct PtJob {
     const float* env;           // device env map (H x W x 3), nullptr => ambient
     int32_t env_w, env_h;
     unsigned long long* counters;  // PT_CNT_N u64, COUNT build only
+    unsigned int* queue;           // tile-queue counter (zeroed on the stream before each launch)
 };
 
 // Enqueue one render launch on `stream`.  Returns hipSuccess or the launch error.

@@ -10,18 +10,21 @@
 //   RenderTile           demofox_path_tracing_simd_tiled.cpp:489-535 (tile surface/layout)
 //
 // Design (DESIGN.md has the numbers):
-//   * one lane = one pixel; the lane renders the launch's nframes samples of that pixel IN FRAME
-//     ORDER and applies the reference's progressive lerp after each, so a launch of S frames is
-//     bit-identical to S calls of DemofoxRenderScalar.  The accumulator is read once and written
-//     once per launch.
-//   * path regeneration: the bounce loop and the sample loop are flattened into one loop of
-//     "segments" (one TestSceneTrace each).  A lane whose path ends (miss, or bounce budget spent)
-//     finishes that sample and starts its next one in the same iteration, so a wave keeps all 64
-//     lanes tracing until its lanes run out of samples; the loop exits when no lane has work
-//     (exec mask empty == wave-wide __any() false; the COUNT build makes the ballot explicit).
-//   * scene geometry is wave-uniform -> scalar loads (SGPR operands) from a device scene table,
-//     re-read every segment rather than pinned in SGPRs (no SGPR spilling); per-lane closest-hit
-//     material / normal lookups and the per-axis vertex components -> LDS tables.
+//   * a lane renders a pixel's nframes samples IN FRAME ORDER and applies the reference's
+//     progressive lerp after each, so a launch of S frames is bit-identical to S calls of
+//     DemofoxRenderScalar.  The accumulator is read once and written once per launch.
+//   * the camera ray and its first TestSceneTrace + bounce-0 shading are the same for every frame
+//     of a pixel (no jitter; the RNG is first drawn after them), so they run once per pixel and
+//     every sample starts at bounce 1 from the saved state (PixelHit, LDS).
+//   * persistent waves + path regeneration: the bounce, sample and pixel loops are flattened into
+//     one loop of "segments" (one TestSceneTrace each).  A lane whose sample ends starts its next
+//     sample, and a lane whose pixel ends takes the next pixel of the wave's 8x8 tile (ballot +
+//     mbcnt), tiles coming from a per-launch atomic queue.  All 64 lanes trace every iteration
+//     until the queue drains; the loop exits when __any(has_pixel) is false.
+//   * scene geometry is compile-time constant, as in the reference's TestSceneTrace: vertex
+//     coordinates are instruction literals (no loads, no registers, nothing to spill);
+//     per-lane closest-hit material / normal lookups and the per-axis vertex components (indexed
+//     by each lane's own ray) -> LDS tables.
 //   * TestQuadTrace's vertex re-ordering (flip) and triangle choice become VGPR selects of the
 //     ray-relative vertex vectors; only the intersection component the distance divides by is
 //     evaluated (the reference computes all three and uses one).
@@ -33,6 +36,11 @@
 #include "pt_exactmath.h"
 #include "pt_sincosf.h"
 #include <math.h>
+#include <algorithm>
+
+#ifndef PT_TRACE_UNROLL
+#define PT_TRACE_UNROLL 6   // primitive loops fully unrolled: the constexpr geometry becomes
+#endif                      // instruction literals (rolled: 1.05 ms vs 0.81 ms per 1080p step)
 
 namespace {
 
@@ -107,17 +115,17 @@ struct AxisRow {
 // TestQuadTrace, scalar.cpp:65-143.  `pq` = (rayPos + rayDir) - rayPos (ray-constant, hoisted),
 // `axis`/`dP`/`dD`/`yD` = the component :121-133 divides by, its ray origin, direction, RN(1/dir).
 // On a closer hit: best = dist, id = q, flag = flipped.
-__device__ __forceinline__ void quad_test(const PtScene* __restrict__ sc, const AxisRow* s_axis, int q, V3 P, V3 D,
-                                          V3 pq, int axis, float dP, float dD, float yD, float& best, int& id,
-                                          int& flag)
+template <class SC>
+__device__ __forceinline__ void quad_test(const AxisRow* s_axis, int q, V3 P, V3 D, V3 pq, int axis, float dP,
+                                          float dD, float yD, float& best, int& id, int& flag)
 {
     const AxisRow ax = s_axis[q * 3 + axis];                  // LDS, issued early
-    const V3 n = v3(sc->qn[q][0], sc->qn[q][1], sc->qn[q][2]);
+    const V3 n = v3(SC::qn[q][0], SC::qn[q][1], SC::qn[q][2]);
     const bool flip = dot(n, D) > 0.0f;                       // :69-80 (flipped order d,c,b,a)
-    const V3 PA = sub(v3(sc->qv[q][0][0], sc->qv[q][0][1], sc->qv[q][0][2]), P);
-    const V3 PB = sub(v3(sc->qv[q][1][0], sc->qv[q][1][1], sc->qv[q][1][2]), P);
-    const V3 PC = sub(v3(sc->qv[q][2][0], sc->qv[q][2][1], sc->qv[q][2][2]), P);
-    const V3 PD = sub(v3(sc->qv[q][3][0], sc->qv[q][3][1], sc->qv[q][3][2]), P);
+    const V3 PA = sub(v3(SC::qv[q][0][0], SC::qv[q][0][1], SC::qv[q][0][2]), P);
+    const V3 PB = sub(v3(SC::qv[q][1][0], SC::qv[q][1][1], SC::qv[q][1][2]), P);
+    const V3 PC = sub(v3(SC::qv[q][2][0], SC::qv[q][2][1], SC::qv[q][2][2]), P);
+    const V3 PD = sub(v3(SC::qv[q][3][0], SC::qv[q][3][1], SC::qv[q][3][2]), P);
     const V3 pa = sel(flip, PD, PA), pb = sel(flip, PC, PB), pc = sel(flip, PB, PC), pd = sel(flip, PA, PD);
     const V3 m = cross(pc, pq);                               // :90
     float v = dot(pa, m);                                     // :91
@@ -151,12 +159,12 @@ __device__ __forceinline__ void quad_test(const PtScene* __restrict__ sc, const 
 }
 
 // TestSphereTrace, scalar.cpp:145-184 (the normal is produced later, only for the winner).
-__device__ __forceinline__ void sphere_test(const PtScene* __restrict__ sc, int s, V3 P, V3 D, float& best, int& id,
-                                            int& flag)
+template <class SC>
+__device__ __forceinline__ void sphere_test(int s, V3 P, V3 D, float& best, int& id, int& flag)
 {
-    const V3 m = sub(P, v3(sc->sph[s][0], sc->sph[s][1], sc->sph[s][2]));
+    const V3 m = sub(P, v3(SC::sph[s][0], SC::sph[s][1], SC::sph[s][2]));
     const float b = dot(m, D);
-    const float c = dot(m, m) - sc->sph_r2[s];
+    const float c = dot(m, m) - SC::sph_r2[s];
     if (c > 0.0f && b > 0.0f) return;
     const float discr = b * b - c;
     if (discr < 0.0f) return;
@@ -192,37 +200,87 @@ __device__ __forceinline__ size_t out_index(const PtJob& j, int lc, int lr)
     }
 }
 
-struct Sample {
-    V3 P, D, T, ret;
-    uint32_t rng;
-    int bounce;
-};
-
 // Frame-constant camera terms (mainImage, scalar.cpp:338-351).
 struct Camera {
     float W, H, yW, yH, aspect, yAspect, cam_dist;
 };
 
-// mainImage, scalar.cpp:329-360: seed + camera ray for (x, fy, iFrame).
-__device__ __forceinline__ void start_sample(Sample& s, const Camera& cam, float fx, float fy, float iFrame)
+// mainImage, scalar.cpp:338-351: the camera ray of pixel (fx, fy).  It does not depend on the
+// frame (no jitter in the reference), so it is computed once per pixel.
+__device__ __forceinline__ V3 camera_dir(const Camera& cam, float fx, float fy)
 {
-    s.rng = ((uint32_t)fx * 1973u + (uint32_t)fy * 9277u + (uint32_t)iFrame * 26699u) | 1u;   // :332
     const float tx = div_x(fx, cam.W, cam.yW) * 2.0f - 1.0f;                                   // :342
     float ty = div_x(fy, cam.H, cam.yH) * 2.0f - 1.0f;
     ty = div_x(ty, cam.aspect, cam.yAspect);                                                    // :347
-    s.D = normalize(v3(tx - 0.0f, ty - 0.0f, cam.cam_dist - 0.0f));                             // :351
-    s.P = v3(0.0f, 0.0f, 0.0f);
-    s.T = v3(1.0f, 1.0f, 1.0f);
-    s.ret = v3(0.0f, 0.0f, 0.0f);
-    s.bounce = 0;
+    return normalize(v3(tx - 0.0f, ty - 0.0f, cam.cam_dist - 0.0f));                            // :351
 }
 
+// scalar.cpp:332
+__device__ __forceinline__ uint32_t seed_of(float fx, float fy, float iFrame)
+{
+    return ((uint32_t)fx * 1973u + (uint32_t)fy * 9277u + (uint32_t)iFrame * 26699u) | 1u;
+}
+
+// Closest hit of one ray against the scene (TestSceneTrace, scalar.cpp:186-287).
+struct Hit {
+    float best;   // c_superFar (10000) on a miss
+    int id;       // primitive 0..8 (quads then spheres)
+    int flag;     // quad: normal flipped; sphere: hit from inside
+};
+
+template <class SC>
+__device__ __forceinline__ Hit trace(const AxisRow* s_axis, V3 P, V3 D)
+{
+    const V3 pq = sub(add(P, D), P);
+    // :122-133 axis used for the hit distance (ray-constant)
+    const int axis = fabsf(D.x) > 0.1f ? 0 : (fabsf(D.y) > 0.1f ? 1 : 2);
+    const float dP = axis == 0 ? P.x : (axis == 1 ? P.y : P.z);
+    const float dD = axis == 0 ? D.x : (axis == 1 ? D.y : D.z);
+    const float yD = rcp_x(dD);
+    Hit h{PT_SUPER_FAR, -1, 0};
+#pragma unroll PT_TRACE_UNROLL
+    for (int q = 0; q < PT_NQUADS; ++q) quad_test<SC>(s_axis, q, P, D, pq, axis, dP, dD, yD, h.best, h.id, h.flag);
+#pragma unroll PT_TRACE_UNROLL
+    for (int k = 0; k < PT_NSPHERES; ++k) sphere_test<SC>(k, P, D, h.best, h.id, h.flag);
+    return h;
+}
+
+// The hit normal the reference's TestQuadTrace/TestSphereTrace stored for the winning primitive.
+__device__ __forceinline__ V3 hit_normal(const PtLdsPrim& pr, const Hit& h, V3 P, V3 D)
+{
+    if (h.id < PT_NQUADS) {
+        const V3 n = v3(pr.nx, pr.ny, pr.nz);
+        return h.flag ? mul(n, -1.0f) : n;                              // :71
+    }
+    const V3 c = sub(add(P, mul(D, h.best)), v3(pr.nx, pr.ny, pr.nz));  // :179
+    return mul(normalize(c), h.flag ? -1.0f : 1.0f);
+}
+
+constexpr int kMaxWeights = 256;   // LDS table of the lerp weights 1/(iFrame+1) of a launch
+constexpr int kChunk = 8;          // frames per phase-B/C chunk (LDS colour slots per pixel)
+constexpr int kWavesPerBlock = 4;
+
+// One 8x8 tile of pixels per wave at a time, in three phases:
+//   A  every lane traces its pixel's camera ray (coherent, once per pixel: the camera ray, its
+//      TestSceneTrace and the bounce-0 shading are identical for every frame -- no jitter, the
+//      RNG is first drawn after them, scalar.cpp:316);
+//   B  the (pixel, frame) samples that continue past bounce 0 form a pool of items; lanes take
+//      items in lane order as they free up (ballot + mbcnt) and trace them to completion, one
+//      segment per iteration, writing each sample's radiance to LDS -- no lane waits for a
+//      longer path of "its" pixel;
+//   C  every lane runs the reference's progressive lerp over its pixel's frames IN FRAME ORDER
+//      (:812), reading the radiance of each frame from LDS (or the constant radiance of a pixel
+//      whose camera ray missed / of c_numBounces = 0).
+// Tiles come from a per-launch atomic queue (persistent waves, next tile prefetched).
 template <int LAYOUT, bool ENV, bool COUNT>
 __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
 {
     const PtScene* __restrict__ sc = job.scene;
     __shared__ PtLdsPrim s_prim[PT_NPRIMS];
     __shared__ AxisRow s_axis[PT_NQUADS * 3];
+    __shared__ float s_w[kMaxWeights];
+    __shared__ float s_col[kWavesPerBlock][64 * kChunk * 3];   // phase-B radiance per (pixel, frame)
+    __shared__ int s_list[kWavesPerBlock][64];                 // lanes whose pixel has items
     {
         const int t = threadIdx.x;
         if (t < PT_NPRIMS) {
@@ -240,128 +298,227 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
             const int q = (t - 64) / 3, k = (t - 64) % 3;
             s_axis[t - 64] = AxisRow{sc->qv[q][0][k], sc->qv[q][1][k], sc->qv[q][2][k], sc->qv[q][3][k]};
         }
+        if (t < kMaxWeights && t < job.nframes)   // :812 1/(iFrame + 1), iFrame exact below 2^24
+            s_w[t] = rcp_x((float)(job.frame_first + (uint32_t)t) + 1.0f);
     }
     __syncthreads();
 
-    // 16x16 pixels per 256-thread block, one 8x8 pixel square per wave (coherent rays per wave).
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int lc = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int lr = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
-    const bool valid = lc < job.ncols && lr < job.nrows;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float* const col_base = s_col[wv];
+    int* const list = s_list[wv];
+    const int tiles_x = (job.ncols + 7) >> 3;
+    const uint32_t total_tiles = (uint32_t)tiles_x * (uint32_t)((job.nrows + 7) >> 3);
+    const int S = job.nframes, B = job.num_bounces;
+    const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;   // channel stride
 
-    unsigned long long n_seg = 0, n_iter = 0, n_samp = 0, n_esc = 0;
-    if (valid) {
-        const size_t o = out_index<LAYOUT>(job, lc, lr);
-        const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;     // channel stride
-        float* px = job.buf + o;
-        V3 acc = v3(px[0], px[cs], px[2 * cs]);
+    Camera cam;
+    cam.W = (float)job.width;
+    cam.H = (float)job.height;
+    cam.yW = rcp_x(cam.W);
+    cam.yH = rcp_x(cam.H);
+    cam.aspect = div_x(cam.W, cam.H, cam.yH);                                   // :346
+    cam.yAspect = rcp_x(cam.aspect);
+    cam.cam_dist = sc->cam_dist;
+    const V3 amb = v3(sc->ambient[0], sc->ambient[1], sc->ambient[2]);
+    const V3 zero = v3(0.0f, 0.0f, 0.0f), one = v3(1.0f, 1.0f, 1.0f);
 
-        Camera cam;
-        cam.W = (float)job.width;
-        cam.H = (float)job.height;
-        cam.yW = rcp_x(cam.W);
-        cam.yH = rcp_x(cam.H);
-        cam.aspect = div_x(cam.W, cam.H, cam.yH);                               // :346
-        cam.yAspect = rcp_x(cam.aspect);
-        cam.cam_dist = sc->cam_dist;
-        const float fx = (float)(job.col0 + lc);                                 // :806
-        const float fy = (float)(job.height - 1 - (job.row_start + lr * job.row_stride));  // :803
-        int sidx = 0;
-        float iFrame = (float)job.frame_first;
-        Sample s;
-        start_sample(s, cam, fx, fy, iFrame);
+    unsigned long long n_seg = 0, n_iter = 0, n_samp = 0, n_esc = 0, n_prim = 0;
 
-        for (;;) {
-            if (COUNT) {
-                n_iter += 64;
-                ++n_seg;
-            }
-            // scene tables are re-read (scalar loads) each segment instead of living in SGPRs
-            asm volatile("" ::: "memory");
-            // ---- TestSceneTrace (:186-287) ----
-            const V3 P = s.P, D = s.D;
-            const V3 pq = sub(add(P, D), P);
-            // :122-133 axis used for the hit distance (ray-constant)
-            const int axis = fabsf(D.x) > 0.1f ? 0 : (fabsf(D.y) > 0.1f ? 1 : 2);
-            const float dP = axis == 0 ? P.x : (axis == 1 ? P.y : P.z);
-            const float dD = axis == 0 ? D.x : (axis == 1 ? D.y : D.z);
-            const float yD = rcp_x(dD);
-            float best = PT_SUPER_FAR;
-            int id = -1, flag = 0;
-#pragma unroll
-            for (int q = 0; q < PT_NQUADS; ++q) quad_test(sc, s_axis, q, P, D, pq, axis, dP, dD, yD, best, id, flag);
-#pragma unroll
-            for (int k = 0; k < PT_NSPHERES; ++k) sphere_test(sc, k, P, D, best, id, flag);
-
-            bool done;
-            if (best == PT_SUPER_FAR) {                          // :305-310 miss
-                V3 amb = v3(sc->ambient[0], sc->ambient[1], sc->ambient[2]);
-                (void)ENV;
-                s.ret = add(s.ret, amb);
-                done = true;
-                if (COUNT) ++n_esc;
+    uint32_t tile = __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(job.queue, 1u) : 0u);
+    uint32_t next_tile = lane == 0 ? atomicAdd(job.queue, 1u) : 0u;
+    while (tile < total_tiles) {
+        const int tyi = (int)(tile / (uint32_t)tiles_x), txi = (int)(tile % (uint32_t)tiles_x);
+        // ---------------- phase A: camera ray, once per pixel ----------------
+        const int lc = txi * 8 + (lane & 7), lr = tyi * 8 + (lane >> 3);
+        const bool valid = lc < job.ncols && lr < job.nrows;
+        const float fx = (float)(job.col0 + lc);                                            // :806
+        const float fy = (float)(job.height - 1 - (job.row_start + lr * job.row_stride));   // :803
+        float* px = nullptr;
+        V3 acc = zero;
+        int kind = -1;            // -1 no pixel, 0 camera ray missed, 1 hit and B == 0, 2 has items
+        V3 c_const = zero;        // radiance of every frame for kinds 0 and 1
+        V3 P1 = zero, n1 = zero;
+        int id1 = 0;
+        if (valid) {
+            px = job.buf + out_index<LAYOUT>(job, lc, lr);
+            acc = v3(px[0], px[cs], px[2 * cs]);
+            const V3 D0 = camera_dir(cam, fx, fy);
+            const Hit h = trace<DemofoxScene>(s_axis, zero, D0);                    // :335 rayPos = origin
+            if (COUNT) ++n_seg, ++n_prim;
+            if (h.best == PT_SUPER_FAR) {                                 // :305-310
+                kind = 0;
+                c_const = add(zero, amb);
+                if (COUNT) n_esc += (unsigned long long)S;
             } else {
-                const PtLdsPrim pr = s_prim[id];
-                V3 n;
-                if (id < PT_NQUADS) {
-                    n = v3(pr.nx, pr.ny, pr.nz);
-                    if (flag) n = mul(n, -1.0f);                  // :71
-                } else {                                          // :179 sphere normal
-                    const V3 h = sub(add(P, mul(D, best)), v3(pr.nx, pr.ny, pr.nz));
-                    n = mul(normalize(h), flag ? -1.0f : 1.0f);
-                }
-                s.P = add(add(P, mul(D, best)), mul(n, PT_NUDGE));   // :313
-                if (s.bounce < job.num_bounces)                    // the last direction is never used
-                    s.D = normalize(add(n, random_unit_vector(s.rng)));   // :316
-                s.ret = add(s.ret, mulv(v3(pr.er, pr.eg, pr.eb), s.T));   // :319
-                s.T = mulv(s.T, v3(pr.ar, pr.ag, pr.ab));                // :322
-                s.bounce += 1;
-                done = s.bounce > job.num_bounces;
+                const PtLdsPrim pr = s_prim[h.id];
+                n1 = hit_normal(pr, h, zero, D0);
+                P1 = add(add(zero, mul(D0, h.best)), mul(n1, PT_NUDGE));  // :313
+                id1 = h.id;
+                kind = B == 0 ? 1 : 2;
+                c_const = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one)); // :319 (ret after bounce 0)
             }
-            if (done) {
-                // :355-356 color = 0 + c * (1/1);  :812 lerp(last, color, 1/(iFrame+1))
-                const V3 col = v3(0.0f + s.ret.x * 1.0f, 0.0f + s.ret.y * 1.0f, 0.0f + s.ret.z * 1.0f);
-                const float t = rcp_x(iFrame + 1.0f);
-                acc = add(acc, mul(sub(col, acc), t));
-                if (COUNT) ++n_samp;
-                if (++sidx == job.nframes) break;
-                iFrame = (float)(job.frame_first + (uint32_t)sidx);
-                start_sample(s, cam, fx, fy, iFrame);
+            if (COUNT) n_samp += (unsigned long long)S;
+        }
+        const uint64_t hitmask = __ballot(kind == 2);
+        const int nh = __popcll(hitmask);
+        if (kind == 2) {
+            const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(hitmask >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)hitmask, 0u));
+            list[slot] = lane;
+        }
+        // advance the queue now (this tile's coordinates are already taken): the prefetched slot
+        // becomes the next tile and the following slot is requested, hidden behind phases B/C
+        tile = __builtin_amdgcn_readfirstlane(next_tile);
+        if (tile < total_tiles) next_tile = lane == 0 ? atomicAdd(job.queue, 1u) : 0u;
+
+        for (int f0 = 0; f0 < S; f0 += kChunk) {
+            const int nf = S - f0 < kChunk ? S - f0 : kChunk;
+            // ---------------- phase B: the pool of (pixel, frame) items ----------------
+            const int nitems = nh * nf;
+            int next_item = 0;
+            bool has_item = false, needs_dir = false;
+            int it_lane = 0, it_f = 0;
+            V3 P = zero, D = zero, T = zero, ret = zero, n = zero;
+            uint32_t rng = 0;
+            int bounce = 0;
+            while (true) {
+                const uint64_t idle = __ballot(!has_item);
+                if (idle != 0 && next_item < nitems) {
+                    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                    const int k = next_item + rank;
+                    const bool take = !has_item && k < nitems;
+                    const int fi = take ? k / nh : 0;
+                    const int src = take ? list[k - fi * nh] : lane;
+                    // pixel state of the item's pixel lives in lane `src` (all lanes shuffle)
+                    const float sPx = __shfl(P1.x, src, 64), sPy = __shfl(P1.y, src, 64), sPz = __shfl(P1.z, src, 64);
+                    const float sNx = __shfl(n1.x, src, 64), sNy = __shfl(n1.y, src, 64), sNz = __shfl(n1.z, src, 64);
+                    const int sId = __shfl(id1, src, 64);
+                    if (take) {
+                        const int slc = txi * 8 + (src & 7), slr = tyi * 8 + (src >> 3);
+                        const float sfx = (float)(job.col0 + slc);
+                        const float sfy = (float)(job.height - 1 - (job.row_start + slr * job.row_stride));
+                        const PtLdsPrim pr = s_prim[sId];
+                        rng = seed_of(sfx, sfy, (float)(job.frame_first + (uint32_t)(f0 + fi)));    // :332
+                        P = v3(sPx, sPy, sPz);                                               // :313 (bounce 0)
+                        n = v3(sNx, sNy, sNz);
+                        ret = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one));                 // :319
+                        T = mulv(one, v3(pr.ar, pr.ag, pr.ab));                              // :322
+                        bounce = 1;
+                        it_lane = src;
+                        it_f = fi;
+                        has_item = true;
+                        needs_dir = true;
+                    }
+                    const int npop = __popcll(idle);
+                    next_item += npop < nitems - next_item ? npop : nitems - next_item;
+                }
+                if (!__any(has_item)) break;
+                if (COUNT) ++n_iter;
+                if (!has_item) continue;
+                if (needs_dir) {                                                  // :316
+                    D = normalize(add(n, random_unit_vector(rng)));
+                    needs_dir = false;
+                }
+                const Hit h = trace<DemofoxScene>(s_axis, P, D);
+                if (COUNT) ++n_seg;
+                bool done;
+                if (h.best == PT_SUPER_FAR) {                                     // :305-310
+                    ret = add(ret, amb);
+                    done = true;
+                    if (COUNT) ++n_esc;
+                } else {
+                    const PtLdsPrim pr = s_prim[h.id];
+                    n = hit_normal(pr, h, P, D);
+                    P = add(add(P, mul(D, h.best)), mul(n, PT_NUDGE));            // :313
+                    ret = add(ret, mulv(v3(pr.er, pr.eg, pr.eb), T));             // :319
+                    T = mulv(T, v3(pr.ar, pr.ag, pr.ab));                         // :322
+                    bounce += 1;
+                    done = bounce > B;
+                    needs_dir = !done;       // the direction after the last bounce is never used
+                }
+                if (done) {
+                    float* c = col_base + (it_lane * kChunk + it_f) * 3;
+                    c[0] = ret.x;
+                    c[1] = ret.y;
+                    c[2] = ret.z;
+                    has_item = false;
+                }
+            }
+            // ---------------- phase C: progressive lerp in frame order ----------------
+            if (kind >= 0) {
+                for (int fi = 0; fi < nf; ++fi) {
+                    V3 c = c_const;
+                    if (kind == 2) {
+                        const float* cp = col_base + (lane * kChunk + fi) * 3;
+                        c = v3(cp[0], cp[1], cp[2]);
+                    }
+                    // color = 0 + c * (1/1) (:355-356); lerp(last, color, 1/(iFrame+1)) (:812)
+                    const V3 colr = v3(0.0f + c.x * 1.0f, 0.0f + c.y * 1.0f, 0.0f + c.z * 1.0f);
+                    const int f = f0 + fi;
+                    const float t = f < kMaxWeights ? s_w[f] : rcp_x((float)(job.frame_first + (uint32_t)f) + 1.0f);
+                    acc = add(acc, mul(sub(colr, acc), t));
+                }
             }
         }
-        px[0] = acc.x;
-        px[cs] = acc.y;
-        px[2 * cs] = acc.z;
+        if (valid) {
+            px[0] = acc.x;
+            px[cs] = acc.y;
+            px[2 * cs] = acc.z;
+        }
     }
     if (COUNT) {
-        // n_iter per lane counts this lane's iterations; the wave issued max over lanes.
-        unsigned long long wave_iters = n_iter;
-        for (int off = 32; off > 0; off >>= 1) {
-            const unsigned long long o = __shfl_xor(wave_iters, off, 64);
-            wave_iters = o > wave_iters ? o : wave_iters;
-        }
         for (int off = 32; off > 0; off >>= 1) {
             n_seg += __shfl_xor(n_seg, off, 64);
             n_samp += __shfl_xor(n_samp, off, 64);
             n_esc += __shfl_xor(n_esc, off, 64);
+            n_prim += __shfl_xor(n_prim, off, 64);
         }
         if (lane == 0) {
             atomicAdd(&job.counters[PT_CNT_SEGMENTS], n_seg);
-            atomicAdd(&job.counters[PT_CNT_LANE_SLOTS], wave_iters);
+            atomicAdd(&job.counters[PT_CNT_LANE_SLOTS], 64ull * n_iter);
             atomicAdd(&job.counters[PT_CNT_SAMPLES], n_samp);
             atomicAdd(&job.counters[PT_CNT_ESCAPED], n_esc);
+            atomicAdd(&job.counters[PT_CNT_PRIMARY], n_prim);
         }
     }
+}
+
+// Persistent grid: as many 256-thread blocks as the device keeps resident (every wave then pulls
+// tiles until the queue is drained), capped by the tile count.  Blocks beyond residency would
+// only find an empty queue, so an over-estimate costs nothing but a launch slot.
+template <typename K>
+int resident_blocks(K kern)
+{
+    static int cache[64][2];   // [device][0: blocks per CU, 1: CUs]
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
+    if (cache[dev][0] == 0) {
+        int nb = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, 0) != hipSuccess || nb <= 0) nb = 4;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        cache[dev][0] = nb;
+        cache[dev][1] = cus;
+    }
+    return cache[dev][0] * cache[dev][1];
 }
 
 template <int LAYOUT, bool ENV>
 hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 {
-    const dim3 grid((unsigned)((job.ncols + 15) / 16), (unsigned)((job.nrows + 15) / 16));
-    if (count)
-        hipLaunchKernelGGL((pt_render_kernel<LAYOUT, ENV, true>), grid, dim3(256), 0, st, job);
-    else
-        hipLaunchKernelGGL((pt_render_kernel<LAYOUT, ENV, false>), grid, dim3(256), 0, st, job);
+    const unsigned tiles = (unsigned)((job.ncols + 7) / 8) * (unsigned)((job.nrows + 7) / 8);
+    hipError_t e = hipMemsetAsync(job.queue, 0, sizeof(unsigned), st);
+    if (e != hipSuccess) return e;
+    if (count) {
+        auto k = pt_render_kernel<LAYOUT, ENV, true>;
+        const unsigned blocks = (unsigned)std::min<long>(resident_blocks(k), (tiles + 3) / 4);
+        hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, job);
+    } else {
+        auto k = pt_render_kernel<LAYOUT, ENV, false>;
+        const unsigned blocks = (unsigned)std::min<long>(resident_blocks(k), (tiles + 3) / 4);
+        hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, job);
+    }
     return hipGetLastError();
 }
 
@@ -370,7 +527,7 @@ hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 hipError_t pt_launch_render(const PtJob& job, hipStream_t st, bool count)
 {
     if (job.ncols <= 0 || job.nrows <= 0 || job.nframes <= 0) return hipSuccess;
-    if (!job.scene || !job.buf) return hipErrorInvalidValue;
+    if (!job.scene || !job.buf || !job.queue) return hipErrorInvalidValue;
     switch (job.layout) {
         case PT_LAYOUT_INTERLEAVED: return launch_t<PT_LAYOUT_INTERLEAVED, false>(job, st, count);
         case PT_LAYOUT_PLANAR8: return launch_t<PT_LAYOUT_PLANAR8, false>(job, st, count);

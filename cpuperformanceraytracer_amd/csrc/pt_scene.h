@@ -42,6 +42,33 @@ struct PtLdsPrim {
     float er, eg, eb, pad2;        // emissive
 };
 
+// The same scene as compile-time constants for the kernel's hot loop: TestSceneTrace hard-codes
+// its geometry in code, and so does the device trace -- vertex coordinates become instruction
+// literals / inline constants (no loads, no registers).  Translated vertices are constexpr f32
+// adds (round-to-nearest, like the reference's per-call adds); the quad normals need sqrtf and
+// '/', so they are written out here as the exact f32 results of normalize(cross(c-a, c-b))
+// (scalar.cpp:68) -- tests/test_scene.py recomputes them with pt_build_demofox_scene and checks
+// every constant of this table bit for bit.
+struct DemofoxScene {
+    static constexpr float T = 10.0f;   // sceneTranslation.z (scalar.cpp:189)
+    static constexpr float qv[PT_NQUADS][4][3] = {
+        {{-12.6f, -12.6f, 25.0f + T}, {12.6f, -12.6f, 25.0f + T}, {12.6f, 12.6f, 25.0f + T}, {-12.6f, 12.6f, 25.0f + T}},
+        {{-12.6f, -12.45f, 25.0f + T}, {12.6f, -12.45f, 25.0f + T}, {12.6f, -12.45f, 15.0f + T}, {-12.6f, -12.45f, 15.0f + T}},
+        {{-12.6f, 12.5f, 25.0f + T}, {12.6f, 12.5f, 25.0f + T}, {12.6f, 12.5f, 15.0f + T}, {-12.6f, 12.5f, 15.0f + T}},
+        {{-12.5f, -12.6f, 25.0f + T}, {-12.5f, -12.6f, 15.0f + T}, {-12.5f, 12.6f, 15.0f + T}, {-12.5f, 12.6f, 25.0f + T}},
+        {{12.5f, -12.6f, 25.0f + T}, {12.5f, -12.6f, 15.0f + T}, {12.5f, 12.6f, 15.0f + T}, {12.5f, 12.6f, 25.0f + T}},
+        {{-5.0f, 12.4f, 22.5f + T}, {5.0f, 12.4f, 22.5f + T}, {5.0f, 12.4f, 17.5f + T}, {-5.0f, 12.4f, 17.5f + T}},
+    };
+    // x + 0.0f (the translation's x/y) is x for every finite x, so those adds are folded above.
+    static constexpr float qn[PT_NQUADS][3] = {
+        {0.0f, 0.0f, 1.0f}, {0.0f, 1.0f, 0.0f}, {0.0f, 1.0f, 0.0f},
+        {1.0f, -0.0f, 0.0f}, {1.0f, -0.0f, 0.0f}, {0.0f, 1.0f, 0.0f},
+    };
+    static constexpr float sph[PT_NSPHERES][4] = {
+        {-9.0f, -9.5f, 20.0f + T, 3.0f}, {0.0f, -9.5f, 20.0f + T, 3.0f}, {9.0f, -9.5f, 20.0f + T, 3.0f}};
+    static constexpr float sph_r2[PT_NSPHERES] = {3.0f * 3.0f, 3.0f * 3.0f, 3.0f * 3.0f};
+};
+
 #ifndef __HIPCC_DEVICE_ONLY__
 // Host-side construction (compiled with -ffp-contract=off: one rounding per op, like the
 // reference).  tanf is the host libm's, like the reference's (MSVC float overload of tan()).

@@ -61,4 +61,5 @@ def count_device(buf, width: int, height: int, *, frame_first: int, nframes: int
     job = _job(buf, width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces, layout)
     out = N.PtWorkCounts()
     N.check(N.load().pt_count_device(ctypes.byref(job), _stream(stream), ctypes.byref(out)), "pt_count_device")
-    return {"segments": out.segments, "lane_slots": out.lane_slots, "samples": out.samples, "escaped": out.escaped}
+    return {"segments": out.segments, "lane_slots": out.lane_slots, "samples": out.samples, "escaped": out.escaped,
+            "primary": out.primary}

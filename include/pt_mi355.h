@@ -75,10 +75,11 @@ typedef struct pt_device_job {
 
 /* Work counters of pt_count_device(). */
 typedef struct pt_work_counts {
-    uint64_t segments;           /* TestSceneTrace calls (traced ray segments)                     */
+    uint64_t segments;           /* TestSceneTrace calls traced (camera rays once per pixel)        */
     uint64_t lane_slots;         /* 64 x loop iterations issued per wave, summed over waves        */
     uint64_t samples;            /* primary samples (pixels x frames)                              */
     uint64_t escaped;            /* paths that ended on a miss                                     */
+    uint64_t primary;            /* camera-ray segments traced (= pixels rendered)                 */
 } pt_work_counts;
 
 /* --- lifecycle -------------------------------------------------------------------------------- */

@@ -117,6 +117,8 @@ void pto_env_sample(const pto_env* env, const float d[3], float o[3])
 #define CNT_SEG() ((void)0)
 #define CNT_ESC() ((void)0)
 #define CNT_SAMP() ((void)0)
+#define CNT_MARK() ((void)0)
+#define CNT_PRIM() ((void)0)
 #include "pt_oracle_core.inc"
 #undef SFX
 #undef CNT
@@ -125,9 +127,12 @@ void pto_env_sample(const pto_env* env, const float d[3], float o[3])
 #undef CNT_SEG
 #undef CNT_ESC
 #undef CNT_SAMP
+#undef CNT_MARK
+#undef CNT_PRIM
 
 /* ---- instantiation 2: counted (single thread) ---- */
 static pto_counts* g_cnt;
+static uint64_t g_mark;
 #define SFX(n) n##_counted
 #define CNT(n) (g_cnt->flops_segment += (uint64_t)(n))
 #define CNTS(n) (g_cnt->flops_sample += (uint64_t)(n))
@@ -135,6 +140,8 @@ static pto_counts* g_cnt;
 #define CNT_SEG() (g_cnt->segments++)
 #define CNT_ESC() (g_cnt->escaped++)
 #define CNT_SAMP() (g_cnt->samples++)
+#define CNT_MARK() (g_mark = g_cnt->flops_segment)
+#define CNT_PRIM() (g_cnt->flops_segment_primary += g_cnt->flops_segment - g_mark, g_cnt->segments_primary++)
 #include "pt_oracle_core.inc"
 
 static void ruv_unused_guard(void) { (void)ruv_counted; (void)ruv_plain; }

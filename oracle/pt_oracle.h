@@ -55,6 +55,8 @@ typedef struct pto_counts {
     uint64_t flops_segment;  /* scene trace + shading, per segment                */
     uint64_t transcendentals;
     uint64_t escaped;        /* paths that ended on a miss                        */
+    uint64_t segments_primary;       /* bounce-0 (camera ray) segments            */
+    uint64_t flops_segment_primary;  /* their flops (trace + bounce-0 shading)    */
 } pto_counts;
 
 /* Render into buf (nrows x width x 3 f32, interleaved RGB, accumulating in place).  0 on success. */

@@ -22,4 +22,5 @@ ms = e0.elapsed_time(e1) / K
 print(json.dumps({"W": W, "H": H, "spp": S, "B": B, "ms_per_launch": ms,
                   "primary_samples_per_s": W * H * S / ms * 1e3, "ray_samples_per_s": W * H * S * B / ms * 1e3,
                   "segments_per_sample": cnt["segments"] / cnt["samples"],
+                  "ref_segments_per_sample": (cnt["segments"] - cnt["primary"]) / cnt["samples"] + 1,
                   "simd_eff": cnt["segments"] / cnt["lane_slots"], "counts": cnt}))

@@ -167,14 +167,28 @@ def test_device_row_shards_equal_full_image():
 
 
 def test_device_counts_match_oracle_counts():
-    """Device-counted traced segments == the oracle's (identical paths => identical counts)."""
+    """Device-counted work == the oracle's path statistics (identical paths => identical counts).
+    The device traces each pixel's camera ray once (it is the same for every frame), so its
+    segment count is the oracle's minus (frames - 1) camera rays per pixel."""
     from cpuperformanceraytracer_amd.device import count_device
-    w, h, f, b = 256, 256, 2, 8
+    w, h, f, b = 256, 256, 3, 8
     buf = torch.zeros(h * w * 3, dtype=torch.float32, device="cuda")
     cnt = count_device(buf, w, h, frame_first=1, nframes=f, num_bounces=b)
     img, oc = pyoracle.render_counted(w, h, nframes=f, num_bounces=b)
     assert bits_equal(buf.cpu().numpy().reshape(h, w, 3), img)
     assert cnt["samples"] == oc["samples"] == w * h * f
-    assert cnt["segments"] == oc["segments"]
+    assert cnt["primary"] == w * h and oc["segments_primary"] == w * h * f
+    assert cnt["segments"] == oc["segments"] - oc["segments_primary"] + cnt["primary"]
     assert cnt["escaped"] == oc["escaped"]
     assert cnt["lane_slots"] >= cnt["segments"]
+
+
+@pytest.mark.parametrize("b", [0, 1])
+def test_low_bounce_counts_vs_oracle(b):
+    """c_numBounces 0 and 1: the camera-ray-only and single-bounce paths of the kernel."""
+    w, h, f = 96, 64, 3
+    pt.init(num_bounces=b, samples_per_frame=f)
+    buf = np.zeros((h, w, 3), np.float32)
+    pt.DemofoxRenderScalar(buf, w, h, 3)
+    ref = pyoracle.render(w, h, nframes=f, num_bounces=b)
+    assert bits_equal(buf, ref), mismatch_report(buf, ref)
