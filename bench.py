@@ -176,13 +176,14 @@ def main() -> None:
 
     # Exact work of the timed launches (deterministic: same frames, counted on a scratch buffer).
     scratch = torch.zeros_like(buf)
-    segs = samples = slots = 0
+    segs = samples = slots = prim = 0
     for k in range(K):
         c = count_device(scratch, W, Hg, frame_first=timed_first + k * S, nframes=S, num_bounces=B,
                          row_start=row_start, row_stride=row_stride, nrows=nrows, stream=stream)
         segs += c["segments"]
         samples += c["samples"]
         slots += c["lane_slots"]
+        prim += c["primary"]
     del scratch
 
     if rank != 0:
@@ -193,7 +194,8 @@ def main() -> None:
     total_ray_samples = W * H * S * B * K * world
     value = total_ray_samples / elapsed
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-    flops_launch = RL.launch_flops(segs, samples) / K
+    flops_launch = RL.launch_flops_exec(segs, prim, samples) / K
+    flops_launch_ref = RL.launch_flops_ref(segs, prim, samples) / K
     achieved_tf = flops_launch / avg_kernel_s / 1e12
     hbm_launch, traffic_src = load_traffic()
     res = {
@@ -216,6 +218,7 @@ def main() -> None:
         "ms_per_frame_8spp": ms_step,
         "traced_segments_per_s": segs * world / (avg_kernel_s * K),
         "segments_per_sample": segs / samples,
+        "ref_segments_per_sample": RL.ref_segments(segs, prim, samples) / samples,
         "simd_lane_efficiency": segs / slots if slots else None,
         "kernel_ms_avg": avg_kernel_s * 1e3,
         "kernel_ms_min": min(kernel_ms),
@@ -228,7 +231,10 @@ def main() -> None:
             "traffic": hbm_launch,
             "kernel": "pt_render_kernel<INTERLEAVED>",
             "flops_per_launch": flops_launch,
-            "flop_model": f"segments x {RL.F_SEGMENT} + samples x {RL.F_SAMPLE} (roofline.py)",
+            "flop_model": "executed = (segments_ref x F_SEGMENT + samples x F_SAMPLE) - (samples - pixels) x "
+                          f"F_SHARED; F = {RL.F_SEGMENT}/{RL.F_SAMPLE}/{RL.F_SHARED} (roofline.py)",
+            "flops_per_launch_ref_equivalent": flops_launch_ref,
+            "achieved_ref_equivalent": flops_launch_ref / avg_kernel_s / 1e12,
             "algorithmic_bytes_per_launch": RL.BYTES_PER_PIXEL_PER_LAUNCH * W * H,
             "hbm_achieved_gbps": RL.BYTES_PER_PIXEL_PER_LAUNCH * W * H / avg_kernel_s / 1e9,
             "hbm_peak_gbps": RL.PEAK_HBM_GBPS,

@@ -38,6 +38,9 @@
 #include <math.h>
 #include <algorithm>
 
+#ifndef PT_AXIS_FROM_LDS
+#define PT_AXIS_FROM_LDS 1   // 0: select from literals (177 VGPRs, 0.89 ms) vs LDS row (127, 0.79 ms)
+#endif
 #ifndef PT_TRACE_UNROLL
 #define PT_TRACE_UNROLL 6   // primitive loops fully unrolled: the constexpr geometry becomes
 #endif                      // instruction literals (rolled: 1.05 ms vs 0.81 ms per 1080p step)
@@ -119,7 +122,16 @@ template <class SC>
 __device__ __forceinline__ void quad_test(const AxisRow* s_axis, int q, V3 P, V3 D, V3 pq, int axis, float dP,
                                           float dD, float yD, float& best, int& id, int& flag)
 {
-    const AxisRow ax = s_axis[q * 3 + axis];                  // LDS, issued early
+#if PT_AXIS_FROM_LDS
+    const AxisRow ax = s_axis[q * 3 + axis];                  // LDS (the compiler places the read)
+#else
+    // the lane's axis component of each vertex, selected from the compile-time scene
+    auto comp = [&](int k) {
+        return axis == 0 ? SC::qv[q][k][0] : (axis == 1 ? SC::qv[q][k][1] : SC::qv[q][k][2]);
+    };
+    const AxisRow ax{comp(0), comp(1), comp(2), comp(3)};
+    (void)s_axis;
+#endif
     const V3 n = v3(SC::qn[q][0], SC::qn[q][1], SC::qn[q][2]);
     const bool flip = dot(n, D) > 0.0f;                       // :69-80 (flipped order d,c,b,a)
     const V3 PA = sub(v3(SC::qv[q][0][0], SC::qv[q][0][1], SC::qv[q][0][2]), P);
@@ -136,16 +148,16 @@ __device__ __forceinline__ void quad_test(const AxisRow* s_axis, int q, V3 P, V3
     // :98 w = ScalarTriple(pq, pb, pa)  |  :111 w = ScalarTriple(pq, pa, pd)
     float w = dot(cross(pq, sel(t1, pb, pa)), sel(t1, pa, pd));
     v = t1 ? v : -v;                                          // :113
+    // :104 / :118 intersectPos = u*a + v*e + w*c (e = b or d), component `axis` only.
     if (u < 0.0f || w < 0.0f) return;                         // :97,99,110,112
+    const float ak = flip ? ax.d : ax.a;
+    const float ck = flip ? ax.b : ax.c;
+    const float ek = t1 ? (flip ? ax.c : ax.b) : (flip ? ax.a : ax.d);
     // :100-103 / :114-117
     const float denom = rcp_x((u + v) + w);
     u *= denom;
     v *= denom;
     w *= denom;
-    // :104 / :118 intersectPos = u*a + v*e + w*c (e = b or d), component `axis` only
-    const float ak = flip ? ax.d : ax.a;
-    const float ck = flip ? ax.b : ax.c;
-    const float ek = t1 ? (flip ? ax.c : ax.b) : (flip ? ax.a : ax.d);
     const float ip = (u * ak + v * ek) + w * ck;
     // :124/128/132 dist = (ip - rayPos_k) / rayDir_k.  A result that is not a normal number with
     // |dist| < 2^124 fails the test below under either division, so the fast quotient is exact
@@ -165,17 +177,17 @@ __device__ __forceinline__ void sphere_test(int s, V3 P, V3 D, float& best, int&
     const V3 m = sub(P, v3(SC::sph[s][0], SC::sph[s][1], SC::sph[s][2]));
     const float b = dot(m, D);
     const float c = dot(m, m) - SC::sph_r2[s];
-    if (c > 0.0f && b > 0.0f) return;
+    if (c > 0.0f && b > 0.0f) return;                         // :157
     const float discr = b * b - c;
-    if (discr < 0.0f) return;
+    if (discr < 0.0f) return;                                 // :164
     const float sq = sqrt_x(discr);
-    float dist = -b - sq;
+    float dist = -b - sq;                                     // :169
     bool inside = false;
-    if (dist < 0.0f) {
+    if (dist < 0.0f) {                                        // :170-174
         inside = true;
         dist = -b + sq;
     }
-    if (dist > PT_MIN_HIT && dist < best) {
+    if (dist > PT_MIN_HIT && dist < best) {                   // :176-181
         best = dist;
         id = PT_NQUADS + s;
         flag = inside ? 1 : 0;
@@ -280,7 +292,7 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
     __shared__ AxisRow s_axis[PT_NQUADS * 3];
     __shared__ float s_w[kMaxWeights];
     __shared__ float s_col[kWavesPerBlock][64 * kChunk * 3];   // phase-B radiance per (pixel, frame)
-    __shared__ int s_list[kWavesPerBlock][64];                 // lanes whose pixel has items
+    __shared__ float4 s_rec[kWavesPerBlock][64][2];            // per item pixel: P1.xyz id | n1.xyz lane
     {
         const int t = threadIdx.x;
         if (t < PT_NPRIMS) {
@@ -305,7 +317,6 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     float* const col_base = s_col[wv];
-    int* const list = s_list[wv];
     const int tiles_x = (job.ncols + 7) >> 3;
     const uint32_t total_tiles = (uint32_t)tiles_x * (uint32_t)((job.nrows + 7) >> 3);
     const int S = job.nframes, B = job.num_bounces;
@@ -324,8 +335,12 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
 
     unsigned long long n_seg = 0, n_iter = 0, n_samp = 0, n_esc = 0, n_prim = 0;
 
-    uint32_t tile = __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(job.queue, 1u) : 0u);
-    uint32_t next_tile = lane == 0 ? atomicAdd(job.queue, 1u) : 0u;
+    // (built with the atomic optimizer off: a single-lane atomic needs no wave reduction, and its
+    // return value is then only waited for where it is used, one tile later)
+    uint32_t next_tile = 0;
+    if (lane == 0) next_tile = atomicAdd(job.queue, 1u);
+    uint32_t tile = __builtin_amdgcn_readfirstlane(next_tile);
+    if (lane == 0) next_tile = atomicAdd(job.queue, 1u);
     while (tile < total_tiles) {
         const int tyi = (int)(tile / (uint32_t)tiles_x), txi = (int)(tile % (uint32_t)tiles_x);
         // ---------------- phase A: camera ray, once per pixel ----------------
@@ -337,7 +352,7 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
         V3 acc = zero;
         int kind = -1;            // -1 no pixel, 0 camera ray missed, 1 hit and B == 0, 2 has items
         V3 c_const = zero;        // radiance of every frame for kinds 0 and 1
-        V3 P1 = zero, n1 = zero;
+        V3 P1 = zero, N1 = zero;
         int id1 = 0;
         if (valid) {
             px = job.buf + out_index<LAYOUT>(job, lc, lr);
@@ -351,8 +366,9 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
                 if (COUNT) n_esc += (unsigned long long)S;
             } else {
                 const PtLdsPrim pr = s_prim[h.id];
-                n1 = hit_normal(pr, h, zero, D0);
+                const V3 n1 = hit_normal(pr, h, zero, D0);
                 P1 = add(add(zero, mul(D0, h.best)), mul(n1, PT_NUDGE));  // :313
+                N1 = n1;
                 id1 = h.id;
                 kind = B == 0 ? 1 : 2;
                 c_const = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one)); // :319 (ret after bounce 0)
@@ -361,15 +377,16 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
         }
         const uint64_t hitmask = __ballot(kind == 2);
         const int nh = __popcll(hitmask);
-        if (kind == 2) {
+        if (kind == 2) {   // compact the pixels with items: slot = rank among them
             const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(hitmask >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)hitmask, 0u));
-            list[slot] = lane;
+            s_rec[wv][slot][0] = make_float4(P1.x, P1.y, P1.z, __builtin_bit_cast(float, id1));
+            s_rec[wv][slot][1] = make_float4(N1.x, N1.y, N1.z, __builtin_bit_cast(float, lane));
         }
         // advance the queue now (this tile's coordinates are already taken): the prefetched slot
         // becomes the next tile and the following slot is requested, hidden behind phases B/C
         tile = __builtin_amdgcn_readfirstlane(next_tile);
-        if (tile < total_tiles) next_tile = lane == 0 ? atomicAdd(job.queue, 1u) : 0u;
+        if (tile < total_tiles && lane == 0) next_tile = atomicAdd(job.queue, 1u);
 
         for (int f0 = 0; f0 < S; f0 += kChunk) {
             const int nf = S - f0 < kChunk ? S - f0 : kChunk;
@@ -389,19 +406,18 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
                     const int k = next_item + rank;
                     const bool take = !has_item && k < nitems;
                     const int fi = take ? k / nh : 0;
-                    const int src = take ? list[k - fi * nh] : lane;
-                    // pixel state of the item's pixel lives in lane `src` (all lanes shuffle)
-                    const float sPx = __shfl(P1.x, src, 64), sPy = __shfl(P1.y, src, 64), sPz = __shfl(P1.z, src, 64);
-                    const float sNx = __shfl(n1.x, src, 64), sNy = __shfl(n1.y, src, 64), sNz = __shfl(n1.z, src, 64);
-                    const int sId = __shfl(id1, src, 64);
                     if (take) {
+                        const int slot = k - fi * nh;                 // the item's pixel record
+                        const float4 a0 = s_rec[wv][slot][0], a1 = s_rec[wv][slot][1];
+                        const int sId = __builtin_bit_cast(int, a0.w);
+                        const int src = __builtin_bit_cast(int, a1.w);  // lane owning the pixel
                         const int slc = txi * 8 + (src & 7), slr = tyi * 8 + (src >> 3);
                         const float sfx = (float)(job.col0 + slc);
                         const float sfy = (float)(job.height - 1 - (job.row_start + slr * job.row_stride));
                         const PtLdsPrim pr = s_prim[sId];
                         rng = seed_of(sfx, sfy, (float)(job.frame_first + (uint32_t)(f0 + fi)));    // :332
-                        P = v3(sPx, sPy, sPz);                                               // :313 (bounce 0)
-                        n = v3(sNx, sNy, sNz);
+                        P = v3(a0.x, a0.y, a0.z);                                            // :313 (bounce 0)
+                        n = v3(a1.x, a1.y, a1.z);
                         ret = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one));                 // :319
                         T = mulv(one, v3(pr.ar, pr.ag, pr.ab));                              // :322
                         bounce = 1;

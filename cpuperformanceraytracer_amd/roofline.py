@@ -7,9 +7,18 @@ camera distance, aspect ratio, 1/(iFrame+1)), sin/cos counted separately as tran
 
 The per-segment figure depends on which early exits of TestQuadTrace/TestSphereTrace a ray takes,
 so it is an average measured by the instrumented CPU restatement over a sample of the benchmark
-workload (tests/test_flops.py re-derives it and checks these constants).  The number of traced
-segments itself is counted exactly on the device for every benchmarked launch
-(pt_count_device), so   FLOP/launch = segments * F_SEGMENT + samples * F_SAMPLE.
+workload (tests/test_flops.py re-derives it and checks these constants).  The traced segments
+themselves are counted exactly on the device for every benchmarked launch (pt_count_device).
+
+Two figures per launch:
+  reference-equivalent  the reference's algorithm producing the same pixels: every frame traces
+                        its own camera ray, so segments_ref = traced - camera rays + samples and
+                        FLOP_ref = segments_ref * F_SEGMENT + samples * F_SAMPLE;
+  executed              what the kernel actually evaluates: the camera ray, its trace and the
+                        bounce-0 shading except the new direction are identical for every frame
+                        of a pixel and evaluated once, so
+                        FLOP_exec = FLOP_ref - (samples - pixels) * F_SHARED.
+The roofline fraction is reported on FLOP_exec (work the hardware did), never on FLOP_ref.
 """
 
 # Mean fp32 FLOP per traced segment (one TestSceneTrace + shading), 1920x1080, 8 bounces,
@@ -20,6 +29,10 @@ F_SEGMENT = 426.8
 F_SAMPLE = 35.0
 # Transcendentals (cosf + sinf) per traced segment: 2 per bounce that continues.
 T_SEGMENT = 1.14
+# FLOP per sample that are identical for every frame of its pixel (camera ray 20 + camera-ray
+# trace + bounce-0 shading without RUV/normalize), 1920x1080 8 bounces rows 0::8 / 3::8 (402.47 /
+# 402.52), 3840x2160 rows 5::16 (402.37).
+F_SHARED = 402.45
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters").
 PEAK_FP32_TFLOPS = 157.3   # FP32 vector (= FP32 MFMA) peak, FMA counted as 2
@@ -29,5 +42,14 @@ PEAK_HBM_GBPS = 8000.0     # HBM3E spec peak (6.29 TB/s measured copy)
 BYTES_PER_PIXEL_PER_LAUNCH = 24
 
 
-def launch_flops(segments: int, samples: int) -> float:
-    return segments * F_SEGMENT + samples * F_SAMPLE
+def ref_segments(traced: int, camera_rays: int, samples: int) -> int:
+    """Segments the reference traces for the same output (one camera ray per frame)."""
+    return traced - camera_rays + samples
+
+
+def launch_flops_ref(traced: int, camera_rays: int, samples: int) -> float:
+    return ref_segments(traced, camera_rays, samples) * F_SEGMENT + samples * F_SAMPLE
+
+
+def launch_flops_exec(traced: int, camera_rays: int, samples: int) -> float:
+    return launch_flops_ref(traced, camera_rays, samples) - (samples - camera_rays) * F_SHARED

@@ -119,6 +119,8 @@ void pto_env_sample(const pto_env* env, const float d[3], float o[3])
 #define CNT_SAMP() ((void)0)
 #define CNT_MARK() ((void)0)
 #define CNT_PRIM() ((void)0)
+#define CNT_SHARED(n) ((void)0)
+#define CNT_SHARED_PRIM(d) ((void)0)
 #include "pt_oracle_core.inc"
 #undef SFX
 #undef CNT
@@ -129,6 +131,8 @@ void pto_env_sample(const pto_env* env, const float d[3], float o[3])
 #undef CNT_SAMP
 #undef CNT_MARK
 #undef CNT_PRIM
+#undef CNT_SHARED
+#undef CNT_SHARED_PRIM
 
 /* ---- instantiation 2: counted (single thread) ---- */
 static pto_counts* g_cnt;
@@ -142,6 +146,8 @@ static uint64_t g_mark;
 #define CNT_SAMP() (g_cnt->samples++)
 #define CNT_MARK() (g_mark = g_cnt->flops_segment)
 #define CNT_PRIM() (g_cnt->flops_segment_primary += g_cnt->flops_segment - g_mark, g_cnt->segments_primary++)
+#define CNT_SHARED(n) (g_cnt->flops_shared += (uint64_t)(n))
+#define CNT_SHARED_PRIM(d) (g_cnt->flops_shared += g_cnt->flops_segment - g_mark - (uint64_t)(d))
 #include "pt_oracle_core.inc"
 
 static void ruv_unused_guard(void) { (void)ruv_counted; (void)ruv_plain; }

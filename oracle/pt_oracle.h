@@ -57,6 +57,9 @@ typedef struct pto_counts {
     uint64_t escaped;        /* paths that ended on a miss                        */
     uint64_t segments_primary;       /* bounce-0 (camera ray) segments            */
     uint64_t flops_segment_primary;  /* their flops (trace + bounce-0 shading)    */
+    uint64_t flops_shared;   /* flops that are identical for every frame of a pixel: the camera
+                                ray, its trace and its shading except the new direction (RUV +
+                                normalize); a renderer may evaluate them once per pixel          */
 } pto_counts;
 
 /* Render into buf (nrows x width x 3 f32, interleaved RGB, accumulating in place).  0 on success. */

@@ -34,7 +34,7 @@ class Counts(ctypes.Structure):
     _fields_ = [("samples", ctypes.c_uint64), ("segments", ctypes.c_uint64), ("flops_sample", ctypes.c_uint64),
                 ("flops_segment", ctypes.c_uint64), ("transcendentals", ctypes.c_uint64),
                 ("escaped", ctypes.c_uint64), ("segments_primary", ctypes.c_uint64),
-                ("flops_segment_primary", ctypes.c_uint64)]
+                ("flops_segment_primary", ctypes.c_uint64), ("flops_shared", ctypes.c_uint64)]
 
 
 _lib = None

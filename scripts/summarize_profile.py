@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Turn a gpurun_out/prof/<tag> directory (scripts/profile_gpu.sh) into committed summaries:
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (as produced)
+  profiles/<tag>_pmc.txt            per-counter means for the render kernel (non-COUNT instance)
+  profiles/pmc_summary.json         HBM bytes per launch of the render kernel (read by bench.py)
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE from separate passes (KiB),
+FETCH_SIZE doubled for the gfx950 half-count of wide reads (our accumulator reads are 12-B-per-lane
+`global_load_dwordx3`, contiguous across the wave: treated as wide; not separately calibrated).
+"""
+import collections
+import csv
+import glob
+import json
+import shutil
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+tag = sys.argv[1]
+src = ROOT / "gpurun_out" / "prof" / tag
+dst = ROOT / "profiles"
+dst.mkdir(exist_ok=True)
+KERNEL = "pt_render_kernel<0, false, false>"
+
+stats = glob.glob(str(src / "trace" / "**" / "*kernel_stats.csv"), recursive=True)
+if stats:
+    shutil.copy(stats[0], dst / f"{tag}_kernel_stats.csv")
+agg = collections.defaultdict(list)
+for f in glob.glob(str(src / "**" / "*counter_collection.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        if KERNEL in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+mean = {k: sum(v) / len(v) for k, v in agg.items()}
+lines = [f"# rocprofv3 PMC means per dispatch of {KERNEL} ({tag})"]
+for k in sorted(mean):
+    lines.append(f"{k:28s} n={len(agg[k]):3d} mean={mean[k]:.6g}")
+avg_ns = None
+if stats:
+    for r in csv.DictReader(open(stats[0])):
+        if KERNEL in r["Name"]:
+            avg_ns = float(r["AverageNs"])
+            lines.append(f"kernel_trace_average_ns      {avg_ns:.1f} (calls={r['Calls']})")
+(dst / f"{tag}_pmc.txt").write_text("\n".join(lines) + "\n")
+out = {"source": f"profiles/{tag}_pmc.txt", "kernel": KERNEL, "kernel_average_ns": avg_ns}
+if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+    out["fetch_kib"] = mean["FETCH_SIZE"]
+    out["write_kib"] = mean["WRITE_SIZE"]
+    out["hbm_bytes_per_launch"] = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
+    out["note"] = "bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB (gfx950 FETCH_SIZE half-count of wide reads)"
+(dst / "pmc_summary.json").write_text(json.dumps(out, indent=1) + "\n")
+print("\n".join(lines))
+print(json.dumps(out, indent=1))

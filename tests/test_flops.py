@@ -18,6 +18,15 @@ def test_flop_constants(w, h, rs, st, nr, frames):
     f_seg = c["flops_segment"] / c["segments"]
     assert abs(f_seg - RL.F_SEGMENT) / RL.F_SEGMENT < 0.005, f_seg
     assert abs(c["transcendentals"] / c["segments"] - RL.T_SEGMENT) < 0.02
+    f_shared = c["flops_shared"] / c["samples"]
+    assert abs(f_shared - RL.F_SHARED) / RL.F_SHARED < 0.005, f_shared
+
+
+def test_executed_flops_model():
+    """FLOP_exec = FLOP_ref - (samples - pixels) * F_SHARED; one frame per pixel => equal."""
+    assert RL.launch_flops_exec(100, 10, 10) == RL.launch_flops_ref(100, 10, 10)
+    assert RL.ref_segments(traced=22, camera_rays=2, samples=16) == 36
+    assert RL.launch_flops_exec(22, 2, 16) < RL.launch_flops_ref(22, 2, 16)
 
 
 def test_counted_render_equals_plain_render():
