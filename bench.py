@@ -45,7 +45,7 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(wl, frames: int) -> dict:
+def cpu_baseline(wl, frames: int, env=None) -> dict:
     """The oracle (C restatement of demofox_path_tracing_scalar.cpp, bit-identical to it) timed on
     this host's cores on a bounded sample of the same workload; plus the reference's own scalar
     build (oracle/_ref, c_numBounces=4 compiled in) single-threaded for calibration."""
@@ -57,12 +57,14 @@ def cpu_baseline(wl, frames: int) -> dict:
     cores = max(1, min(16, ncpu))
     pyoracle.render(64, 64, nframes=1, num_bounces=wl.num_bounces, nthreads=cores)   # warm
     t0 = time.perf_counter()
-    pyoracle.render(wl.width, wl.height, frame_first=1, nframes=frames, num_bounces=wl.num_bounces, nthreads=cores)
+    pyoracle.render(wl.width, wl.height, frame_first=1, nframes=frames, num_bounces=wl.num_bounces, nthreads=cores,
+                    env=env)
     dt = time.perf_counter() - t0
     samples = wl.width * wl.height * frames
     out = {"value": samples * wl.num_bounces / dt, "unit": "ray-samples/s", "cores": cores, "kind": "port",
            "sample": f"{wl.width}x{wl.height}, {frames} frames (spp), {wl.num_bounces} bounces, "
-                     f"oracle/pt_oracle.c (gcc -O2, {cores} threads, row-cyclic); {dt:.2f} s wall",
+                     f"oracle/pt_oracle.c (gcc -O2, {cores} threads, row-cyclic){', env map' if env is not None else ''}; "
+                     f"{dt:.2f} s wall",
            "primary_samples_per_s": samples / dt, "host_cpus_visible": ncpu,
            "cpu_model": _cpu_model()}
     ref = ROOT / "oracle" / "_ref" / "libref_scalar.so"
@@ -92,9 +94,10 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def load_traffic(kernel_substr: str = "pt_render_kernel"):
-    """Per-launch HBM bytes of the render kernel from the committed rocprofv3 PMC summary."""
-    p = ROOT / "profiles" / "pmc_summary.json"
+def load_traffic(workload: str):
+    """Per-launch HBM bytes of the render kernel from the committed rocprofv3 PMC summary of this
+    workload (profiles/pmc_summary.json for the headline c2, pmc_summary_<workload>.json else)."""
+    p = ROOT / "profiles" / ("pmc_summary.json" if workload == "c2_1080p" else f"pmc_summary_{workload}.json")
     if not p.exists():
         return None, None
     d = json.loads(p.read_text())
@@ -107,8 +110,8 @@ def main() -> None:
     import torch.distributed as dist
 
     from cpuperformanceraytracer_amd import roofline as RL
-    from cpuperformanceraytracer_amd.config import CONFIGS
-    from cpuperformanceraytracer_amd.device import count_device, ensure_backend, render_device
+    from cpuperformanceraytracer_amd.config import CONFIGS, synthetic_env
+    from cpuperformanceraytracer_amd.device import count_device, ensure_backend, render_device, set_env_map
     from cpuperformanceraytracer_amd.shard import gather_rows, max_rows, rows_of
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,6 +131,9 @@ def main() -> None:
     row_start, row_stride, nrows = rows_of(rank, world, Hg)
     mr = max_rows(world, Hg)
     ensure_backend(dev.index, B)
+    env = synthetic_env() if wl.env else None
+    if env is not None:
+        set_env_map(env, dev.index, B)
 
     buf = torch.zeros(mr * W * 3, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -135,7 +141,7 @@ def main() -> None:
 
     def step(f):
         render_device(buf, W, Hg, frame_first=f, nframes=S, num_bounces=B, row_start=row_start,
-                      row_stride=row_stride, nrows=nrows, stream=stream)
+                      row_stride=row_stride, nrows=nrows, use_env=wl.env, stream=stream)
 
     for _ in range(args.warmup):
         step(frame)
@@ -176,10 +182,11 @@ def main() -> None:
 
     # Exact work of the timed launches (deterministic: same frames, counted on a scratch buffer).
     scratch = torch.zeros_like(buf)
-    segs = samples = slots = prim = 0
+    segs = samples = slots = prim = escaped = 0
     for k in range(K):
         c = count_device(scratch, W, Hg, frame_first=timed_first + k * S, nframes=S, num_bounces=B,
-                         row_start=row_start, row_stride=row_stride, nrows=nrows, stream=stream)
+                         row_start=row_start, row_stride=row_stride, nrows=nrows, use_env=wl.env, stream=stream)
+        escaped += c["escaped"]
         segs += c["segments"]
         samples += c["samples"]
         slots += c["lane_slots"]
@@ -197,7 +204,9 @@ def main() -> None:
     flops_launch = RL.launch_flops_exec(segs, prim, samples) / K
     flops_launch_ref = RL.launch_flops_ref(segs, prim, samples) / K
     achieved_tf = flops_launch / avg_kernel_s / 1e12
-    hbm_launch, traffic_src = load_traffic()
+    hbm_launch, traffic_src = load_traffic(wl.name)
+    # config 4: one 12-byte texel gather per escaping path
+    env_bytes = RL.BYTES_PER_ENV_GATHER * escaped / K if wl.env else 0
     res = {
         "metric": METRIC,
         "value": value,
@@ -210,12 +219,14 @@ def main() -> None:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (the reference's fixed demofox quad+sphere scene; no dataset)",
+        "data": "synthetic (the reference's fixed demofox quad+sphere scene; no dataset)" + (
+            "; env map: 2048x1024 log-normal f32, seed 0xC0FFEE, standing in for the missing chinese_garden_2k.hdr"
+            if wl.env else ""),
         "config": {"workload": wl.name, "width": W, "height": H, "spp": S, "bounces": B,
                    "image_rows_total": Hg, "parallelism": f"rows interleaved x{world}" if world > 1 else "single GPU",
                    "step": f"one launch accumulating {S} frames (spp) of every pixel in HBM"},
         "primary_samples_per_s": W * H * S * K * world / elapsed,
-        "ms_per_frame_8spp": ms_step,
+        "ms_per_frame_1spp": ms_step / S,
         "traced_segments_per_s": segs * world / (avg_kernel_s * K),
         "segments_per_sample": segs / samples,
         "ref_segments_per_sample": RL.ref_segments(segs, prim, samples) / samples,
@@ -229,14 +240,14 @@ def main() -> None:
             "unit": "TFLOP/s",
             "frac": achieved_tf / RL.PEAK_FP32_TFLOPS,
             "traffic": hbm_launch,
-            "kernel": "pt_render_kernel<INTERLEAVED>",
+            "kernel": f"pt_render_kernel<INTERLEAVED, ENV={int(wl.env)}>",
             "flops_per_launch": flops_launch,
             "flop_model": "executed = (segments_ref x F_SEGMENT + samples x F_SAMPLE) - (samples - pixels) x "
                           f"F_SHARED; F = {RL.F_SEGMENT}/{RL.F_SAMPLE}/{RL.F_SHARED} (roofline.py)",
             "flops_per_launch_ref_equivalent": flops_launch_ref,
             "achieved_ref_equivalent": flops_launch_ref / avg_kernel_s / 1e12,
-            "algorithmic_bytes_per_launch": RL.BYTES_PER_PIXEL_PER_LAUNCH * W * H,
-            "hbm_achieved_gbps": RL.BYTES_PER_PIXEL_PER_LAUNCH * W * H / avg_kernel_s / 1e9,
+            "algorithmic_bytes_per_launch": RL.BYTES_PER_PIXEL_PER_LAUNCH * W * H + env_bytes,
+            "hbm_achieved_gbps": (RL.BYTES_PER_PIXEL_PER_LAUNCH * W * H + env_bytes) / avg_kernel_s / 1e9,
             "hbm_peak_gbps": RL.PEAK_HBM_GBPS,
             "traffic_source": traffic_src,
         },
@@ -244,7 +255,7 @@ def main() -> None:
     if world > 1:
         res["gather_ms"] = gather_ms
     if world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(wl, args.cpu_frames)
+        res["cpu_baseline"] = cpu_baseline(wl, args.cpu_frames, env)
     print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

@@ -13,6 +13,8 @@ from .renderer import (  # noqa: F401
     DemofoxRenderScalar,
     DemofoxRenderSimd,
     DemofoxRenderSimdTiled,
+    DemofoxRenderSimtTextured,
+    LoadTexture,
     RenderBufferInfo,
     RenderTile,
     RenderTileInfo,
@@ -20,12 +22,14 @@ from .renderer import (  # noqa: F401
     init,
     make_tiles,
     readback,
+    set_env_map,
     set_frame,
     shutdown,
+    texture,
 )
 
 __all__ = [
     "CONFIGS", "Workload", "check_valid_settings", "BeginFrame", "DemofoxRenderScalar", "DemofoxRenderSimd",
-    "DemofoxRenderSimdTiled", "RenderBufferInfo", "RenderTile", "RenderTileInfo", "get_frame", "init",
-    "make_tiles", "readback", "set_frame", "shutdown",
+    "DemofoxRenderSimdTiled", "DemofoxRenderSimtTextured", "LoadTexture", "RenderBufferInfo", "RenderTile", "RenderTileInfo", "get_frame", "init",
+    "make_tiles", "readback", "set_env_map", "set_frame", "shutdown", "texture",
 ]

@@ -29,6 +29,7 @@ EXPORTED_SYMBOLS = (
     "pt_init", "pt_shutdown", "pt_last_error", "pt_default_config", "pt_set_frame", "pt_get_frame",
     "pt_render_scalar", "pt_render_simd", "pt_render_simd_tiled", "pt_render_tile", "pt_begin_frame",
     "pt_readback", "pt_render_device", "pt_count_device",
+    "pt_load_texture", "pt_decode_hdr", "pt_free_texture", "pt_set_env_map", "pt_render_simt_textured",
 )
 
 
@@ -54,7 +55,12 @@ class PtDeviceJob(ctypes.Structure):
     _fields_ = [("buf", ctypes.c_void_p), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
                 ("row_start", ctypes.c_int32), ("row_stride", ctypes.c_int32), ("nrows", ctypes.c_int32),
                 ("layout", ctypes.c_int32), ("frame_first", ctypes.c_uint32), ("nframes", ctypes.c_int32),
-                ("num_bounces", ctypes.c_int32)]
+                ("num_bounces", ctypes.c_int32), ("use_env", ctypes.c_int32)]
+
+
+class PtTexture(ctypes.Structure):
+    _fields_ = [("data", ctypes.POINTER(ctypes.c_float)), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("components", ctypes.c_int32)]
 
 
 class PtWorkCounts(ctypes.Structure):
@@ -100,6 +106,11 @@ def load() -> ctypes.CDLL:
         "pt_readback": (i32, [vp]),
         "pt_render_device": (i32, [ctypes.POINTER(PtDeviceJob), vp]),
         "pt_count_device": (i32, [ctypes.POINTER(PtDeviceJob), vp, ctypes.POINTER(PtWorkCounts)]),
+        "pt_load_texture": (i32, [ctypes.c_char_p, ctypes.POINTER(PtTexture)]),
+        "pt_decode_hdr": (i32, [vp, ctypes.c_size_t, ctypes.POINTER(PtTexture)]),
+        "pt_free_texture": (None, [ctypes.POINTER(PtTexture)]),
+        "pt_set_env_map": (i32, [ctypes.POINTER(PtTexture)]),
+        "pt_render_simt_textured": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, ctypes.POINTER(PtTexture)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

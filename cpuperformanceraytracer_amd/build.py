@@ -23,8 +23,8 @@ CSRC = PKG / "csrc"
 LIB = PKG / "libpt_mi355.so"
 ARCH = os.environ.get("PT_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["pt_kernel.hip", "pt_scene.cpp", "pt_capi.cpp", "pt_dropin.cpp"]
-HEADERS = ["pt_kernel.h", "pt_scene.h", "pt_sincosf.h", "pt_exactmath.h"]
+SOURCES = ["pt_kernel.hip", "pt_scene.cpp", "pt_capi.cpp", "pt_dropin.cpp", "pt_texture.cpp"]
+HEADERS = ["pt_kernel.h", "pt_scene.h", "pt_sincosf.h", "pt_exactmath.h", "pt_invtrig.h"]
 PARITY_FLAGS = [
     "-ffp-contract=off",
     "-fhip-fp32-correctly-rounded-divide-sqrt",
@@ -64,6 +64,18 @@ def build_lib(force: bool = False, verbose: bool = False) -> Path:
     subprocess.run(cmd, check=True)
     os.replace(str(LIB) + ".tmp", LIB)
     return LIB
+
+
+def build_variant(name: str, defines=(), extra=()) -> Path:
+    """Dev tool: the library with extra -D defines into build/libpt_<name>.so (select it with
+    PT_MI355_LIB=...); used for kernel A/B experiments."""
+    out = ROOT / "build" / f"libpt_{name}.so"
+    out.parent.mkdir(exist_ok=True)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           *PARITY_FLAGS, *PERF_FLAGS, *[f"-D{d}" for d in defines], *extra, f"-I{ROOT / 'include'}", f"-I{CSRC}",
+           "-Wno-unused-function", *[str(CSRC / s) for s in SOURCES], "-o", str(out)]
+    subprocess.run(cmd, check=True)
+    return out
 
 
 def build_oracle(verbose: bool = False) -> None:

@@ -37,6 +37,7 @@ class Workload:
     height: int
     spp: int
     num_bounces: int
+    env: bool = False   # miss radiance = env-map sample (config 4) instead of the ambient
 
     @property
     def primary_samples(self) -> int:
@@ -52,9 +53,24 @@ CONFIGS = {
     "c1_golden": Workload("c1_golden", 256, 256, 1, 4),          # configs[0] (CPU golden)
     "c2_1080p": Workload("c2_1080p", 1920, 1080, 8, 8),          # configs[1] (headline)
     "c3_4k": Workload("c3_4k", 3840, 2160, 64, 8),               # configs[2]
-    "c4_env_1080p": Workload("c4_env_1080p", 1920, 1080, 16, 8),  # configs[3] (env map)
+    "c4_env_1080p": Workload("c4_env_1080p", 1920, 1080, 16, 8, env=True),  # configs[3] (env map)
     "c5_8k": Workload("c5_8k", 7680, 4320, 256, 8),              # configs[4] (8 GPUs)
 }
+
+
+# Config 4 names chinese_garden_2k.hdr, which is missing from the reference checkout
+# (.MISSING_LARGE_BLOBS); the stand-in is a synthetic 2k equirectangular map of the same shape.
+SYNTHETIC_ENV_SHAPE = (1024, 2048)   # rows (height) x columns (width)
+SYNTHETIC_ENV_SEED = 0xC0FFEE
+
+
+def synthetic_env(height: int = SYNTHETIC_ENV_SHAPE[0], width: int = SYNTHETIC_ENV_SHAPE[1],
+                  seed: int = SYNTHETIC_ENV_SEED):
+    """H x W x 3 f32 radiance, log-normal (median 0.37, sigma 1): HDR-like dynamic range, as a
+    texture LoadTexture would return (row 0 = bottom)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    return rng.lognormal(mean=-1.0, sigma=1.0, size=(height, width, 3)).astype(np.float32)
 
 
 def check_valid_settings(width: int, height: int, num_tiles_x: int = NUM_TILES_X,

@@ -31,16 +31,26 @@ struct State {
     unsigned long long* dcounters = nullptr;
     unsigned int* dqueue = nullptr;     // ring of kQueueSlots tile-queue counters
     unsigned queue_next = 0;
+    // env map in HBM (pt_set_env_map / pt_render_simt_textured)
+    float* denv = nullptr;
+    int32_t env_w = 0, env_h = 0;
+    const float* env_src = nullptr;     // host data the device copy was made from
 };
 
 State g;
 char g_err[512] = "no error";
 
+int vfail(int code, const char* fmt, va_list ap)
+{
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    return code;
+}
+
 int fail(int code, const char* fmt, ...)
 {
     va_list ap;
     va_start(ap, fmt);
-    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    vfail(code, fmt, ap);
     va_end(ap);
     return code;
 }
@@ -153,7 +163,65 @@ int check_frame_args(const float* buf, int32_t w, int32_t h, int32_t nc)
     return PT_OK;
 }
 
+int tiled_settings(int32_t w, int32_t h, int32_t ntx, int32_t nty, int32_t tw, int32_t th)
+{
+    // CheckValidSettings (Application.cpp:36-94) + the tile cover DemofoxRenderSimdTiled assumes
+    if (ntx <= 0 || nty <= 0 || tw <= 0 || th <= 0) return fail(PT_EINVAL, "invalid tiling");
+    if (tw % 8) return fail(PT_EINVAL, "tile width %d must be a multiple of 8 (SIMD lane width)", tw);
+    if (w % 8) return fail(PT_EINVAL, "image width %d must be a multiple of 8", w);
+    if (w % ntx || h % nty) return fail(PT_EINVAL, "image %dx%d not divisible into %dx%d tiles", w, h, ntx, nty);
+    if (ntx * tw != w || nty * th != h) return fail(PT_EINVAL, "tiles %dx(%d) x %dx(%d) do not cover %dx%d", ntx, tw, nty, th, w, h);
+    return PT_OK;
+}
+
+int check_texture(const pt_texture* t)
+{
+    if (!t->data) return fail(PT_EINVAL, "texture has no data");
+    if (t->width <= 0 || t->height <= 0) return fail(PT_EINVAL, "invalid texture size %dx%d", t->width, t->height);
+    if (t->components != 3) return fail(PT_EINVAL, "texture must have 3 components (RGB f32), got %d", t->components);
+    if ((int64_t)t->width * t->height > (int64_t)1 << 28) return fail(PT_EINVAL, "texture too large");
+    return PT_OK;
+}
+
+void release_env()
+{
+    if (g.denv) {
+        (void)hipStreamSynchronize(g.stream);
+        (void)hipFree(g.denv);
+    }
+    g.denv = nullptr;
+    g.env_w = g.env_h = 0;
+    g.env_src = nullptr;
+}
+
+int upload_env(const pt_texture* t)
+{
+    int rc;
+    if ((rc = check_texture(t))) return rc;
+    const size_t bytes = (size_t)t->width * t->height * 3 * sizeof(float);
+    release_env();
+    if (hipMalloc(&g.denv, bytes) != hipSuccess) {
+        g.denv = nullptr;
+        return fail(PT_ENOMEM, "hipMalloc(env %zu) failed", bytes);
+    }
+    HIP_TRY(hipMemcpyAsync(g.denv, t->data, bytes, hipMemcpyHostToDevice, g.stream));
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    g.env_w = t->width;
+    g.env_h = t->height;
+    g.env_src = t->data;
+    return PT_OK;
+}
+
 }  // namespace
+
+int pt_internal_fail(int code, const char* fmt, ...)
+{
+    va_list ap;
+    va_start(ap, fmt);
+    vfail(code, fmt, ap);
+    va_end(ap);
+    return code;
+}
 
 extern "C" {
 
@@ -204,6 +272,7 @@ void pt_shutdown(void)
     if (g.dcounters) (void)hipFree(g.dcounters);
     if (g.dscene) (void)hipFree(g.dscene);
     if (g.dqueue) (void)hipFree(g.dqueue);
+    if (g.denv) (void)hipFree(g.denv);
     if (g.stream) (void)hipStreamDestroy(g.stream);
     g = State{};
 }
@@ -251,12 +320,7 @@ int pt_render_simd_tiled(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t 
 {
     int rc;
     if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
-    // CheckValidSettings (Application.cpp:36-94) + the tile cover DemofoxRenderSimdTiled assumes
-    if (ntx <= 0 || nty <= 0 || tw <= 0 || th <= 0) return fail(PT_EINVAL, "invalid tiling");
-    if (tw % 8) return fail(PT_EINVAL, "tile width %d must be a multiple of 8 (SIMD lane width)", tw);
-    if (w % 8) return fail(PT_EINVAL, "image width %d must be a multiple of 8", w);
-    if (w % ntx || h % nty) return fail(PT_EINVAL, "image %dx%d not divisible into %dx%d tiles", w, h, ntx, nty);
-    if (ntx * tw != w || nty * th != h) return fail(PT_EINVAL, "tiles %dx(%d) x %dx(%d) do not cover %dx%d", ntx, tw, nty, th, w, h);
+    if ((rc = tiled_settings(w, h, ntx, nty, tw, th))) return rc;
     if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
     const size_t bytes = (size_t)w * h * 3 * sizeof(float);
     if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
@@ -264,6 +328,41 @@ int pt_render_simd_tiled(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t 
     j.layout = PT_LAYOUT_TILED_PLANAR8;
     j.tile_w = tw;
     j.tile_h = th;
+    if ((rc = launch(j, g.stream, false))) return rc;
+    g.frame += (uint32_t)g.cfg.samples_per_frame;
+    return stage_out(buf, 0, bytes);
+}
+
+int pt_set_env_map(const pt_texture* tex)
+{
+    int rc;
+    if ((rc = ensure_init())) return rc;
+    if (!tex) {
+        release_env();
+        return PT_OK;
+    }
+    return upload_env(tex);
+}
+
+int pt_render_simt_textured(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty, int32_t tw, int32_t th,
+                            int32_t nc, const pt_texture* tex)
+{
+    int rc;
+    if (!tex) return fail(PT_EINVAL, "null texture");
+    if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
+    if ((rc = tiled_settings(w, h, ntx, nty, tw, th)) || (rc = check_texture(tex))) return rc;
+    if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
+    if (!g.denv || g.env_src != tex->data || g.env_w != tex->width || g.env_h != tex->height)
+        if ((rc = upload_env(tex))) return rc;
+    const size_t bytes = (size_t)w * h * 3 * sizeof(float);
+    if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
+    PtJob j = base_job(g.dbuf, w, h);
+    j.layout = PT_LAYOUT_TILED_PLANAR8;   // RenderTile, simt_textured.cpp:491-533
+    j.tile_w = tw;
+    j.tile_h = th;
+    j.env = g.denv;
+    j.env_w = g.env_w;
+    j.env_h = g.env_h;
     if ((rc = launch(j, g.stream, false))) return rc;
     g.frame += (uint32_t)g.cfg.samples_per_frame;
     return stage_out(buf, 0, bytes);
@@ -341,6 +440,12 @@ static int device_job(const pt_device_job* dj, PtJob* j)
     j->frame_first = dj->frame_first;
     j->nframes = dj->nframes;
     j->num_bounces = dj->num_bounces;
+    if (dj->use_env) {
+        if (!g.denv) return fail(PT_ESTATE, "use_env without an env map (pt_set_env_map)");
+        j->env = g.denv;
+        j->env_w = g.env_w;
+        j->env_h = g.env_h;
+    }
     return PT_OK;
 }
 

@@ -37,3 +37,27 @@ void RenderTile(RenderBufferInfo& BufferInfo, RenderTileInfo& TileInfo)
                             TileInfo.TileMinX, TileInfo.TileMaxX, TileInfo.TileMinY,  TileInfo.TileMaxY};
     pt_check(pt_render_tile(&b, &t), "RenderTile");
 }
+
+texture LoadTexture(char* filename)
+{
+    texture t;
+    pt_texture p;
+    if (pt_load_texture(filename, &p) != PT_OK) {
+        fprintf(stderr, "LoadTexture: %s\n", pt_last_error());
+        return t;
+    }
+    t.Data = p.data;
+    t.Width = p.width;
+    t.Height = p.height;
+    t.Components = p.components;
+    return t;
+}
+
+void DemofoxRenderSimtTextured(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY,
+                               i32 TileWidth, i32 TileHeight, i32 NumChannels, texture Texture)
+{
+    const pt_texture p = {Texture.Data, Texture.Width, Texture.Height, Texture.Components};
+    pt_check(pt_render_simt_textured(BufferOut, BufferWidth, BufferHeight, NumTilesX, NumTilesY, TileWidth, TileHeight,
+                                     NumChannels, &p),
+             "DemofoxRenderSimtTextured");
+}

@@ -55,4 +55,27 @@ __device__ __forceinline__ float sqrt_rn(float x)
     return res;
 }
 
+// General-purpose guarded forms: the fast path where its preconditions provably hold, IEEE
+// otherwise (bit-identical to '/' and sqrtf for every input).
+__device__ __forceinline__ float sqrt_guarded(float x)
+{
+    float s = sqrt_rn(x);
+    if (__builtin_expect(!(x >= 0x1p-100f), 0)) s = __builtin_sqrtf(x);   // 0, tiny, NaN
+    return s;
+}
+
+// a / b: div_rn is correctly rounded when b is in [2^-125, 2^125], |a| < 2^124 and the quotient
+// is normal; the result is accepted only with a margin of one binade on both ends of the normal
+// range (so a rounded quotient cannot hide a subnormal or overflowing true quotient).
+__device__ __forceinline__ float div_guarded(float a, float b)
+{
+    const float ab = __builtin_fabsf(b);
+    float q = div_rn(a, b, rcp_rn(b));
+    const float aq = __builtin_fabsf(q);
+    const bool ok = ab >= 0x1p-125f && ab <= 0x1p125f && __builtin_fabsf(a) < 0x1p124f && aq >= 0x1p-125f &&
+                    aq <= 0x1p126f;
+    if (__builtin_expect(!ok, 0)) q = a / b;
+    return q;
+}
+
 }  // namespace pt

@@ -35,6 +35,11 @@
 #include "pt_kernel.h"
 #include "pt_exactmath.h"
 #include "pt_sincosf.h"
+// the env-map lookup's atan2f/asinf with the guarded fast '/' and sqrt (bit-identical)
+#define PT_IT_HD __device__ __forceinline__
+#define PT_IT_DIV(a, b) pt::div_guarded((a), (b))
+#define PT_IT_SQRT(x) pt::sqrt_guarded(x)
+#include "pt_invtrig.h"
 #include <math.h>
 #include <algorithm>
 
@@ -65,12 +70,7 @@ __device__ __forceinline__ V3 cross(V3 u, V3 v)
 }
 
 // ---- correctly rounded '/' and sqrt (pt_exactmath.h), IEEE fallback outside the fast range ----
-__device__ __forceinline__ float sqrt_x(float x)
-{
-    float s = pt::sqrt_rn(x);
-    if (__builtin_expect(!(x >= 0x1p-100f), 0)) s = __builtin_sqrtf(x);   // 0, tiny, NaN
-    return s;
-}
+__device__ __forceinline__ float sqrt_x(float x) { return pt::sqrt_guarded(x); }
 __device__ __forceinline__ float rcp_x(float x)
 {
     float r = pt::rcp_rn(x);
@@ -268,8 +268,39 @@ __device__ __forceinline__ V3 hit_normal(const PtLdsPrim& pr, const Hit& h, V3 P
     return mul(normalize(c), h.flag ? -1.0f : 1.0f);
 }
 
+// Miss radiance of the textured variant: EquirectangularTextureSample (texture.cpp:101-139), the
+// per-lane nearest lookup demofox_path_tracing_simt_textured.cpp:408 adds (unweighted) on a miss.
+// atan2f/asinf are the glibc algorithms (pt_invtrig.h); the texture is H x W x 3 f32, row 0 the
+// bottom row (stbi flip-on-load, asset_loading.cpp:12), L2/MALL-resident.
+__device__ __forceinline__ V3 env_sample(const float* __restrict__ env, int W, int H, V3 d)
+{
+    float u = pt::atan2f_glibc(d.z, d.x);
+    float v = pt::asinf_glibc(d.y);
+    u = u * 0.1591f;                                        // uv *= invAtan
+    v = v * 0.3183f;
+    u = u + 0.5f;
+    v = v + 0.5f;
+    u -= (float)(int32_t)u;                                 // :115-116
+    v -= (float)(int32_t)v;
+    if (u >= 0.0f && u < 1.0f && v >= 0.0f && v < 1.0f) {  // :121
+        const int32_t row = (int32_t)(v * (float)(H - 1));
+        const int32_t col = (int32_t)(u * (float)(W - 1));
+        const float* t = env + 3u * (uint32_t)(row * W + col);   // TexelFetch :6-14 (< 2^28 texels)
+        return v3(t[0], t[1], t[2]);
+    }
+    return v3(0.0f, 0.0f, 0.0f);
+}
+
+template <bool ENV>
+__device__ __forceinline__ V3 miss_radiance(const PtJob& job, V3 amb, V3 d)
+{
+    if (ENV) return env_sample(job.env, job.env_w, job.env_h, d);
+    return amb;
+}
+
 constexpr int kMaxWeights = 256;   // LDS table of the lerp weights 1/(iFrame+1) of a launch
 constexpr int kChunk = 8;          // frames per phase-B/C chunk (LDS colour slots per pixel)
+
 constexpr int kWavesPerBlock = 4;
 
 // One 8x8 tile of pixels per wave at a time, in three phases:
@@ -291,7 +322,8 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
     __shared__ PtLdsPrim s_prim[PT_NPRIMS];
     __shared__ AxisRow s_axis[PT_NQUADS * 3];
     __shared__ float s_w[kMaxWeights];
-    __shared__ float s_col[kWavesPerBlock][64 * kChunk * 3];   // phase-B radiance per (pixel, frame)
+    constexpr int CH = kChunk;
+    __shared__ float s_col[kWavesPerBlock][64 * CH * 3];   // phase-B radiance per (pixel, frame)
     __shared__ float4 s_rec[kWavesPerBlock][64][2];            // per item pixel: P1.xyz id | n1.xyz lane
     {
         const int t = threadIdx.x;
@@ -362,7 +394,7 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
             if (COUNT) ++n_seg, ++n_prim;
             if (h.best == PT_SUPER_FAR) {                                 // :305-310
                 kind = 0;
-                c_const = add(zero, amb);
+                c_const = add(zero, miss_radiance<ENV>(job, amb, D0));
                 if (COUNT) n_esc += (unsigned long long)S;
             } else {
                 const PtLdsPrim pr = s_prim[h.id];
@@ -388,8 +420,8 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
         tile = __builtin_amdgcn_readfirstlane(next_tile);
         if (tile < total_tiles && lane == 0) next_tile = atomicAdd(job.queue, 1u);
 
-        for (int f0 = 0; f0 < S; f0 += kChunk) {
-            const int nf = S - f0 < kChunk ? S - f0 : kChunk;
+        for (int f0 = 0; f0 < S; f0 += CH) {
+            const int nf = S - f0 < CH ? S - f0 : CH;
             // ---------------- phase B: the pool of (pixel, frame) items ----------------
             const int nitems = nh * nf;
             int next_item = 0;
@@ -440,7 +472,7 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
                 if (COUNT) ++n_seg;
                 bool done;
                 if (h.best == PT_SUPER_FAR) {                                     // :305-310
-                    ret = add(ret, amb);
+                    ret = add(ret, miss_radiance<ENV>(job, amb, D));            // ambient or env (:408)
                     done = true;
                     if (COUNT) ++n_esc;
                 } else {
@@ -454,7 +486,7 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
                     needs_dir = !done;       // the direction after the last bounce is never used
                 }
                 if (done) {
-                    float* c = col_base + (it_lane * kChunk + it_f) * 3;
+                    float* c = col_base + (it_lane * CH + it_f) * 3;
                     c[0] = ret.x;
                     c[1] = ret.y;
                     c[2] = ret.z;
@@ -466,7 +498,7 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
                 for (int fi = 0; fi < nf; ++fi) {
                     V3 c = c_const;
                     if (kind == 2) {
-                        const float* cp = col_base + (lane * kChunk + fi) * 3;
+                        const float* cp = col_base + (lane * CH + fi) * 3;
                         c = v3(cp[0], cp[1], cp[2]);
                     }
                     // color = 0 + c * (1/1) (:355-356); lerp(last, color, 1/(iFrame+1)) (:812)
@@ -544,6 +576,15 @@ hipError_t pt_launch_render(const PtJob& job, hipStream_t st, bool count)
 {
     if (job.ncols <= 0 || job.nrows <= 0 || job.nframes <= 0) return hipSuccess;
     if (!job.scene || !job.buf || !job.queue) return hipErrorInvalidValue;
+    if (job.env) {
+        if (job.env_w <= 0 || job.env_h <= 0) return hipErrorInvalidValue;
+        switch (job.layout) {
+            case PT_LAYOUT_INTERLEAVED: return launch_t<PT_LAYOUT_INTERLEAVED, true>(job, st, count);
+            case PT_LAYOUT_PLANAR8: return launch_t<PT_LAYOUT_PLANAR8, true>(job, st, count);
+            case PT_LAYOUT_TILED_PLANAR8: return launch_t<PT_LAYOUT_TILED_PLANAR8, true>(job, st, count);
+            default: return hipErrorInvalidValue;
+        }
+    }
     switch (job.layout) {
         case PT_LAYOUT_INTERLEAVED: return launch_t<PT_LAYOUT_INTERLEAVED, false>(job, st, count);
         case PT_LAYOUT_PLANAR8: return launch_t<PT_LAYOUT_PLANAR8, false>(job, st, count);

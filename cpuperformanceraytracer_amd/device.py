@@ -22,8 +22,16 @@ def ensure_backend(device_index: int, num_bounces: int = 4) -> None:
     _backend_device = device_index
 
 
+def set_env_map(env, device_index: int = 0, num_bounces: int = 4) -> None:
+    """Copy an env map (H x W x 3 f32, row 0 = bottom, as LoadTexture returns it) into HBM for
+    device jobs with use_env=True; None releases it."""
+    ensure_backend(device_index, num_bounces)
+    from .renderer import set_env_map as _set
+    _set(env)
+
+
 def _job(buf, width: int, height: int, row_start: int, row_stride: int, nrows: int, frame_first: int,
-         nframes: int, num_bounces: int, layout: int) -> N.PtDeviceJob:
+         nframes: int, num_bounces: int, layout: int, use_env: bool = False) -> N.PtDeviceJob:
     import torch
     if not isinstance(buf, torch.Tensor) or buf.device.type != "cuda":
         raise N.PtError(N.PT_EINVAL, "render_device", "buf must be a device (cuda/hip) tensor")
@@ -33,7 +41,7 @@ def _job(buf, width: int, height: int, row_start: int, row_stride: int, nrows: i
         raise N.PtError(N.PT_EINVAL, "render_device", f"buf holds {buf.numel()} < {nrows}x{width}x3 floats")
     ensure_backend(buf.device.index if buf.device.index is not None else torch.cuda.current_device(), num_bounces)
     return N.PtDeviceJob(buf.data_ptr(), width, height, row_start, row_stride, nrows, layout, frame_first,
-                         nframes, num_bounces)
+                         nframes, num_bounces, 1 if use_env else 0)
 
 
 def _stream(stream):
@@ -44,21 +52,22 @@ def _stream(stream):
 
 def render_device(buf, width: int, height: int, *, frame_first: int, nframes: int, num_bounces: int,
                   row_start: int = 0, row_stride: int = 1, nrows: int | None = None,
-                  layout: int = N.PT_LAYOUT_INTERLEAVED, stream=None) -> None:
+                  layout: int = N.PT_LAYOUT_INTERLEAVED, use_env: bool = False, stream=None) -> None:
     """Accumulate frames [frame_first, frame_first+nframes) of global rows row_start + k*row_stride
-    (k < nrows) into `buf` (nrows x width x 3 f32, in HBM).  Asynchronous on `stream`."""
+    (k < nrows) into `buf` (nrows x width x 3 f32, in HBM).  Asynchronous on `stream`.
+    use_env: miss radiance from the env map of set_env_map (config 4) instead of the ambient."""
     nrows = height if nrows is None else nrows
-    job = _job(buf, width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces, layout)
+    job = _job(buf, width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces, layout, use_env)
     N.check(N.load().pt_render_device(ctypes.byref(job), _stream(stream)), "pt_render_device")
 
 
 def count_device(buf, width: int, height: int, *, frame_first: int, nframes: int, num_bounces: int,
                  row_start: int = 0, row_stride: int = 1, nrows: int | None = None,
-                 layout: int = N.PT_LAYOUT_INTERLEAVED, stream=None) -> dict:
+                 layout: int = N.PT_LAYOUT_INTERLEAVED, use_env: bool = False, stream=None) -> dict:
     """Like render_device (it does render into buf) but also counts the work: traced segments,
     issued lane-slots, samples, escaped paths.  Synchronous."""
     nrows = height if nrows is None else nrows
-    job = _job(buf, width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces, layout)
+    job = _job(buf, width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces, layout, use_env)
     out = N.PtWorkCounts()
     N.check(N.load().pt_count_device(ctypes.byref(job), _stream(stream), ctypes.byref(out)), "pt_count_device")
     return {"segments": out.segments, "lane_slots": out.lane_slots, "samples": out.samples, "escaped": out.escaped,

@@ -7,6 +7,9 @@ Same names, argument meaning and error behaviour as the reference's frame functi
   DemofoxRenderSimd(BufferOut, Width, Height, NumChannels)        demofox_path_tracing_simd.h:7
   DemofoxRenderSimdTiled(BufferOut, W, H, NTX, NTY, TW, TH, NC)   demofox_path_tracing_simd_tiled.h:7
   RenderBufferInfo / RenderTileInfo / RenderTile(info, tile)      demofox_path_tracing_simd_tiled.cpp:473-535
+  texture / LoadTexture(filename)                                 texture.h:6-12, asset_loading.cpp:9-16
+  DemofoxRenderSimtTextured(BufferOut, W, H, NTX, NTY, TW, TH, NC, Texture)
+                                                                  demofox_path_tracing_simt_textured.h:8
 
 `BufferOut` is a float32 numpy array (the host render target of Application.cpp:142-151).  Each
 frame call advances the frame counter first (the reference's `static f32 iFrame`) and returns after
@@ -131,3 +134,71 @@ def make_tiles(width: int, height: int, num_tiles_x: int, num_tiles_y: int):
         for ty in range(num_tiles_y):
             tiles.append(RenderTileInfo(tx, ty, tw, th, tx * tw, tx * tw + tw - 1, ty * th, ty * th + th - 1))
     return tiles
+
+
+@dataclass
+class texture:
+    """texture.h:6-12 -- Data is Height x Width x Components f32, row 0 = bottom row."""
+    Data: np.ndarray
+    Width: int
+    Height: int
+    Components: int = 3
+
+
+def _pt_texture(t) -> tuple[N.PtTexture, np.ndarray]:
+    data = t.Data if isinstance(t, texture) else t
+    data = np.ascontiguousarray(data, dtype=np.float32)
+    if data.ndim != 3:
+        raise N.PtError(N.PT_EINVAL, "texture", "texture data must be Height x Width x Components")
+    h, w, c = data.shape
+    if isinstance(t, texture) and (t.Width != w or t.Height != h or t.Components != c):
+        raise N.PtError(N.PT_EINVAL, "texture", "texture Width/Height/Components disagree with Data.shape")
+    return N.PtTexture(data.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), w, h, c), data
+
+
+def _from_pt_texture(pt: N.PtTexture) -> texture:
+    L = N.load()
+    try:
+        n = pt.width * pt.height * pt.components
+        data = np.ctypeslib.as_array(pt.data, shape=(n,)).copy().reshape(pt.height, pt.width, pt.components)
+    finally:
+        L.pt_free_texture(ctypes.byref(pt))
+    return texture(data, data.shape[1], data.shape[0], data.shape[2])
+
+
+def LoadTexture(filename) -> texture:
+    """asset_loading.cpp:9-16: an RGBE .hdr file, flipped vertically (row 0 = bottom)."""
+    pt = N.PtTexture()
+    N.check(N.load().pt_load_texture(str(filename).encode(), ctypes.byref(pt)), "LoadTexture")
+    return _from_pt_texture(pt)
+
+
+def DecodeHdr(data: bytes) -> texture:
+    """LoadTexture on an in-memory .hdr file."""
+    pt = N.PtTexture()
+    buf = ctypes.create_string_buffer(bytes(data), len(data))
+    N.check(N.load().pt_decode_hdr(buf, len(data), ctypes.byref(pt)), "pt_decode_hdr")
+    return _from_pt_texture(pt)
+
+
+def set_env_map(tex) -> None:
+    """Upload an env map (texture, or an H x W x 3 float32 array) to HBM for device jobs with
+    use_env; None releases it."""
+    L = N.load()
+    if tex is None:
+        N.check(L.pt_set_env_map(None), "pt_set_env_map")
+        return
+    pt, keep = _pt_texture(tex)
+    N.check(L.pt_set_env_map(ctypes.byref(pt)), "pt_set_env_map")
+    del keep
+
+
+def DemofoxRenderSimtTextured(BufferOut: np.ndarray, BufferWidth: int, BufferHeight: int, NumTilesX: int,
+                              NumTilesY: int, TileWidth: int, TileHeight: int, NumChannels: int, Texture) -> None:
+    """demofox_path_tracing_simt_textured.cpp:560-620: the tiled frame with miss radiance =
+    EquirectangularTextureSample(Texture, rayDir) (:408, texture.cpp:101-139)."""
+    pt, keep = _pt_texture(Texture)
+    N.check(N.load().pt_render_simt_textured(_buf(BufferOut, BufferWidth, BufferHeight, NumChannels), BufferWidth,
+                                             BufferHeight, NumTilesX, NumTilesY, TileWidth, TileHeight, NumChannels,
+                                             ctypes.byref(pt)), "DemofoxRenderSimtTextured")
+    del keep

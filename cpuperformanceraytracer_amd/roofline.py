@@ -40,6 +40,9 @@ PEAK_HBM_GBPS = 8000.0     # HBM3E spec peak (6.29 TB/s measured copy)
 
 # Algorithmic HBM bytes: the accumulator is read once and written once per launch.
 BYTES_PER_PIXEL_PER_LAUNCH = 24
+# Config 4: one RGB f32 texel gathered per escaping path (texture.cpp:8-13).  The env-sample
+# arithmetic (atan2f/asinf, ~40 FLOP) is not part of F_SEGMENT: the config-4 roofline under-counts.
+BYTES_PER_ENV_GATHER = 12
 
 
 def ref_segments(traced: int, camera_rays: int, samples: int) -> int:

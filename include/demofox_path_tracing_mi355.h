@@ -6,6 +6,8 @@
 //   demofox_path_tracing_simd.h:7        void DemofoxRenderSimd(f32*, i32, i32, i32)
 //   demofox_path_tracing_simd_tiled.h:7  void DemofoxRenderSimdTiled(f32*, i32, i32, i32, i32, i32, i32, i32)
 //   demofox_path_tracing_simd_tiled.cpp:473-489  RenderBufferInfo, RenderTileInfo, RenderTile(&, &)
+//   texture.h:6-12, asset_loading.h:6       struct texture, texture LoadTexture(char*)
+//   demofox_path_tracing_simt_textured.h:8  void DemofoxRenderSimtTextured(f32*, i32 x7, texture)
 // Like the reference (which __debugbreak()s on bad settings), these have no error return: on
 // failure they print pt_last_error() to stderr and abort().
 #pragma once
@@ -34,3 +36,15 @@ void DemofoxRenderSimd(f32* BufferOut, i32 Width, i32 Height, i32 NumChannels);
 void DemofoxRenderSimdTiled(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY,
                             i32 TileWidth, i32 TileHeight, i32 NumChannels);
 void RenderTile(RenderBufferInfo& BufferInfo, RenderTileInfo& TileInfo);
+
+struct texture {
+    f32* Data = 0;
+    i32 Width = 0;
+    i32 Height = 0;
+    i32 Components = 3;
+};
+
+// Like stbi_loadf: Data == 0 when the file cannot be read (the reference does not check either).
+texture LoadTexture(char* filename);
+void DemofoxRenderSimtTextured(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY,
+                               i32 TileWidth, i32 TileHeight, i32 NumChannels, texture Texture);

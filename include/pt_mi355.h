@@ -17,6 +17,7 @@
  */
 #ifndef PT_MI355_H
 #define PT_MI355_H
+#include <stddef.h>
 #include <stdint.h>
 #ifdef __cplusplus
 extern "C" {
@@ -60,6 +61,14 @@ typedef struct pt_tile_info {
     int32_t tile_min_y, tile_max_y;
 } pt_tile_info;
 
+/* Mirror of `texture` (texture.h:6-12): height x width x components f32, row 0 = the image's
+ * bottom row (LoadTexture flips on load, asset_loading.cpp:12).  The env map of config 4. */
+typedef struct pt_texture {
+    float* data;
+    int32_t width, height;
+    int32_t components;          /* 3 (stbi_loadf of an .hdr always yields RGB)                    */
+} pt_texture;
+
 /* Device-resident job: the buffer already lives in HBM (bench, multi-GPU shards).  Renders the
  * global rows Y = row_start + k*row_stride, k in [0, nrows), of a width x height image into a
  * compact buffer of nrows rows, accumulating frames frame_first .. frame_first+nframes-1. */
@@ -71,6 +80,7 @@ typedef struct pt_device_job {
     uint32_t frame_first;        /* >= 1                                                            */
     int32_t nframes;
     int32_t num_bounces;
+    int32_t use_env;             /* 0: ambient miss term; 1: the env map set by pt_set_env_map      */
 } pt_device_job;
 
 /* Work counters of pt_count_device(). */
@@ -106,6 +116,19 @@ int pt_render_tile(const pt_buffer_info* buffer, const pt_tile_info* tile);
 int pt_begin_frame(void);
 /* PT_FLAG_DEFER_READBACK: copy the device accumulator of `buf` back into it */
 int pt_readback(float* buf);
+
+/* --- env map (config 4: miss radiance = EquirectangularTextureSample, texture.cpp:101-139) ----- */
+/* replaces LoadTexture, asset_loading.cpp:9-16 (Radiance RGBE .hdr, flipped vertically) */
+int pt_load_texture(const char* path, pt_texture* out);
+int pt_decode_hdr(const void* bytes, size_t nbytes, pt_texture* out);   /* same, from memory */
+void pt_free_texture(pt_texture* tex);
+/* copy `tex` into HBM as the env map of device jobs with use_env (NULL: release it) */
+int pt_set_env_map(const pt_texture* tex);
+/* replaces DemofoxRenderSimtTextured, demofox_path_tracing_simt_textured.h:8 / .cpp:560-620:
+ * the tiled frame call with the env-map miss term (tile layout of RenderTile :491-533).  The
+ * texture is uploaded when its (data, width, height) differ from the previous call's. */
+int pt_render_simt_textured(float* buf, int32_t width, int32_t height, int32_t num_tiles_x, int32_t num_tiles_y,
+                            int32_t tile_width, int32_t tile_height, int32_t num_channels, const pt_texture* tex);
 
 /* --- device-resident entry points -------------------------------------------------------------- */
 int pt_render_device(const pt_device_job* job, void* hip_stream);      /* async on hip_stream     */

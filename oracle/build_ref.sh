@@ -53,4 +53,6 @@ $CXX $FLAGS -c "$HERE/ref_driver.cpp" -o "$GEN/drv.o"
 $CXX $FLAGS -DREF_DRIVER_MAIN -c "$HERE/ref_driver.cpp" -o "$GEN/drv_main.o"
 $CXX -shared -o "$OUT/libref_scalar.so" "$GEN/scalar.o" "$GEN/drv.o" -lm
 $CXX -o "$OUT/ref_scalar" "$GEN/scalar.o" "$GEN/drv_main.o" -lm
-echo "build_ref.sh: built $OUT/libref_scalar.so and $OUT/ref_scalar"
+# LoadTexture's decoder (config 4): the reference's vendored stb_image.h, compiled where it lies
+$CXX -std=c++17 -O2 -w -I"$REF" "$HERE/ref_hdr.cpp" -o "$OUT/ref_hdr" -lm
+echo "build_ref.sh: built $OUT/libref_scalar.so, $OUT/ref_scalar and $OUT/ref_hdr"

@@ -7,19 +7,24 @@ from cpuperformanceraytracer_amd.device import render_device, count_device
 W, H, S, B = 1920, 1080, 8, 8
 if len(sys.argv) > 1:
     W, H, S, B = map(int, sys.argv[1:5])
+ENV = len(sys.argv) > 5 and sys.argv[5] == "env"
+if ENV:
+    from cpuperformanceraytracer_amd.config import synthetic_env
+    from cpuperformanceraytracer_amd.device import set_env_map
+    set_env_map(synthetic_env(), 0, B)
 buf = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
-cnt = count_device(buf, W, H, frame_first=1, nframes=S, num_bounces=B)
+cnt = count_device(buf, W, H, frame_first=1, nframes=S, num_bounces=B, use_env=ENV)
 for i in range(3):
-    render_device(buf, W, H, frame_first=1 + S * (i + 1), nframes=S, num_bounces=B)
+    render_device(buf, W, H, frame_first=1 + S * (i + 1), nframes=S, num_bounces=B, use_env=ENV)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 K = 10
 e0.record()
 for i in range(K):
-    render_device(buf, W, H, frame_first=1 + S * (i + 4), nframes=S, num_bounces=B)
+    render_device(buf, W, H, frame_first=1 + S * (i + 4), nframes=S, num_bounces=B, use_env=ENV)
 e1.record(); torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / K
-print(json.dumps({"W": W, "H": H, "spp": S, "B": B, "ms_per_launch": ms,
+print(json.dumps({"lib": __import__("os").environ.get("PT_MI355_LIB", "default"), "env": ENV, "W": W, "H": H, "spp": S, "B": B, "ms_per_launch": ms,
                   "primary_samples_per_s": W * H * S / ms * 1e3, "ray_samples_per_s": W * H * S * B / ms * 1e3,
                   "segments_per_sample": cnt["segments"] / cnt["samples"],
                   "ref_segments_per_sample": (cnt["segments"] - cnt["primary"]) / cnt["samples"] + 1,

@@ -1,0 +1,135 @@
+"""GPU parity of config 4: miss radiance = equirectangular env-map sample.
+
+Reference: demofox_path_tracing_simt_textured.cpp:402-410 adds EquirectangularTextureSample(Texture,
+rayDir) (texture.cpp:101-139) -- unweighted by the throughput -- where the scalar path adds the
+constant ambient (demofox_path_tracing_scalar.cpp:305-310); everything else is the scalar path.
+Bar: BIT-EXACT against the CPU oracle (oracle/pt_oracle.c, pto_env_sample), which evaluates
+atan2f/asinf with the host glibc; the kernel uses the same algorithms (csrc/pt_invtrig.h).
+
+The textures are synthetic (seeded): the reference's own HDR_040_Field_Env.hdr cannot travel to
+the GPU box; its decoding is pinned on the CPU against stb_image (tests/test_texture.py).
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import bits_equal, mismatch_report
+from layouts import tiled_to_interleaved
+from oracle import pyoracle
+
+pytestmark = pytest.mark.gpu
+
+import cpuperformanceraytracer_amd as pt  # noqa: E402
+from cpuperformanceraytracer_amd import _native as N  # noqa: E402
+from cpuperformanceraytracer_amd.config import synthetic_env  # noqa: E402
+
+
+def _distinct_env(h: int, w: int, seed: int) -> np.ndarray:
+    """Every texel different (an index error shows up as a mismatch)."""
+    rng = np.random.default_rng(seed)
+    return (rng.random((h, w, 3), dtype=np.float32) * 4.0 + 0.01).astype(np.float32)
+
+
+def _device_render(env, w, h, frames, bounces, frame_first=1, **rows):
+    import torch
+    from cpuperformanceraytracer_amd.device import render_device, set_env_map
+    set_env_map(env, 0, bounces)
+    nrows = rows.get("nrows", h)
+    buf = torch.zeros(nrows * w * 3, dtype=torch.float32, device="cuda:0")
+    render_device(buf, w, h, frame_first=frame_first, nframes=frames, num_bounces=bounces, use_env=True, **rows)
+    torch.cuda.synchronize()
+    return buf.cpu().numpy().reshape(nrows, w, 3)
+
+
+@pytest.mark.parametrize("env_hw,w,h,frames", [((32, 64), 320, 180, 4), ((1024, 2048), 256, 144, 16),
+                                               ((7, 5), 97, 61, 3)])
+def test_env_device_vs_oracle(env_hw, w, h, frames):
+    env = _distinct_env(*env_hw, seed=env_hw[0] * 31 + env_hw[1])
+    got = _device_render(env, w, h, frames, 8)
+    ref = pyoracle.render(w, h, nframes=frames, num_bounces=8, env=env)
+    assert bits_equal(got, ref), mismatch_report(got, ref)
+
+
+@pytest.mark.parametrize("env_hw", [(1, 1), (1, 9), (6, 1), (2, 2)])
+def test_degenerate_textures(env_hw):
+    """(H-1) or (W-1) == 0: every lookup lands in row / column 0 (texture.cpp:124-125)."""
+    env = _distinct_env(*env_hw, seed=7)
+    got = _device_render(env, 64, 48, 2, 4)
+    ref = pyoracle.render(64, 48, nframes=2, num_bounces=4, env=env)
+    assert bits_equal(got, ref), mismatch_report(got, ref)
+
+
+def test_low_bounces_env():
+    """c_numBounces 0 and 1: the camera-ray miss term (phase A) and one bounce."""
+    env = synthetic_env(64, 128, seed=3)
+    for b in (0, 1):
+        got = _device_render(env, 128, 72, 3, b)
+        ref = pyoracle.render(128, 72, nframes=3, num_bounces=b, env=env)
+        assert bits_equal(got, ref), (b, mismatch_report(got, ref))
+
+
+def test_simt_textured_tiled_vs_oracle():
+    """DemofoxRenderSimtTextured (host buffer, tile layout), two progressive frames, 2k env."""
+    pt.init(num_bounces=8)
+    env = synthetic_env()
+    tex = pt.texture(env, env.shape[1], env.shape[0], 3)
+    w, h, ntx, nty = 320, 192, 4, 3
+    tw, th = w // ntx, h // nty
+    buf = np.zeros(w * h * 3, np.float32)
+    for _ in range(2):
+        pt.DemofoxRenderSimtTextured(buf, w, h, ntx, nty, tw, th, 3, tex)
+    assert pt.get_frame() == 2
+    got = tiled_to_interleaved(buf, w, h, tw, th)
+    ref = pyoracle.render(w, h, nframes=2, num_bounces=8, env=env)
+    assert bits_equal(got, ref), mismatch_report(got, ref)
+
+
+def test_env_replaced_between_calls():
+    """A new texture (same shape, new contents) is re-uploaded and used."""
+    pt.init(num_bounces=4)
+    w, h = 96, 64
+    e1, e2 = _distinct_env(16, 32, 1), _distinct_env(16, 32, 2)
+    a = _device_render(e1, w, h, 2, 4)
+    b = _device_render(e2, w, h, 2, 4)
+    assert bits_equal(a, pyoracle.render(w, h, nframes=2, num_bounces=4, env=e1))
+    assert bits_equal(b, pyoracle.render(w, h, nframes=2, num_bounces=4, env=e2))
+    assert not bits_equal(a, b)
+
+
+def test_env_errors():
+    import torch
+    from cpuperformanceraytracer_amd.device import render_device
+    pt.init(num_bounces=4)
+    buf = torch.zeros(16 * 16 * 3, dtype=torch.float32, device="cuda:0")
+    pt.set_env_map(None)
+    with pytest.raises(N.PtError) as e:
+        render_device(buf, 16, 16, frame_first=1, nframes=1, num_bounces=4, use_env=True)
+    assert e.value.code == N.PT_ESTATE
+    with pytest.raises(N.PtError):
+        pt.set_env_map(np.zeros((4, 4, 4), np.float32))            # 4 components
+    with pytest.raises(N.PtError):
+        pt.set_env_map(np.zeros((0, 4, 3), np.float32))            # empty
+    out = np.zeros(64 * 64 * 3, np.float32)
+    with pytest.raises(N.PtError):                                  # tiles must cover the image
+        pt.DemofoxRenderSimtTextured(out, 64, 64, 3, 2, 16, 32, 3, pt.texture(np.ones((2, 2, 3), np.float32), 2, 2))
+    assert pt.get_frame() == 0
+
+
+def test_config4_full_size_sampled_rows():
+    """configs[3] at full size: 1920x1080, 16 spp, 8 bounces, the 2048x1024 synthetic env.  The
+    whole frame is rendered on the GPU; every 27th row (40 rows, 1.23 M samples) is checked bit for
+    bit against the oracle rendering those rows only."""
+    import torch
+    from cpuperformanceraytracer_amd.device import render_device, set_env_map
+    W, H, S, B = 1920, 1080, 16, 8
+    env = synthetic_env()
+    set_env_map(env, 0, B)
+    buf = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda:0")
+    render_device(buf, W, H, frame_first=1, nframes=S, num_bounces=B, use_env=True)
+    torch.cuda.synchronize()
+    img = buf.cpu().numpy().reshape(H, W, 3)
+    assert np.isfinite(img).all() and (img > 0).mean() > 0.99
+    rows = list(range(5, H, 27))
+    ref = pyoracle.render(W, H, nframes=S, num_bounces=B, row_start=5, row_stride=27, nrows=len(rows), env=env)
+    assert bits_equal(img[rows], ref), mismatch_report(img[rows], ref)
