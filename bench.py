@@ -41,24 +41,29 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2_1080p")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=8, help="frames of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="wall time of the CPU baseline sample (whole frames of the workload)")
     return ap.parse_args()
 
 
-def cpu_baseline(wl, frames: int, env=None) -> dict:
+def cpu_baseline(wl, seconds: float, env=None) -> dict:
     """The oracle (C restatement of demofox_path_tracing_scalar.cpp, bit-identical to it) timed on
-    this host's cores on a bounded sample of the same workload; plus the reference's own scalar
-    build (oracle/_ref, c_numBounces=4 compiled in) single-threaded for calibration."""
+    this host's cores on a bounded sample of the same workload -- full-size frames, as many as fit
+    in about `seconds` of wall time -- plus the reference's own scalar build (oracle/_ref,
+    c_numBounces=4 compiled in) single-threaded, for calibration."""
     from oracle import pyoracle
     try:
         ncpu = len(os.sched_getaffinity(0))
     except AttributeError:
         ncpu = os.cpu_count() or 1
     cores = max(1, min(16, ncpu))
-    pyoracle.render(64, 64, nframes=1, num_bounces=wl.num_bounces, nthreads=cores)   # warm
+    kw = dict(num_bounces=wl.num_bounces, nthreads=cores, env=env)
     t0 = time.perf_counter()
-    pyoracle.render(wl.width, wl.height, frame_first=1, nframes=frames, num_bounces=wl.num_bounces, nthreads=cores,
-                    env=env)
+    pyoracle.render(wl.width, wl.height, frame_first=1, nframes=1, **kw)      # calibration frame
+    t1 = time.perf_counter() - t0
+    frames = int(max(1, min(1024, round(seconds / max(t1, 1e-6)))))
+    t0 = time.perf_counter()
+    pyoracle.render(wl.width, wl.height, frame_first=2, nframes=frames, **kw)
     dt = time.perf_counter() - t0
     samples = wl.width * wl.height * frames
     out = {"value": samples * wl.num_bounces / dt, "unit": "ray-samples/s", "cores": cores, "kind": "port",
@@ -68,7 +73,7 @@ def cpu_baseline(wl, frames: int, env=None) -> dict:
            "primary_samples_per_s": samples / dt, "host_cpus_visible": ncpu,
            "cpu_model": _cpu_model()}
     ref = ROOT / "oracle" / "_ref" / "libref_scalar.so"
-    if ref.exists():
+    if ref.exists() and env is None:
         import ctypes
         import numpy as np
         L = ctypes.CDLL(str(ref))
@@ -77,10 +82,15 @@ def cpu_baseline(wl, frames: int, env=None) -> dict:
         buf = np.zeros((h, w, 3), np.float32)
         t0 = time.perf_counter()
         L.ref_render_scalar(buf.ctypes.data, w, h, 1)
+        t1 = time.perf_counter() - t0
+        rf = int(max(1, min(256, round(seconds / 4 / max(t1, 1e-6)))))
+        t0 = time.perf_counter()
+        L.ref_render_scalar(buf.ctypes.data, w, h, rf)
         dt = time.perf_counter() - t0
-        out["reference_scalar"] = {"primary_samples_per_s": w * h / dt, "ray_samples_per_s": w * h * 4 / dt,
-                                   "cores": 1, "sample": f"{w}x{h}, 1 frame, 4 bounces (compiled-in "
-                                   "c_numBounces), DemofoxRenderScalar built unmodified by oracle/build_ref.sh"}
+        out["reference_scalar"] = {"primary_samples_per_s": w * h * rf / dt, "ray_samples_per_s": w * h * rf * 4 / dt,
+                                   "cores": 1, "sample": f"{w}x{h}, {rf} frames, 4 bounces (compiled-in "
+                                   f"c_numBounces), DemofoxRenderScalar built unmodified by oracle/build_ref.sh; "
+                                   f"{dt:.2f} s wall"}
     return out
 
 
@@ -255,7 +265,7 @@ def main() -> None:
     if world > 1:
         res["gather_ms"] = gather_ms
     if world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(wl, args.cpu_frames, env)
+        res["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, env)
     print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

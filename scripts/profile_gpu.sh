@@ -6,14 +6,16 @@
 # Output under gpurun_out/prof/<tag>/ ; scripts/summarize_profile.py turns it into profiles/.
 set -euo pipefail
 TAG=${1:-r01}
+WORKLOAD=${WORKLOAD:-c2_1080p}
 STEPS=${STEPS:-10}
 OUT=$PWD/gpurun_out/prof/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-CMD=(python3 "$PWD/bench.py" --steps "$STEPS" --warmup 2 --no-cpu-baseline)
+CMD=(python3 "$PWD/bench.py" --workload "$WORKLOAD" --steps "$STEPS" --warmup 2 --no-cpu-baseline)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- "${CMD[@]}" > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- "${CMD[@]}" > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- "${CMD[@]}" > "$OUT/write.log" 2>&1
+[ "${TRACE_ONLY:-0}" = 1 ] && exit 0
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/sq" -o run -- "${CMD[@]}" > "$OUT/sq.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY --output-format csv -d "$OUT/sq2" -o run -- "${CMD[@]}" > "$OUT/sq2.log" 2>&1 || echo "sq2 pass failed (counter names?)"
 find "$OUT" -name '*.csv' | head -50

@@ -2,7 +2,9 @@
 """Turn a gpurun_out/prof/<tag> directory (scripts/profile_gpu.sh) into committed summaries:
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (as produced)
   profiles/<tag>_pmc.txt            per-counter means for the render kernel (non-COUNT instance)
-  profiles/pmc_summary.json         HBM bytes per launch of the render kernel (read by bench.py)
+  profiles/pmc_summary.json         HBM bytes per launch of the render kernel (read by bench.py);
+                                    pmc_summary_<workload>.json for workloads other than c2_1080p
+usage: summarize_profile.py TAG [WORKLOAD]
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE from separate passes (KiB).
 The guide's x2 correction is for 16-B-per-lane streaming reads; this kernel reads the accumulator
@@ -20,10 +22,13 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
 tag = sys.argv[1]
+workload = sys.argv[2] if len(sys.argv) > 2 else "c2_1080p"
 src = ROOT / "gpurun_out" / "prof" / tag
 dst = ROOT / "profiles"
 dst.mkdir(exist_ok=True)
-KERNEL = "pt_render_kernel<0, false, false>"
+ENV = workload.startswith("c4")
+KERNEL = f"pt_render_kernel<0, {'true' if ENV else 'false'}, false>"
+SUMMARY = "pmc_summary.json" if workload == "c2_1080p" else f"pmc_summary_{workload}.json"
 
 stats = glob.glob(str(src / "trace" / "**" / "*kernel_stats.csv"), recursive=True)
 if stats:
@@ -44,7 +49,7 @@ if stats:
             avg_ns = float(r["AverageNs"])
             lines.append(f"kernel_trace_average_ns      {avg_ns:.1f} (calls={r['Calls']})")
 (dst / f"{tag}_pmc.txt").write_text("\n".join(lines) + "\n")
-out = {"source": f"profiles/{tag}_pmc.txt", "kernel": KERNEL, "kernel_average_ns": avg_ns}
+out = {"source": f"profiles/{tag}_pmc.txt", "workload": workload, "kernel": KERNEL, "kernel_average_ns": avg_ns}
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     out["fetch_kib"] = mean["FETCH_SIZE"]
     out["write_kib"] = mean["WRITE_SIZE"]
@@ -52,6 +57,6 @@ if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     out["hbm_bytes_per_launch_if_fetch_doubled"] = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
     out["note"] = ("bytes = (FETCH_SIZE + WRITE_SIZE) KiB; the x2 FETCH correction of the guide applies to "
                    "16-B/lane reads, not to this kernel's 12-B/lane accumulator reads (see script header)")
-(dst / "pmc_summary.json").write_text(json.dumps(out, indent=1) + "\n")
+(dst / SUMMARY).write_text(json.dumps(out, indent=1) + "\n")
 print("\n".join(lines))
 print(json.dumps(out, indent=1))
