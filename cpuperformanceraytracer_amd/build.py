@@ -32,7 +32,10 @@ PARITY_FLAGS = [
 ]
 # Performance-only flags (no effect on results): the tile-queue atomic is issued by one lane, so the
 # wave-reduction rewrite of the atomic optimizer only adds an immediate wait on its return value.
-PERF_FLAGS = ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
+# -fno-slp-vectorize: the SLP vectorizer pairs independent f32 ops into v_pk_* (no faster than two
+# plain ops on gfx950) and then needs v_mov copies to build the register pairs: off, the hot loop
+# has 100 fewer VALU instructions and needs 96 instead of 122 VGPRs (5 waves per SIMD).
+PERF_FLAGS = ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None", "-fno-slp-vectorize"]
 
 
 def hipcc() -> str:

@@ -46,6 +46,9 @@
 #ifndef PT_AXIS_FROM_LDS
 #define PT_AXIS_FROM_LDS 1   // 0: select from literals (177 VGPRs, 0.89 ms) vs LDS row (127, 0.79 ms)
 #endif
+#ifndef PT_KERNEL_ATTR
+#define PT_KERNEL_ATTR
+#endif
 #ifndef PT_TRACE_UNROLL
 #define PT_TRACE_UNROLL 6   // primitive loops fully unrolled: the constexpr geometry becomes
 #endif                      // instruction literals (rolled: 1.05 ms vs 0.81 ms per 1080p step)
@@ -110,6 +113,32 @@ __device__ __forceinline__ V3 random_unit_vector(uint32_t& s)
     return v3(r * ca, r * sa, z);
 }
 
+#ifndef PT_AXIS_ASM
+#define PT_AXIS_ASM 1     // per-quad LDS rows read one quad ahead by inline asm (see trace)
+#endif
+#ifndef PT_AXIS_EARLY
+#define PT_AXIS_EARLY 1   // select the quad's axis components before the early exit (see quad_test)
+#endif
+#ifndef PT_FLIP_FOLD
+#define PT_FLIP_FOLD 1    // facing test of an axis-aligned quad normal = one component's sign
+#endif
+
+// dot(n, D) > 0 (scalar.cpp:69) for the compile-time normal n.  For a signed unit axis n and finite
+// D this is exactly the sign test of that component: the products with n's zero components are
+// signed zeros, which neither change a non-zero sum nor make a zero sum positive.
+__device__ __forceinline__ bool facing(V3 n, V3 D)
+{
+#if PT_FLIP_FOLD
+    if (n.x == 0.0f && n.z == 0.0f && n.y == 1.0f) return D.y > 0.0f;
+    if (n.x == 0.0f && n.z == 0.0f && n.y == -1.0f) return D.y < 0.0f;
+    if (n.y == 0.0f && n.z == 0.0f && n.x == 1.0f) return D.x > 0.0f;
+    if (n.y == 0.0f && n.z == 0.0f && n.x == -1.0f) return D.x < 0.0f;
+    if (n.x == 0.0f && n.y == 0.0f && n.z == 1.0f) return D.z > 0.0f;
+    if (n.x == 0.0f && n.y == 0.0f && n.z == -1.0f) return D.z < 0.0f;
+#endif
+    return dot(n, D) > 0.0f;
+}
+
 // Per-quad, per-axis vertex components (A_k, B_k, C_k, D_k): indexed by the lane's axis.
 struct AxisRow {
     float a, b, c, d;
@@ -120,9 +149,12 @@ struct AxisRow {
 // On a closer hit: best = dist, id = q, flag = flipped.
 template <class SC>
 __device__ __forceinline__ void quad_test(const AxisRow* s_axis, int q, V3 P, V3 D, V3 pq, int axis, float dP,
-                                          float dD, float yD, float& best, int& id, int& flag)
+                                          float dD, float yD, float& best, int& id, int& flag, AxisRow pre = {})
 {
-#if PT_AXIS_FROM_LDS
+#if PT_AXIS_ASM
+    const AxisRow ax = pre;                                   // read one quad ahead (trace)
+    (void)s_axis;
+#elif PT_AXIS_FROM_LDS
     const AxisRow ax = s_axis[q * 3 + axis];                  // LDS (the compiler places the read)
 #else
     // the lane's axis component of each vertex, selected from the compile-time scene
@@ -133,7 +165,7 @@ __device__ __forceinline__ void quad_test(const AxisRow* s_axis, int q, V3 P, V3
     (void)s_axis;
 #endif
     const V3 n = v3(SC::qn[q][0], SC::qn[q][1], SC::qn[q][2]);
-    const bool flip = dot(n, D) > 0.0f;                       // :69-80 (flipped order d,c,b,a)
+    const bool flip = facing(n, D);                           // :69-80 (flipped order d,c,b,a)
     const V3 PA = sub(v3(SC::qv[q][0][0], SC::qv[q][0][1], SC::qv[q][0][2]), P);
     const V3 PB = sub(v3(SC::qv[q][1][0], SC::qv[q][1][1], SC::qv[q][1][2]), P);
     const V3 PC = sub(v3(SC::qv[q][2][0], SC::qv[q][2][1], SC::qv[q][2][2]), P);
@@ -149,10 +181,19 @@ __device__ __forceinline__ void quad_test(const AxisRow* s_axis, int q, V3 P, V3
     float w = dot(cross(pq, sel(t1, pb, pa)), sel(t1, pa, pd));
     v = t1 ? v : -v;                                          // :113
     // :104 / :118 intersectPos = u*a + v*e + w*c (e = b or d), component `axis` only.
+#if PT_AXIS_EARLY
+    // selected for every lane BEFORE the divergent exit: the LDS row is then read at the top of
+    // the test and its latency hidden by the arithmetic above (inside the branch it is exposed)
+    const float ak = flip ? ax.d : ax.a;
+    const float ck = flip ? ax.b : ax.c;
+    const float ek = t1 ? (flip ? ax.c : ax.b) : (flip ? ax.a : ax.d);
+    if (u < 0.0f || w < 0.0f) return;                         // :97,99,110,112
+#else
     if (u < 0.0f || w < 0.0f) return;                         // :97,99,110,112
     const float ak = flip ? ax.d : ax.a;
     const float ck = flip ? ax.b : ax.c;
     const float ek = t1 ? (flip ? ax.c : ax.b) : (flip ? ax.a : ax.d);
+#endif
     // :100-103 / :114-117
     const float denom = rcp_x((u + v) + w);
     u *= denom;
@@ -250,8 +291,26 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, V3 P, V3 D)
     const float dD = axis == 0 ? D.x : (axis == 1 ? D.y : D.z);
     const float yD = rcp_x(dD);
     Hit h{PT_SUPER_FAR, -1, 0};
+#if PT_AXIS_ASM
+    // software pipeline of the per-quad LDS rows: row q+1 is read while quad q is tested, so the
+    // LDS latency hides under a quad test instead of stalling inside its divergent tail
+    typedef __attribute__((address_space(3))) const AxisRow lds_row_t;
+    const uint32_t base = (uint32_t)(uintptr_t)(lds_row_t*)s_axis + (uint32_t)axis * (uint32_t)sizeof(AxisRow);
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    f32x4 row;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(row) : "v"(base));
+#pragma unroll
+    for (int q = 0; q < PT_NQUADS; ++q) {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(row));
+        const AxisRow cur{row.x, row.y, row.z, row.w};
+        if (q + 1 < PT_NQUADS)
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(row) : "v"(base), "i"((q + 1) * 3 * (int)sizeof(AxisRow)));
+        quad_test<SC>(s_axis, q, P, D, pq, axis, dP, dD, yD, h.best, h.id, h.flag, cur);
+    }
+#else
 #pragma unroll PT_TRACE_UNROLL
     for (int q = 0; q < PT_NQUADS; ++q) quad_test<SC>(s_axis, q, P, D, pq, axis, dP, dD, yD, h.best, h.id, h.flag);
+#endif
 #pragma unroll PT_TRACE_UNROLL
     for (int k = 0; k < PT_NSPHERES; ++k) sphere_test<SC>(k, P, D, h.best, h.id, h.flag);
     return h;
@@ -298,8 +357,11 @@ __device__ __forceinline__ V3 miss_radiance(const PtJob& job, V3 amb, V3 d)
     return amb;
 }
 
-constexpr int kMaxWeights = 256;   // LDS table of the lerp weights 1/(iFrame+1) of a launch
-constexpr int kChunk = 8;          // frames per phase-B/C chunk (LDS colour slots per pixel)
+constexpr int kMaxWeights = 64;    // LDS table of the lerp weights 1/(iFrame+1) of a launch
+#ifndef PT_CHUNK
+#define PT_CHUNK 8
+#endif
+constexpr int kChunk = PT_CHUNK;   // frames per phase-B/C chunk (LDS colour slots per pixel)
 
 constexpr int kWavesPerBlock = 4;
 
@@ -316,7 +378,7 @@ constexpr int kWavesPerBlock = 4;
 //      whose camera ray missed / of c_numBounces = 0).
 // Tiles come from a per-launch atomic queue (persistent waves, next tile prefetched).
 template <int LAYOUT, bool ENV, bool COUNT>
-__global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
+__global__ __launch_bounds__(256) PT_KERNEL_ATTR void pt_render_kernel(PtJob job)
 {
     const PtScene* __restrict__ sc = job.scene;
     __shared__ PtLdsPrim s_prim[PT_NPRIMS];
@@ -324,7 +386,10 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
     __shared__ float s_w[kMaxWeights];
     constexpr int CH = kChunk;
     __shared__ float s_col[kWavesPerBlock][64 * CH * 3];   // phase-B radiance per (pixel, frame)
-    __shared__ float4 s_rec[kWavesPerBlock][64][2];            // per item pixel: P1.xyz id | n1.xyz lane
+    // per item pixel: P1.xyz + (id | lane << 8) and n1 (planar), 28 B: with kChunk 8 the block
+    // fits 32 KiB of LDS, so 5 blocks (5 waves per SIMD) stay resident per CU
+    __shared__ float4 s_rec[kWavesPerBlock][64];
+    __shared__ float s_nrm[kWavesPerBlock][3][64];
     {
         const int t = threadIdx.x;
         if (t < PT_NPRIMS) {
@@ -412,8 +477,10 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
         if (kind == 2) {   // compact the pixels with items: slot = rank among them
             const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(hitmask >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)hitmask, 0u));
-            s_rec[wv][slot][0] = make_float4(P1.x, P1.y, P1.z, __builtin_bit_cast(float, id1));
-            s_rec[wv][slot][1] = make_float4(N1.x, N1.y, N1.z, __builtin_bit_cast(float, lane));
+            s_rec[wv][slot] = make_float4(P1.x, P1.y, P1.z, __builtin_bit_cast(float, id1 | (lane << 8)));
+            s_nrm[wv][0][slot] = N1.x;
+            s_nrm[wv][1][slot] = N1.y;
+            s_nrm[wv][2][slot] = N1.z;
         }
         // advance the queue now (this tile's coordinates are already taken): the prefetched slot
         // becomes the next tile and the following slot is requested, hidden behind phases B/C
@@ -440,16 +507,17 @@ __global__ __launch_bounds__(256) void pt_render_kernel(PtJob job)
                     const int fi = take ? k / nh : 0;
                     if (take) {
                         const int slot = k - fi * nh;                 // the item's pixel record
-                        const float4 a0 = s_rec[wv][slot][0], a1 = s_rec[wv][slot][1];
-                        const int sId = __builtin_bit_cast(int, a0.w);
-                        const int src = __builtin_bit_cast(int, a1.w);  // lane owning the pixel
+                        const float4 a0 = s_rec[wv][slot];
+                        const int packed = __builtin_bit_cast(int, a0.w);
+                        const int sId = packed & 0xff;
+                        const int src = packed >> 8;                  // lane owning the pixel
                         const int slc = txi * 8 + (src & 7), slr = tyi * 8 + (src >> 3);
                         const float sfx = (float)(job.col0 + slc);
                         const float sfy = (float)(job.height - 1 - (job.row_start + slr * job.row_stride));
                         const PtLdsPrim pr = s_prim[sId];
                         rng = seed_of(sfx, sfy, (float)(job.frame_first + (uint32_t)(f0 + fi)));    // :332
                         P = v3(a0.x, a0.y, a0.z);                                            // :313 (bounce 0)
-                        n = v3(a1.x, a1.y, a1.z);
+                        n = v3(s_nrm[wv][0][slot], s_nrm[wv][1][slot], s_nrm[wv][2][slot]);
                         ret = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one));                 // :319
                         T = mulv(one, v3(pr.ar, pr.ag, pr.ab));                              // :322
                         bounce = 1;
