@@ -11,9 +11,35 @@
 #include "../../include/pt_mi355.h"
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 namespace {
+
+// Tile schedule of a recurring job geometry: the previous launch's per-tile costs, and the order
+// built from them (longest tiles first) for the next launch on the same stream.  Per-pixel work
+// varies ~10x across the image (rays inside the box bounce, sky rays stop), and with the tiles
+// taken in raster order the last-dequeued expensive tiles left most of the chip idle at the end.
+struct Sched {
+    bool used = false;
+    hipStream_t stream = nullptr;
+    int32_t width = 0, height = 0, col0 = 0, ncols = 0, row_start = 0, row_stride = 0, nrows = 0, bounces = 0;
+    const float* env = nullptr;
+    uint32_t ntiles = 0;
+    uint32_t* cost = nullptr;
+    uint32_t* order = nullptr;
+    uint32_t* units = nullptr;    // ntiles + 2 words: run starts, then the run count
+    bool have_cost = false;
+    bool built = false;           // order/units hold a schedule
+    unsigned long long launches = 0;
+    unsigned long long last_use = 0;
+};
+constexpr int kSchedSlots = 16;
+constexpr uint32_t kSchedMinTiles = 512;   // smaller jobs (e.g. one RenderTile) are not scheduled
+#ifndef PT_SCHED_REBUILD
+#define PT_SCHED_REBUILD 16
+#endif
+constexpr unsigned long long kSchedRebuild = PT_SCHED_REBUILD;
 
 struct State {
     bool inited = false;
@@ -29,12 +55,14 @@ struct State {
     size_t mirror_bytes = 0;
     bool mirror_valid = false;          // deferred mode: device copy is authoritative
     unsigned long long* dcounters = nullptr;
-    unsigned int* dqueue = nullptr;     // ring of kQueueSlots tile-queue counters
+    unsigned int* dqueue = nullptr;     // ring of kQueueSlots tile-queue blocks (PT_QUEUE_WORDS each)
     unsigned queue_next = 0;
     // env map in HBM (pt_set_env_map / pt_render_simt_textured)
     float* denv = nullptr;
     int32_t env_w = 0, env_h = 0;
     const float* env_src = nullptr;     // host data the device copy was made from
+    Sched sched[kSchedSlots];
+    unsigned long long sched_clock = 0;
 };
 
 State g;
@@ -63,6 +91,11 @@ int fail(int code, const char* fmt, ...)
 
 constexpr uint32_t kMaxFrame = 1u << 24;   // iFrame is an f32 counter: exact below 2^24
 constexpr unsigned kQueueSlots = 256;      // launches in flight that may share the ring
+#if PT_DIAG
+constexpr int kCounterSlots = 32 + 4 * 65536 + 96 * 65536;   // + per-wave records, per-tile log
+#else
+constexpr int kCounterSlots = 32;
+#endif
 
 int ensure_init()
 {
@@ -142,13 +175,84 @@ PtJob base_job(float* buf, int32_t w, int32_t h)
     j.env = nullptr;
     j.env_w = j.env_h = 0;
     j.counters = nullptr;
+    j.order = nullptr;
+    j.units = nullptr;
+    j.nunits = nullptr;
+    j.cost = nullptr;
     j.scene = g.dscene;
     return j;
 }
 
+void free_sched(Sched& s)
+{
+    if (s.cost) (void)hipFree(s.cost);
+    if (s.order) (void)hipFree(s.order);
+    if (s.units) (void)hipFree(s.units);
+    s = Sched{};
+}
+
+Sched* find_sched(const PtJob& j, hipStream_t st)
+{
+    const uint32_t n = pt_job_tiles(j);
+    if (n < kSchedMinTiles) return nullptr;
+    Sched* lru = &g.sched[0];
+    for (Sched& s : g.sched) {
+        if (s.used && s.stream == st && s.width == j.width && s.height == j.height && s.col0 == j.col0 &&
+            s.ncols == j.ncols && s.row_start == j.row_start && s.row_stride == j.row_stride && s.nrows == j.nrows &&
+            s.bounces == j.num_bounces && s.env == j.env) {
+            s.last_use = ++g.sched_clock;
+            return &s;
+        }
+        if (!s.used || (lru->used && s.last_use < lru->last_use)) lru = &s;
+    }
+    if (lru->used) {   // evict: its buffers may still be read by a launch (its stream may be gone)
+        (void)hipDeviceSynchronize();
+        free_sched(*lru);
+    }
+    Sched s;
+    if (hipMalloc(&s.cost, n * sizeof(uint32_t)) != hipSuccess || hipMalloc(&s.order, n * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&s.units, (n + 2) * sizeof(uint32_t)) != hipSuccess) {
+        free_sched(s);
+        return nullptr;   // unscheduled launch (raster order): correct, only slower
+    }
+    s.used = true;
+    s.stream = st;
+    s.width = j.width;
+    s.height = j.height;
+    s.col0 = j.col0;
+    s.ncols = j.ncols;
+    s.row_start = j.row_start;
+    s.row_stride = j.row_stride;
+    s.nrows = j.nrows;
+    s.bounces = j.num_bounces;
+    s.env = j.env;
+    s.ntiles = n;
+    s.last_use = ++g.sched_clock;
+    *lru = s;
+    return lru;
+}
+
 int launch(PtJob j, hipStream_t st, bool count)
 {
-    j.queue = g.dqueue + (g.queue_next++ % kQueueSlots);
+    if (Sched* s = find_sched(j, st)) {
+        // (re)build the schedule from the last launch's costs on the 2nd launch of a geometry and
+        // then every kSchedRebuild launches (the costs of a fixed view barely change; the builder
+        // is a one-workgroup kernel of ~80 us)
+        if (s->have_cost && (!s->built || s->launches % kSchedRebuild == 0)) {
+            hipError_t e = pt_launch_schedule(s->cost, s->order, s->units, s->units + s->ntiles + 1, s->ntiles, st);
+            if (e != hipSuccess) return fail(PT_EHIP, "schedule launch failed: %s", hipGetErrorString(e));
+            s->built = true;
+        }
+        if (s->built) {
+            j.order = s->order;
+            j.units = s->units;
+            j.nunits = s->units + s->ntiles + 1;
+        }
+        j.cost = s->cost;
+        s->have_cost = true;
+        ++s->launches;
+    }
+    j.queue = g.dqueue + (size_t)(g.queue_next++ % kQueueSlots) * PT_QUEUE_WORDS;
     hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
     return PT_OK;
@@ -250,9 +354,9 @@ int pt_init(const pt_config* cfg)
     if (c.device < 0 || c.device >= ndev) return fail(PT_EHIP, "device %d not available (%d devices)", c.device, ndev);
     HIP_TRY(hipSetDevice(c.device));
     HIP_TRY(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
-    if (hipMalloc(&g.dcounters, PT_CNT_N * sizeof(unsigned long long)) != hipSuccess)
+    if (hipMalloc(&g.dcounters, kCounterSlots * sizeof(unsigned long long)) != hipSuccess)
         return fail(PT_ENOMEM, "hipMalloc(counters) failed");
-    if (hipMalloc(&g.dqueue, kQueueSlots * sizeof(unsigned)) != hipSuccess)
+    if (hipMalloc(&g.dqueue, (size_t)kQueueSlots * PT_QUEUE_WORDS * sizeof(unsigned)) != hipSuccess)
         return fail(PT_ENOMEM, "hipMalloc(queue) failed");
     g.cfg = c;
     pt_build_demofox_scene(&g.scene, c.ambient);
@@ -273,6 +377,8 @@ void pt_shutdown(void)
     if (g.dscene) (void)hipFree(g.dscene);
     if (g.dqueue) (void)hipFree(g.dqueue);
     if (g.denv) (void)hipFree(g.denv);
+    for (Sched& sc : g.sched)
+        if (sc.used) free_sched(sc);
     if (g.stream) (void)hipStreamDestroy(g.stream);
     g = State{};
 }
@@ -464,12 +570,33 @@ int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
     if (!out) return fail(PT_EINVAL, "null counts");
     if ((rc = ensure_init()) || (rc = device_job(dj, &j))) return rc;
     hipStream_t st = (hipStream_t)stream;
-    HIP_TRY(hipMemsetAsync(g.dcounters, 0, PT_CNT_N * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(g.dcounters, 0, kCounterSlots * sizeof(unsigned long long), st));
+#if PT_DIAG
+    HIP_TRY(hipMemsetAsync(g.dcounters + PT_CNT_N + 9, 0xff, sizeof(unsigned long long), st));    // min
+    HIP_TRY(hipMemsetAsync(g.dcounters + PT_CNT_N + 12, 0xff, sizeof(unsigned long long), st));   // min
+#endif
     j.counters = g.dcounters;
     if ((rc = launch(j, st, true))) return rc;
-    unsigned long long h[PT_CNT_N];
+    static unsigned long long h[kCounterSlots];
     HIP_TRY(hipMemcpyAsync(h, g.dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+#if PT_DIAG
+    fprintf(stderr, "PT_DIAG cycles: A %llu take %llu dir %llu trace %llu shade %llu C %llu tile %llu\n",
+            h[PT_CNT_N + 0], h[PT_CNT_N + 1], h[PT_CNT_N + 2], h[PT_CNT_N + 3], h[PT_CNT_N + 4], h[PT_CNT_N + 5],
+            h[PT_CNT_N + 6]);
+    fprintf(stderr, "PT_DIAG wave lifetimes %llu memtime ticks, %llu realtime (100 MHz) ticks\n", h[PT_CNT_N + 7],
+            h[PT_CNT_N + 10]);
+    const unsigned long long r0 = h[PT_CNT_N + 12];
+    fprintf(stderr, "PT_DIAG realtime (us from first start): last start %.1f, first end %.1f, last end %.1f\n",
+            (h[PT_CNT_N + 8] - r0) * 0.01, (h[PT_CNT_N + 9] - r0) * 0.01, (h[PT_CNT_N + 11] - r0) * 0.01);
+    if (const char* path = getenv("PT_DIAG_OUT")) {
+        FILE* f = fopen(path, "wb");
+        if (f) {
+            fwrite(h + 32, sizeof(unsigned long long), 4 * 65536 + 96 * 65536, f);
+            fclose(f);
+        }
+    }
+#endif
     out->segments = h[PT_CNT_SEGMENTS];
     out->lane_slots = h[PT_CNT_LANE_SLOTS];
     out->samples = h[PT_CNT_SAMPLES];

@@ -37,8 +37,27 @@ struct PtJob {
     const float* env;           // device env map (H x W x 3), nullptr => ambient
     int32_t env_w, env_h;
     unsigned long long* counters;  // PT_CNT_N u64, COUNT build only
-    unsigned int* queue;           // tile-queue counter (zeroed on the stream before each launch)
+    unsigned int* queue;           // PT_QUEUE_WORDS tile-queue words (zeroed on the stream before each launch)
+    const uint32_t* order;         // tile schedule: position -> tile (a permutation), nullptr = identity
+    const uint32_t* units;         // schedule runs: unit k = positions [units[k], units[k+1]), nullptr = one tile each
+    const uint32_t* nunits;        // device word: number of units (with units)
+    uint32_t* cost;                // per-tile work of this launch (trace iterations), nullptr = not recorded
 };
+
+// Tile queues: one counter per XCD group, 128 B apart (PT_QUEUE_WORDS u32 per launch).
+#define PT_NQUEUES 8
+#define PT_QUEUE_WORDS (PT_NQUEUES * 32)
 
 // Enqueue one render launch on `stream`.  Returns hipSuccess or the launch error.
 hipError_t pt_launch_render(const PtJob& job, hipStream_t stream, bool count);
+
+// Tiles of a job (8x8 pixel tiles over ncols x nrows).
+inline uint32_t pt_job_tiles(const PtJob& j)
+{
+    return (uint32_t)((j.ncols + 7) / 8) * (uint32_t)((j.nrows + 7) / 8);
+}
+
+// Enqueue the schedule builder: order = the tiles sorted by descending cost (a permutation),
+// units = runs of about equal cost over it (ntiles + 1 words), *nunits = their number.
+hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* units, uint32_t* nunits,
+                              uint32_t ntiles, hipStream_t stream);

@@ -357,6 +357,18 @@ __device__ __forceinline__ V3 miss_radiance(const PtJob& job, V3 amb, V3 d)
     return amb;
 }
 
+#ifndef PT_DIAG
+#define PT_DIAG 0   // diagnostic build: per-phase shader-clock cycles in counters[5..] (COUNT launches)
+#endif
+#if PT_DIAG
+#define DIAG_MARK(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
+#define DIAG_ADD(k, t0) \
+    if (COUNT) dg[k] += __builtin_amdgcn_s_memtime() - (t0)
+#else
+#define DIAG_MARK(var)
+#define DIAG_ADD(k, t0)
+#endif
+
 constexpr int kMaxWeights = 64;    // LDS table of the lerp weights 1/(iFrame+1) of a launch
 #ifndef PT_CHUNK
 #define PT_CHUNK 8
@@ -431,15 +443,105 @@ __global__ __launch_bounds__(256) PT_KERNEL_ATTR void pt_render_kernel(PtJob job
     const V3 zero = v3(0.0f, 0.0f, 0.0f), one = v3(1.0f, 1.0f, 1.0f);
 
     unsigned long long n_seg = 0, n_iter = 0, n_samp = 0, n_esc = 0, n_prim = 0;
+#if PT_DIAG
+    unsigned long long dg[7] = {0, 0, 0, 0, 0, 0, 0};   // A, take, dir, trace, shade, C, tile-total
+    const unsigned long long t_birth = __builtin_amdgcn_s_memtime();
+    const unsigned long long r_birth = __builtin_amdgcn_s_memrealtime();
+    unsigned long long n_tiles_diag = 0;
+#endif
 
     // (built with the atomic optimizer off: a single-lane atomic needs no wave reduction, and its
     // return value is then only waited for where it is used, one tile later)
-    uint32_t next_tile = 0;
-    if (lane == 0) next_tile = atomicAdd(job.queue, 1u);
-    uint32_t tile = __builtin_amdgcn_readfirstlane(next_tile);
-    if (lane == 0) next_tile = atomicAdd(job.queue, 1u);
-    while (tile < total_tiles) {
+    // Tile schedule.  The launch's work is a list of UNITS -- runs of tiles in schedule order
+    // (job.order: the previous launch's tiles sorted by descending cost, so the long tiles start
+    // first and the tail is made of short ones; job.units: run boundaries, each run worth about
+    // kUnitCost trace iterations, so a run of cheap sky tiles costs one dequeue, not dozens).
+    // Without a schedule every tile is a unit, in raster order.
+    // Units are dealt to PT_NQUEUES groups of blocks (block b -> group b % 8, the XCD it is
+    // dispatched to): group x owns unit slots x, x+8, ...  Each wave's first unit is static (its
+    // index in the group), later ones come from the group's own counter (one returning atomic per
+    // unit, requested one unit ahead); a group whose units are used up takes the others'.  One
+    // counter for the whole chip saturated (~90 dequeues/us, MI355X_MICROARCH.md "dequeue").
+    constexpr uint32_t kNone = 0xffffffffu;
+    const uint32_t nunits = job.units ? *job.nunits : total_tiles;
+    const uint32_t ngroups = gridDim.x < PT_NQUEUES ? gridDim.x : PT_NQUEUES;   // small grids: fewer
+    const uint32_t qg = blockIdx.x % ngroups;
+    auto group_waves = [&](uint32_t g) { return ((gridDim.x - g + ngroups - 1) / ngroups) * kWavesPerBlock; };
+    auto slot_of = [&](uint32_t g, uint32_t c) {   // unit slot of dynamic position c of group g
+        const uint32_t slot = g + ngroups * (group_waves(g) + c);
+        return slot < nunits ? slot : kNone;
+    };
+    // Stealing happens only at the end of the launch, when thousands of waves run out at once and
+    // atomics on the counters queue up: a group found exhausted is remembered per wave, and a
+    // plain load of a counter screens it first (a counter only grows, so a load that shows it used
+    // up is right; without the screening the tail's atomics tripled the launch time).
+    uint32_t dead = 0;   // lane 0: groups known to be exhausted
+    auto steal = [&]() {
+        for (uint32_t k = 1; k < ngroups; ++k) {
+            const uint32_t g = (qg + k) % ngroups;
+            if ((dead >> g) & 1u) continue;
+            unsigned int* const c = job.queue + g * 32u;
+            if (slot_of(g, __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == kNone) {
+                dead |= 1u << g;
+                continue;
+            }
+            const uint32_t slot = slot_of(g, atomicAdd(c, 1u));
+            if (slot != kNone) return slot;
+            dead |= 1u << g;
+        }
+        return kNone;
+    };
+    auto unit_lo = [&](uint32_t u) { return job.units ? job.units[u] : u; };
+    auto unit_hi = [&](uint32_t u) { return job.units ? job.units[u + 1] : u + 1; };
+    auto tile_at = [&](uint32_t i) { return job.order ? job.order[i] : i; };
+    unsigned int* const q = job.queue + qg * 32u;
+    // lane 0: the current unit's remaining schedule positions [c_pos, c_end), the next unit's
+    // [n_pos, n_end) (bounds loaded one unit ahead), the raw counter of the unit after it, and the
+    // next tile (its schedule entry loaded one tile ahead)
+    uint32_t c_pos = kNone, c_end = kNone, n_pos = kNone, n_end = kNone, pending = 0;
+    auto take_next = [&]() -> uint32_t {
+        if (c_pos == c_end) {   // current unit done: switch to the prefetched one
+            c_pos = n_pos;
+            c_end = n_end;
+            if (c_pos == kNone) return kNone;
+            uint32_t u = ((dead >> qg) & 1u) ? kNone : slot_of(qg, pending);
+            if (u == kNone) {
+                dead |= 1u << qg;
+                u = steal();
+            }
+            n_pos = u == kNone ? kNone : unit_lo(u);
+            n_end = u == kNone ? kNone : unit_hi(u);
+            if (!((dead >> qg) & 1u)) pending = atomicAdd(q, 1u);
+        }
+        return tile_at(c_pos++);
+    };
+    uint32_t tile = kNone, next_tile = kNone;
+    if (lane == 0) {
+        const uint32_t u0 = qg + ngroups * ((blockIdx.x / ngroups) * kWavesPerBlock + (uint32_t)wv);
+        if (u0 < nunits) {   // static first unit
+            c_pos = unit_lo(u0);
+            c_end = unit_hi(u0);
+            uint32_t u1 = slot_of(qg, atomicAdd(q, 1u));
+            if (u1 == kNone) {
+                dead |= 1u << qg;
+                u1 = steal();
+            }
+            n_pos = u1 == kNone ? kNone : unit_lo(u1);
+            n_end = u1 == kNone ? kNone : unit_hi(u1);
+            if (!((dead >> qg) & 1u)) pending = atomicAdd(q, 1u);
+            tile = take_next();
+            next_tile = take_next();
+        }
+    }
+    tile = __builtin_amdgcn_readfirstlane(tile);
+    while (tile != kNone) {
         const int tyi = (int)(tile / (uint32_t)tiles_x), txi = (int)(tile % (uint32_t)tiles_x);
+        DIAG_MARK(t_tile);
+#if PT_DIAG
+        const unsigned long long r_tile0 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t diag_tile_id = tile;
+        ++n_tiles_diag;
+#endif
         // ---------------- phase A: camera ray, once per pixel ----------------
         const int lc = txi * 8 + (lane & 7), lr = tyi * 8 + (lane >> 3);
         const bool valid = lc < job.ncols && lr < job.nrows;
@@ -484,11 +586,14 @@ __global__ __launch_bounds__(256) PT_KERNEL_ATTR void pt_render_kernel(PtJob job
         }
         // advance the queue now (this tile's coordinates are already taken): the prefetched slot
         // becomes the next tile and the following slot is requested, hidden behind phases B/C
+        const uint32_t this_tile = tile;
         tile = __builtin_amdgcn_readfirstlane(next_tile);
-        if (tile < total_tiles && lane == 0) next_tile = atomicAdd(job.queue, 1u);
+        if (tile != kNone && lane == 0) next_tile = take_next();
+        uint32_t tile_work = 1;   // trace iterations of this tile (the schedule's cost)
 
         for (int f0 = 0; f0 < S; f0 += CH) {
             const int nf = S - f0 < CH ? S - f0 : CH;
+            DIAG_ADD(0, t_tile);
             // ---------------- phase B: the pool of (pixel, frame) items ----------------
             const int nitems = nh * nf;
             int next_item = 0;
@@ -498,6 +603,7 @@ __global__ __launch_bounds__(256) PT_KERNEL_ATTR void pt_render_kernel(PtJob job
             uint32_t rng = 0;
             int bounce = 0;
             while (true) {
+                DIAG_MARK(t_it);
                 const uint64_t idle = __ballot(!has_item);
                 if (idle != 0 && next_item < nitems) {
                     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
@@ -530,13 +636,20 @@ __global__ __launch_bounds__(256) PT_KERNEL_ATTR void pt_render_kernel(PtJob job
                     next_item += npop < nitems - next_item ? npop : nitems - next_item;
                 }
                 if (!__any(has_item)) break;
+                ++tile_work;
+                DIAG_ADD(1, t_it);
+                DIAG_MARK(t_dir);
                 if (COUNT) ++n_iter;
                 if (!has_item) continue;
                 if (needs_dir) {                                                  // :316
                     D = normalize(add(n, random_unit_vector(rng)));
                     needs_dir = false;
                 }
+                DIAG_ADD(2, t_dir);
+                DIAG_MARK(t_tr);
                 const Hit h = trace<DemofoxScene>(s_axis, P, D);
+                DIAG_ADD(3, t_tr);
+                DIAG_MARK(t_sh);
                 if (COUNT) ++n_seg;
                 bool done;
                 if (h.best == PT_SUPER_FAR) {                                     // :305-310
@@ -560,8 +673,10 @@ __global__ __launch_bounds__(256) PT_KERNEL_ATTR void pt_render_kernel(PtJob job
                     c[2] = ret.z;
                     has_item = false;
                 }
+                DIAG_ADD(4, t_sh);
             }
             // ---------------- phase C: progressive lerp in frame order ----------------
+            DIAG_MARK(t_c);
             if (kind >= 0) {
                 for (int fi = 0; fi < nf; ++fi) {
                     V3 c = c_const;
@@ -576,12 +691,23 @@ __global__ __launch_bounds__(256) PT_KERNEL_ATTR void pt_render_kernel(PtJob job
                     acc = add(acc, mul(sub(colr, acc), t));
                 }
             }
+            DIAG_ADD(5, t_c);
         }
         if (valid) {
             px[0] = acc.x;
             px[cs] = acc.y;
             px[2 * cs] = acc.z;
         }
+        if (job.cost && lane == 0) job.cost[this_tile] = tile_work;
+#if PT_DIAG
+        if (COUNT && lane == 0 && n_tiles_diag <= 32) {
+            unsigned long long* tl = job.counters + 32 + 4 * 65536 + 96 * (size_t)(blockIdx.x * kWavesPerBlock + wv);
+            tl[3 * (n_tiles_diag - 1) + 0] = r_tile0;
+            tl[3 * (n_tiles_diag - 1) + 1] = __builtin_amdgcn_s_memrealtime();
+            tl[3 * (n_tiles_diag - 1) + 2] = ((unsigned long long)diag_tile_id << 32) | tile_work;
+        }
+#endif
+        DIAG_ADD(6, t_tile);
     }
     if (COUNT) {
         for (int off = 32; off > 0; off >>= 1) {
@@ -596,6 +722,22 @@ __global__ __launch_bounds__(256) PT_KERNEL_ATTR void pt_render_kernel(PtJob job
             atomicAdd(&job.counters[PT_CNT_SAMPLES], n_samp);
             atomicAdd(&job.counters[PT_CNT_ESCAPED], n_esc);
             atomicAdd(&job.counters[PT_CNT_PRIMARY], n_prim);
+#if PT_DIAG
+            for (int k = 0; k < 7; ++k) atomicAdd(&job.counters[PT_CNT_N + k], dg[k]);
+            const unsigned long long t_death = __builtin_amdgcn_s_memtime();
+            atomicAdd(&job.counters[PT_CNT_N + 7], t_death - t_birth);      // wave lifetimes
+            const unsigned long long r_death = __builtin_amdgcn_s_memrealtime();
+            atomicAdd(&job.counters[PT_CNT_N + 10], r_death - r_birth);      // 100 MHz ticks
+            atomicMax(&job.counters[PT_CNT_N + 8], r_birth);                 // last wave start
+            atomicMin(&job.counters[PT_CNT_N + 9], r_death);                 // first wave end
+            atomicMax(&job.counters[PT_CNT_N + 11], r_death);                // last wave end
+            atomicMin(&job.counters[PT_CNT_N + 12], r_birth);                // first wave start
+            unsigned long long* rec = job.counters + 32 + 4 * (size_t)(blockIdx.x * kWavesPerBlock + wv);
+            rec[0] = r_birth;
+            rec[1] = r_death;
+            rec[2] = n_tiles_diag;
+            rec[3] = n_iter;
+#endif
         }
     }
 }
@@ -606,25 +748,28 @@ __global__ __launch_bounds__(256) PT_KERNEL_ATTR void pt_render_kernel(PtJob job
 template <typename K>
 int resident_blocks(K kern)
 {
-    static int cache[64][2];   // [device][0: blocks per CU, 1: CUs]
+    struct Entry {
+        const void* kern;
+        int dev, blocks;
+    };
+    static Entry cache[64];   // (kernel, device) -> resident blocks; one entry per instantiation
+    static int used = 0;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
-    if (cache[dev][0] == 0) {
-        int nb = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, 0) != hipSuccess || nb <= 0) nb = 4;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        cache[dev][0] = nb;
-        cache[dev][1] = cus;
-    }
-    return cache[dev][0] * cache[dev][1];
+    if (hipGetDevice(&dev) != hipSuccess) return 1024;
+    for (int i = 0; i < used; ++i)
+        if (cache[i].kern == (const void*)kern && cache[i].dev == dev) return cache[i].blocks;
+    int nb = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, 0) != hipSuccess || nb <= 0) nb = 4;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (used < 64) cache[used++] = Entry{(const void*)kern, dev, nb * cus};
+    return nb * cus;
 }
 
 template <int LAYOUT, bool ENV>
 hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 {
     const unsigned tiles = (unsigned)((job.ncols + 7) / 8) * (unsigned)((job.nrows + 7) / 8);
-    hipError_t e = hipMemsetAsync(job.queue, 0, sizeof(unsigned), st);
+    hipError_t e = hipMemsetAsync(job.queue, 0, PT_QUEUE_WORDS * sizeof(unsigned), st);
     if (e != hipSuccess) return e;
     if (count) {
         auto k = pt_render_kernel<LAYOUT, ENV, true>;
@@ -638,7 +783,110 @@ hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
     return hipGetLastError();
 }
 
+// The schedule of the next launch from this launch's per-tile costs (trace iterations + 1), one
+// workgroup, O(tiles) with coalesced loads:
+//   (1) counting sort of the tiles by descending cost (costs capped at kCostBins - 1);
+//   (2) units: inside the run of tiles of equal cost c, consecutive groups of max(1, kUnitCost / c)
+//       tiles -- expensive tiles are units of their own, cheap ones are dequeued in runs.  Built
+//       from the histogram alone (no per-tile prefix pass).
+constexpr int kCostBins = 1024;
+constexpr uint32_t kUnitCost = 12;
+static_assert(kCostBins == 1024, "the schedule kernel scans one histogram bin per thread");
+
+// In-place exclusive scan of a[0..1023] by a 1024-thread workgroup (one entry per thread);
+// returns the total.  Wave-level shuffles, then the 16 wave totals.
+__device__ uint32_t block_exclusive_scan_1024(uint32_t* a, uint32_t* wave_tot)
+{
+    const uint32_t t = threadIdx.x, ln = t & 63, w = t >> 6;
+    const uint32_t v = a[t];
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (ln >= (uint32_t)d) x += y;
+    }
+    if (ln == 63) wave_tot[w] = x;
+    __syncthreads();
+    if (t == 0) {
+        uint32_t run = 0;
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t c = wave_tot[k];
+            wave_tot[k] = run;
+            run += c;
+        }
+        wave_tot[16] = run;
+    }
+    __syncthreads();
+    a[t] = wave_tot[w] + x - v;
+    const uint32_t total = wave_tot[16];
+    __syncthreads();
+    return total;
+}
+
+__global__ __launch_bounds__(1024) void pt_schedule_kernel(const uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
+                                                           uint32_t* __restrict__ units, uint32_t* __restrict__ nunits,
+                                                           uint32_t n)
+{
+    __shared__ uint32_t hist[kCostBins];    // tiles per bin, then the bin's first schedule position
+    __shared__ uint32_t ucnt[kCostBins];    // units per bin, then the bin's first unit index
+    __shared__ uint32_t wave_tot[17];
+    const uint32_t t = threadIdx.x;
+    constexpr uint32_t nt = 1024, kBatch = 8;
+    constexpr uint32_t kNoBin = 0xffffffffu;
+    hist[t] = 0;
+    __syncthreads();
+    auto bin_at = [&](uint32_t i) {   // descending cost: the most expensive tiles get bin 0
+        if (i >= n) return kNoBin;
+        const uint32_t c = cost[i];
+        return (uint32_t)(kCostBins - 1) - (c < (uint32_t)(kCostBins - 1) ? c : (uint32_t)(kCostBins - 1));
+    };
+    for (uint32_t base = 0; base < n; base += nt * kBatch) {
+        uint32_t b[kBatch];
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k) b[k] = bin_at(base + k * nt + t);   // loads in flight together
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k)
+            if (b[k] != kNoBin) atomicAdd(&hist[b[k]], 1u);
+    }
+    __syncthreads();
+    const uint32_t count = hist[t];   // bin t
+    block_exclusive_scan_1024(hist, wave_tot);
+    const uint32_t first_pos = hist[t];
+    // units of bin t: cost c = kCostBins - 1 - t, k = max(1, U / c) tiles each
+    const uint32_t c = (uint32_t)(kCostBins - 1) - t;
+    const uint32_t per = c >= kUnitCost || c == 0 ? 1u : kUnitCost / c;
+    ucnt[t] = (count + per - 1) / per;
+    __syncthreads();
+    const uint32_t total_units = block_exclusive_scan_1024(ucnt, wave_tot);
+    {
+        const uint32_t u0 = ucnt[t];
+        for (uint32_t j = 0, p = first_pos; p < first_pos + count; ++j, p += per) units[u0 + j] = p;
+    }
+    if (t == 0) {
+        *nunits = total_units;
+        units[total_units] = n;
+    }
+    // scatter: order[position] = tile (positions inside a bin in arbitrary order)
+    for (uint32_t base = 0; base < n; base += nt * kBatch) {
+        uint32_t b[kBatch];
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k) b[k] = bin_at(base + k * nt + t);
+#pragma unroll
+        for (uint32_t k = 0; k < kBatch; ++k)
+            if (b[k] != kNoBin) order[atomicAdd(&hist[b[k]], 1u)] = base + k * nt + t;
+    }
+}
+
 }  // namespace
+
+hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* units, uint32_t* nunits,
+                              uint32_t ntiles, hipStream_t st)
+{
+    if (ntiles == 0) return hipSuccess;
+    if (!cost || !order || !units || !nunits) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pt_schedule_kernel, dim3(1), dim3(1024), 0, st, cost, order, units, nunits, ntiles);
+    return hipGetLastError();
+}
 
 hipError_t pt_launch_render(const PtJob& job, hipStream_t st, bool count)
 {

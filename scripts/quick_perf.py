@@ -13,7 +13,13 @@ if ENV:
     from cpuperformanceraytracer_amd.device import set_env_map
     set_env_map(synthetic_env(), 0, B)
 buf = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
+count_device(buf, W, H, frame_first=1, nframes=S, num_bounces=B, use_env=ENV)   # warm
+c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+c0.record()
 cnt = count_device(buf, W, H, frame_first=1, nframes=S, num_bounces=B, use_env=ENV)
+c1.record()
+torch.cuda.synchronize()
+count_ms = c0.elapsed_time(c1)
 for i in range(3):
     render_device(buf, W, H, frame_first=1 + S * (i + 1), nframes=S, num_bounces=B, use_env=ENV)
 torch.cuda.synchronize()
@@ -28,4 +34,4 @@ print(json.dumps({"lib": __import__("os").environ.get("PT_MI355_LIB", "default")
                   "primary_samples_per_s": W * H * S / ms * 1e3, "ray_samples_per_s": W * H * S * B / ms * 1e3,
                   "segments_per_sample": cnt["segments"] / cnt["samples"],
                   "ref_segments_per_sample": (cnt["segments"] - cnt["primary"]) / cnt["samples"] + 1,
-                  "simd_eff": cnt["segments"] / cnt["lane_slots"], "counts": cnt}))
+                  "simd_eff": cnt["segments"] / cnt["lane_slots"], "counts": cnt, "count_launch_ms": count_ms}))
