@@ -250,7 +250,7 @@ def main() -> None:
             "unit": "TFLOP/s",
             "frac": achieved_tf / RL.PEAK_FP32_TFLOPS,
             "traffic": hbm_launch,
-            "kernel": f"pt_render_kernel<INTERLEAVED, ENV={int(wl.env)}>",
+            "kernel": "pt_render_env_kernel<INTERLEAVED>" if wl.env else "pt_render_kernel<INTERLEAVED>",
             "flops_per_launch": flops_launch,
             "flop_model": "executed = (segments_ref x F_SEGMENT + samples x F_SAMPLE) - (samples - pixels) x "
                           f"F_SHARED; F = {RL.F_SEGMENT}/{RL.F_SAMPLE}/{RL.F_SHARED} (roofline.py)",

@@ -46,9 +46,6 @@
 #ifndef PT_AXIS_FROM_LDS
 #define PT_AXIS_FROM_LDS 1   // 0: select from literals (177 VGPRs, 0.89 ms) vs LDS row (127, 0.79 ms)
 #endif
-#ifndef PT_KERNEL_ATTR
-#define PT_KERNEL_ATTR
-#endif
 #ifndef PT_TRACE_UNROLL
 #define PT_TRACE_UNROLL 6   // primitive loops fully unrolled: the constexpr geometry becomes
 #endif                      // instruction literals (rolled: 1.05 ms vs 0.81 ms per 1080p step)
@@ -390,7 +387,7 @@ constexpr int kWavesPerBlock = 4;
 //      whose camera ray missed / of c_numBounces = 0).
 // Tiles come from a per-launch atomic queue (persistent waves, next tile prefetched).
 template <int LAYOUT, bool ENV, bool COUNT>
-__global__ __launch_bounds__(256) PT_KERNEL_ATTR void pt_render_kernel(PtJob job)
+__device__ __forceinline__ void render_body(const PtJob& job)
 {
     const PtScene* __restrict__ sc = job.scene;
     __shared__ PtLdsPrim s_prim[PT_NPRIMS];
@@ -742,6 +739,27 @@ __global__ __launch_bounds__(256) PT_KERNEL_ATTR void pt_render_kernel(PtJob job
     }
 }
 
+// Kernel entry points.  The ambient kernel is held to 96 VGPRs (5 waves per SIMD; measured
+// 4 % faster than 4 waves at 106); the env-map kernel needs ~116 and runs at 4.
+template <int LAYOUT, bool COUNT>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void pt_render_kernel(PtJob job)
+{
+    render_body<LAYOUT, false, COUNT>(job);
+}
+
+template <int LAYOUT, bool COUNT>
+__global__ __launch_bounds__(256) void pt_render_env_kernel(PtJob job)
+{
+    render_body<LAYOUT, true, COUNT>(job);
+}
+
+template <int LAYOUT, bool ENV, bool COUNT>
+constexpr auto kernel_of()
+{
+    if constexpr (ENV) return pt_render_env_kernel<LAYOUT, COUNT>;
+    else return pt_render_kernel<LAYOUT, COUNT>;
+}
+
 // Persistent grid: as many 256-thread blocks as the device keeps resident (every wave then pulls
 // tiles until the queue is drained), capped by the tile count.  Blocks beyond residency would
 // only find an empty queue, so an over-estimate costs nothing but a launch slot.
@@ -772,11 +790,11 @@ hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
     hipError_t e = hipMemsetAsync(job.queue, 0, PT_QUEUE_WORDS * sizeof(unsigned), st);
     if (e != hipSuccess) return e;
     if (count) {
-        auto k = pt_render_kernel<LAYOUT, ENV, true>;
+        auto k = kernel_of<LAYOUT, ENV, true>();
         const unsigned blocks = (unsigned)std::min<long>(resident_blocks(k), (tiles + 3) / 4);
         hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, job);
     } else {
-        auto k = pt_render_kernel<LAYOUT, ENV, false>;
+        auto k = kernel_of<LAYOUT, ENV, false>();
         const unsigned blocks = (unsigned)std::min<long>(resident_blocks(k), (tiles + 3) / 4);
         hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, job);
     }

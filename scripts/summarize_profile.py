@@ -27,7 +27,7 @@ src = ROOT / "gpurun_out" / "prof" / tag
 dst = ROOT / "profiles"
 dst.mkdir(exist_ok=True)
 ENV = workload.startswith("c4")
-KERNEL = f"pt_render_kernel<0, {'true' if ENV else 'false'}, false>"
+KERNEL = "pt_render_env_kernel<0, false>" if ENV else "pt_render_kernel<0, false>"
 SUMMARY = "pmc_summary.json" if workload == "c2_1080p" else f"pmc_summary_{workload}.json"
 
 stats = glob.glob(str(src / "trace" / "**" / "*kernel_stats.csv"), recursive=True)
