@@ -45,7 +45,9 @@ struct PtJob {
 };
 
 // Tile queues: one counter per XCD group, 128 B apart (PT_QUEUE_WORDS u32 per launch).
+#ifndef PT_NQUEUES
 #define PT_NQUEUES 8
+#endif
 #define PT_QUEUE_WORDS (PT_NQUEUES * 32)
 
 // Enqueue one render launch on `stream`.  Returns hipSuccess or the launch error.
