@@ -23,6 +23,7 @@ PT_LAYOUT_PLANAR8 = 1
 PT_LAYOUT_TILED_PLANAR8 = 2
 
 PT_FLAG_DEFER_READBACK = 1
+PT_FLAG_PIN_HOST = 2
 
 # Every symbol include/pt_mi355.h declares (tests/test_abi.py checks they are all exported).
 EXPORTED_SYMBOLS = (

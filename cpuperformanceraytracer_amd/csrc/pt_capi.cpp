@@ -35,6 +35,7 @@ struct Sched {
     unsigned long long last_use = 0;
 };
 constexpr int kSchedSlots = 16;
+constexpr int kBands = 4;   // PT_FLAG_PIN_HOST: row bands of a pipelined frame
 constexpr uint32_t kSchedMinTiles = 512;   // smaller jobs (e.g. one RenderTile) are not scheduled
 #ifndef PT_SCHED_REBUILD
 #define PT_SCHED_REBUILD 16
@@ -63,6 +64,11 @@ struct State {
     const float* env_src = nullptr;     // host data the device copy was made from
     Sched sched[kSchedSlots];
     unsigned long long sched_clock = 0;
+    // PT_FLAG_PIN_HOST: the registered host buffer, copy streams and band events
+    const float* pinned = nullptr;
+    size_t pinned_bytes = 0;
+    hipStream_t s_in = nullptr, s_out = nullptr;
+    hipEvent_t ev_in[kBands] = {}, ev_done[kBands] = {};
 };
 
 State g;
@@ -258,6 +264,72 @@ int launch(PtJob j, hipStream_t st, bool count)
     return PT_OK;
 }
 
+void unpin()
+{
+    if (g.pinned) {
+        (void)hipDeviceSynchronize();
+        (void)hipHostUnregister((void*)g.pinned);
+    }
+    g.pinned = nullptr;
+    g.pinned_bytes = 0;
+}
+
+bool pin(const float* p, size_t bytes)
+{
+    if (g.pinned == p && g.pinned_bytes == bytes) return true;
+    unpin();
+    if (hipHostRegister((void*)p, bytes, hipHostRegisterDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;   // e.g. already page-locked by the caller: unpipelined path
+    }
+    g.pinned = p;
+    g.pinned_bytes = bytes;
+    return true;
+}
+
+// One frame call on a host buffer: the job `j` (whole image) is rendered into the device mirror
+// of `buf`.  With PT_FLAG_PIN_HOST (and without deferred readback) the frame is split into
+// kBands row bands (multiples of row_align rows: contiguous in every layout) whose upload,
+// render and download overlap on three streams; otherwise upload, render, download in turn.
+int render_frame(float* buf, PtJob j, int32_t row_align)
+{
+    int rc;
+    const size_t bytes = (size_t)j.width * j.height * 3 * sizeof(float);
+    const uint32_t spf = (uint32_t)g.cfg.samples_per_frame;
+    if ((g.cfg.flags & PT_FLAG_PIN_HOST) && !(g.cfg.flags & PT_FLAG_DEFER_READBACK) && pin(buf, bytes)) {
+        if ((rc = ensure_dbuf(bytes))) return rc;
+        g.mirror_valid = false;
+        g.mirror_host = nullptr;
+        const int32_t w = j.width, h = j.height;
+        int32_t rows = (h + kBands - 1) / kBands;
+        rows = (rows + row_align - 1) / row_align * row_align;
+        int k = 0;
+        for (int32_t r0 = 0; r0 < h && k < kBands; r0 += rows, ++k) {
+            const int32_t r1 = r0 + rows < h ? r0 + rows : h;
+            const size_t off = (size_t)r0 * w * 3, len = (size_t)(r1 - r0) * w * 3 * sizeof(float);
+            HIP_TRY(hipMemcpyAsync(g.dbuf + off, buf + off, len, hipMemcpyHostToDevice, g.s_in));
+            HIP_TRY(hipEventRecord(g.ev_in[k], g.s_in));
+            HIP_TRY(hipStreamWaitEvent(g.stream, g.ev_in[k], 0));
+            PtJob b = j;
+            b.row_start = r0;
+            b.nrows = r1 - r0;
+            b.buf = j.layout == PT_LAYOUT_TILED_PLANAR8 ? g.dbuf : g.dbuf + off;   // tiled: global offsets
+            if ((rc = launch(b, g.stream, false))) return rc;
+            HIP_TRY(hipEventRecord(g.ev_done[k], g.stream));
+            HIP_TRY(hipStreamWaitEvent(g.s_out, g.ev_done[k], 0));
+            HIP_TRY(hipMemcpyAsync(buf + off, g.dbuf + off, len, hipMemcpyDeviceToHost, g.s_out));
+        }
+        g.frame += spf;
+        HIP_TRY(hipStreamSynchronize(g.s_out));
+        return PT_OK;
+    }
+    if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
+    j.buf = g.dbuf;
+    if ((rc = launch(j, g.stream, false))) return rc;
+    g.frame += spf;
+    return stage_out(buf, 0, bytes);
+}
+
 int check_frame_args(const float* buf, int32_t w, int32_t h, int32_t nc)
 {
     if (!buf) return fail(PT_EINVAL, "null buffer");
@@ -354,6 +426,12 @@ int pt_init(const pt_config* cfg)
     if (c.device < 0 || c.device >= ndev) return fail(PT_EHIP, "device %d not available (%d devices)", c.device, ndev);
     HIP_TRY(hipSetDevice(c.device));
     HIP_TRY(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&g.s_in, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&g.s_out, hipStreamNonBlocking));
+    for (int k = 0; k < kBands; ++k) {
+        HIP_TRY(hipEventCreateWithFlags(&g.ev_in[k], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&g.ev_done[k], hipEventDisableTiming));
+    }
     if (hipMalloc(&g.dcounters, kCounterSlots * sizeof(unsigned long long)) != hipSuccess)
         return fail(PT_ENOMEM, "hipMalloc(counters) failed");
     if (hipMalloc(&g.dqueue, (size_t)kQueueSlots * PT_QUEUE_WORDS * sizeof(unsigned)) != hipSuccess)
@@ -379,6 +457,13 @@ void pt_shutdown(void)
     if (g.denv) (void)hipFree(g.denv);
     for (Sched& sc : g.sched)
         if (sc.used) free_sched(sc);
+    unpin();
+    for (int k = 0; k < kBands; ++k) {
+        if (g.ev_in[k]) (void)hipEventDestroy(g.ev_in[k]);
+        if (g.ev_done[k]) (void)hipEventDestroy(g.ev_done[k]);
+    }
+    if (g.s_in) (void)hipStreamDestroy(g.s_in);
+    if (g.s_out) (void)hipStreamDestroy(g.s_out);
     if (g.stream) (void)hipStreamDestroy(g.stream);
     g = State{};
 }
@@ -399,12 +484,7 @@ int pt_render_scalar(float* buf, int32_t w, int32_t h, int32_t nc)
     int rc;
     if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
     if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
-    const size_t bytes = (size_t)w * h * 3 * sizeof(float);
-    if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
-    PtJob j = base_job(g.dbuf, w, h);
-    if ((rc = launch(j, g.stream, false))) return rc;
-    g.frame += (uint32_t)g.cfg.samples_per_frame;
-    return stage_out(buf, 0, bytes);
+    return render_frame(buf, base_job(nullptr, w, h), 8);
 }
 
 int pt_render_simd(float* buf, int32_t w, int32_t h, int32_t nc)
@@ -413,13 +493,9 @@ int pt_render_simd(float* buf, int32_t w, int32_t h, int32_t nc)
     if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
     if (w % 8) return fail(PT_EINVAL, "image width %d must be a multiple of 8 (SIMD lane width)", w);
     if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
-    const size_t bytes = (size_t)w * h * 3 * sizeof(float);
-    if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
-    PtJob j = base_job(g.dbuf, w, h);
+    PtJob j = base_job(nullptr, w, h);
     j.layout = PT_LAYOUT_PLANAR8;
-    if ((rc = launch(j, g.stream, false))) return rc;
-    g.frame += (uint32_t)g.cfg.samples_per_frame;
-    return stage_out(buf, 0, bytes);
+    return render_frame(buf, j, 8);
 }
 
 int pt_render_simd_tiled(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty, int32_t tw, int32_t th, int32_t nc)
@@ -428,15 +504,11 @@ int pt_render_simd_tiled(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t 
     if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
     if ((rc = tiled_settings(w, h, ntx, nty, tw, th))) return rc;
     if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
-    const size_t bytes = (size_t)w * h * 3 * sizeof(float);
-    if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
-    PtJob j = base_job(g.dbuf, w, h);
+    PtJob j = base_job(nullptr, w, h);
     j.layout = PT_LAYOUT_TILED_PLANAR8;
     j.tile_w = tw;
     j.tile_h = th;
-    if ((rc = launch(j, g.stream, false))) return rc;
-    g.frame += (uint32_t)g.cfg.samples_per_frame;
-    return stage_out(buf, 0, bytes);
+    return render_frame(buf, j, th);
 }
 
 int pt_set_env_map(const pt_texture* tex)
@@ -460,18 +532,14 @@ int pt_render_simt_textured(float* buf, int32_t w, int32_t h, int32_t ntx, int32
     if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
     if (!g.denv || g.env_src != tex->data || g.env_w != tex->width || g.env_h != tex->height)
         if ((rc = upload_env(tex))) return rc;
-    const size_t bytes = (size_t)w * h * 3 * sizeof(float);
-    if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
-    PtJob j = base_job(g.dbuf, w, h);
+    PtJob j = base_job(nullptr, w, h);
     j.layout = PT_LAYOUT_TILED_PLANAR8;   // RenderTile, simt_textured.cpp:491-533
     j.tile_w = tw;
     j.tile_h = th;
     j.env = g.denv;
     j.env_w = g.env_w;
     j.env_h = g.env_h;
-    if ((rc = launch(j, g.stream, false))) return rc;
-    g.frame += (uint32_t)g.cfg.samples_per_frame;
-    return stage_out(buf, 0, bytes);
+    return render_frame(buf, j, th);
 }
 
 int pt_begin_frame(void)
@@ -555,12 +623,47 @@ static int device_job(const pt_device_job* dj, PtJob* j)
     return PT_OK;
 }
 
+#if PT_DIAG
+static void diag_dump(const unsigned long long* h)
+{
+    fprintf(stderr, "PT_DIAG cycles: A %llu take %llu dir %llu trace %llu shade %llu C %llu tile %llu\n",
+            h[PT_CNT_N + 0], h[PT_CNT_N + 1], h[PT_CNT_N + 2], h[PT_CNT_N + 3], h[PT_CNT_N + 4], h[PT_CNT_N + 5],
+            h[PT_CNT_N + 6]);
+    fprintf(stderr, "PT_DIAG wave lifetimes %llu memtime ticks, %llu realtime (100 MHz) ticks\n", h[PT_CNT_N + 7],
+            h[PT_CNT_N + 10]);
+    const unsigned long long r0 = h[PT_CNT_N + 12];
+    fprintf(stderr, "PT_DIAG realtime (us from first start): last start %.1f, first end %.1f, last end %.1f\n",
+            (h[PT_CNT_N + 8] - r0) * 0.01, (h[PT_CNT_N + 9] - r0) * 0.01, (h[PT_CNT_N + 11] - r0) * 0.01);
+    if (const char* path = getenv("PT_DIAG_OUT")) {
+        FILE* f = fopen(path, "wb");
+        if (f) {
+            fwrite(h + 32, sizeof(unsigned long long), 4 * 65536 + 96 * 65536, f);
+            fclose(f);
+        }
+    }
+}
+#endif
+
 int pt_render_device(const pt_device_job* dj, void* stream)
 {
     int rc;
     PtJob j;
     if ((rc = ensure_init()) || (rc = device_job(dj, &j))) return rc;
+#if PT_DIAG   // diagnostic build: every device launch records and dumps its timeline (synchronous)
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(g.dcounters, 0, kCounterSlots * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(g.dcounters + PT_CNT_N + 9, 0xff, sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(g.dcounters + PT_CNT_N + 12, 0xff, sizeof(unsigned long long), st));
+    j.counters = g.dcounters;
+    if ((rc = launch(j, st, false))) return rc;
+    static unsigned long long h[kCounterSlots];
+    HIP_TRY(hipMemcpyAsync(h, g.dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    diag_dump(h);
+    return PT_OK;
+#else
     return launch(j, (hipStream_t)stream, false);
+#endif
 }
 
 int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
@@ -581,21 +684,7 @@ int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
     HIP_TRY(hipMemcpyAsync(h, g.dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
 #if PT_DIAG
-    fprintf(stderr, "PT_DIAG cycles: A %llu take %llu dir %llu trace %llu shade %llu C %llu tile %llu\n",
-            h[PT_CNT_N + 0], h[PT_CNT_N + 1], h[PT_CNT_N + 2], h[PT_CNT_N + 3], h[PT_CNT_N + 4], h[PT_CNT_N + 5],
-            h[PT_CNT_N + 6]);
-    fprintf(stderr, "PT_DIAG wave lifetimes %llu memtime ticks, %llu realtime (100 MHz) ticks\n", h[PT_CNT_N + 7],
-            h[PT_CNT_N + 10]);
-    const unsigned long long r0 = h[PT_CNT_N + 12];
-    fprintf(stderr, "PT_DIAG realtime (us from first start): last start %.1f, first end %.1f, last end %.1f\n",
-            (h[PT_CNT_N + 8] - r0) * 0.01, (h[PT_CNT_N + 9] - r0) * 0.01, (h[PT_CNT_N + 11] - r0) * 0.01);
-    if (const char* path = getenv("PT_DIAG_OUT")) {
-        FILE* f = fopen(path, "wb");
-        if (f) {
-            fwrite(h + 32, sizeof(unsigned long long), 4 * 65536 + 96 * 65536, f);
-            fclose(f);
-        }
-    }
+    diag_dump(h);
 #endif
     out->segments = h[PT_CNT_SEGMENTS];
     out->lane_slots = h[PT_CNT_LANE_SLOTS];

@@ -357,10 +357,10 @@ __device__ __forceinline__ V3 miss_radiance(const PtJob& job, V3 amb, V3 d)
 #ifndef PT_DIAG
 #define PT_DIAG 0   // diagnostic build: per-phase shader-clock cycles in counters[5..] (COUNT launches)
 #endif
-#if PT_DIAG
+#if PT_DIAG >= 2   // per-phase cycle counters (heavier: perturbs register allocation)
 #define DIAG_MARK(var) const unsigned long long var = __builtin_amdgcn_s_memtime()
 #define DIAG_ADD(k, t0) \
-    if (COUNT) dg[k] += __builtin_amdgcn_s_memtime() - (t0)
+    dg[k] += __builtin_amdgcn_s_memtime() - (t0)
 #else
 #define DIAG_MARK(var)
 #define DIAG_ADD(k, t0)
@@ -441,7 +441,9 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 
     unsigned long long n_seg = 0, n_iter = 0, n_samp = 0, n_esc = 0, n_prim = 0;
 #if PT_DIAG
+#if PT_DIAG >= 2
     unsigned long long dg[7] = {0, 0, 0, 0, 0, 0, 0};   // A, take, dir, trace, shade, C, tile-total
+#endif
     const unsigned long long t_birth = __builtin_amdgcn_s_memtime();
     const unsigned long long r_birth = __builtin_amdgcn_s_memrealtime();
     unsigned long long n_tiles_diag = 0;
@@ -697,7 +699,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         }
         if (job.cost && lane == 0) job.cost[this_tile] = tile_work;
 #if PT_DIAG
-        if (COUNT && lane == 0 && n_tiles_diag <= 32) {
+        if (job.counters && lane == 0 && n_tiles_diag <= 32) {
             unsigned long long* tl = job.counters + 32 + 4 * 65536 + 96 * (size_t)(blockIdx.x * kWavesPerBlock + wv);
             tl[3 * (n_tiles_diag - 1) + 0] = r_tile0;
             tl[3 * (n_tiles_diag - 1) + 1] = __builtin_amdgcn_s_memrealtime();
@@ -719,8 +721,13 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             atomicAdd(&job.counters[PT_CNT_SAMPLES], n_samp);
             atomicAdd(&job.counters[PT_CNT_ESCAPED], n_esc);
             atomicAdd(&job.counters[PT_CNT_PRIMARY], n_prim);
+        }
+    }
 #if PT_DIAG
+    if (job.counters && lane == 0) {
+#if PT_DIAG >= 2
             for (int k = 0; k < 7; ++k) atomicAdd(&job.counters[PT_CNT_N + k], dg[k]);
+#endif
             const unsigned long long t_death = __builtin_amdgcn_s_memtime();
             atomicAdd(&job.counters[PT_CNT_N + 7], t_death - t_birth);      // wave lifetimes
             const unsigned long long r_death = __builtin_amdgcn_s_memrealtime();
@@ -734,15 +741,18 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             rec[1] = r_death;
             rec[2] = n_tiles_diag;
             rec[3] = n_iter;
-#endif
-        }
     }
+#endif
 }
 
 // Kernel entry points.  The ambient kernel is held to 96 VGPRs (5 waves per SIMD; measured
 // 4 % faster than 4 waves at 106); the env-map kernel needs ~116 and runs at 4.
+#ifndef PT_AMBIENT_WAVES
+#define PT_AMBIENT_WAVES 5
+#endif
 template <int LAYOUT, bool COUNT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 5))) void pt_render_kernel(PtJob job)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT_AMBIENT_WAVES, PT_AMBIENT_WAVES))) void
+pt_render_kernel(PtJob job)
 {
     render_body<LAYOUT, false, COUNT>(job);
 }

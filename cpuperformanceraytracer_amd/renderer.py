@@ -37,17 +37,18 @@ def _buf(a: np.ndarray, width: int, height: int, num_channels: int) -> int:
 
 
 def init(num_bounces: int = 4, samples_per_frame: int = 1, ambient=(0.1, 0.1, 0.1), device: int = 0,
-         defer_readback: bool = False) -> None:
+         defer_readback: bool = False, pin_host: bool = False) -> None:
     """(Re)initialise the backend: the runtime form of the reference's compile-time settings
     (c_numBounces scalar.cpp:19, NUM_SAMPLES_PER_FRAME global_preprocessor_flags.h:30).
-    Resets the frame counter to 0, like a fresh process of the reference."""
+    Resets the frame counter to 0, like a fresh process of the reference.
+    pin_host: page-lock the frame buffer and overlap its transfers with rendering (row bands)."""
     L = N.load()
     c = N.PtConfig()
     L.pt_default_config(ctypes.byref(c))
     c.device = device
     c.num_bounces = num_bounces
     c.samples_per_frame = samples_per_frame
-    c.flags = N.PT_FLAG_DEFER_READBACK if defer_readback else 0
+    c.flags = (N.PT_FLAG_DEFER_READBACK if defer_readback else 0) | (N.PT_FLAG_PIN_HOST if pin_host else 0)
     for i in range(3):
         c.ambient[i] = float(ambient[i])
     N.check(L.pt_init(ctypes.byref(c)), "pt_init")

@@ -37,6 +37,9 @@ extern "C" {
 
 #define PT_FLAG_DEFER_READBACK 1u  /* keep the accumulator in HBM between frame calls: no H2D/D2H;    */
                                    /* the host buffer is refreshed only by pt_readback().            */
+#define PT_FLAG_PIN_HOST 2u        /* page-lock the caller's frame buffer (hipHostRegister; kept until */
+                                   /* pt_shutdown or another buffer is passed) and overlap its PCIe  */
+                                   /* transfers with rendering, in row bands (same results).         */
 
 /* Runtime form of the reference's compile-time configuration (global_preprocessor_flags.h and the
  * file-scope constants of demofox_path_tracing_scalar.cpp:6-25). */

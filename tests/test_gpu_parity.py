@@ -192,3 +192,26 @@ def test_low_bounce_counts_vs_oracle(b):
     pt.DemofoxRenderScalar(buf, w, h, 3)
     ref = pyoracle.render(w, h, nframes=f, num_bounces=b)
     assert bits_equal(buf, ref), mismatch_report(buf, ref)
+
+
+def test_pinned_pipelined_frames():
+    """PT_FLAG_PIN_HOST: the frame is uploaded, rendered and downloaded in 4 overlapping row bands
+    -- every layout equals the oracle bit for bit, frame after frame."""
+    pt.init(num_bounces=8, samples_per_frame=2, pin_host=True)
+    w, h = 640, 384
+    a = np.zeros((h, w, 3), np.float32)
+    for _ in range(3):
+        pt.DemofoxRenderScalar(a, w, h, 3)
+    ref = pyoracle.render(w, h, nframes=6, num_bounces=8)
+    assert bits_equal(a, ref), mismatch_report(a, ref)
+    pt.init(num_bounces=8, samples_per_frame=2, pin_host=True)
+    b = np.zeros(w * h * 3, np.float32)
+    for _ in range(3):
+        pt.DemofoxRenderSimd(b, w, h, 3)
+    assert bits_equal(planar8_to_interleaved(b, w, h), ref)
+    pt.init(num_bounces=8, samples_per_frame=2, pin_host=True)
+    c = np.zeros(w * h * 3, np.float32)
+    for _ in range(3):
+        pt.DemofoxRenderSimdTiled(c, w, h, 5, 8, 128, 48, 3)
+    assert bits_equal(tiled_to_interleaved(c, w, h, 128, 48), ref)
+    pt.shutdown()
