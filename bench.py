@@ -114,6 +114,33 @@ def load_traffic(workload: str):
     return d.get("hbm_bytes_per_launch"), d.get("source")
 
 
+def measure_output_stage(buf, W: int, H: int, stream) -> dict:
+    """the output stage (ACES + sRGB + 8-bit pack, v4 :1260-1331) on this
+    rank's accumulator -- an HBM-bound pass: 12 B read + 4 B written per pixel."""
+    import ctypes
+    import torch
+    from cpuperformanceraytracer_amd import _native as N
+    from cpuperformanceraytracer_amd import roofline as RL
+    out = torch.empty(W * H, dtype=torch.int32, device=buf.device)
+    L = N.load()
+    args = (buf.data_ptr(), W, H, N.PT_LAYOUT_INTERLEAVED, 0, 0, out.data_ptr(), N.PT_PIXEL_RGBA8,
+            ctypes.c_void_p(stream.cuda_stream))
+    for _ in range(3):
+        N.check(L.pt_tonemap_device(*args), "pt_tonemap_device")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 20
+    e0.record(stream)
+    for _ in range(reps):
+        L.pt_tonemap_device(*args)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    nbytes = 16 * W * H
+    return {"kernel": "pt_tonemap_kernel<INTERLEAVED>", "pixels": W * H, "ms": ms,
+            "bound": "hbm", "achieved_gbps": nbytes / (ms * 1e-3) / 1e9, "peak_gbps": RL.PEAK_HBM_GBPS,
+            "frac": nbytes / (ms * 1e-3) / 1e9 / RL.PEAK_HBM_GBPS, "bytes": nbytes}
+
+
 def main() -> None:
     args = parse()
     import torch
@@ -203,6 +230,8 @@ def main() -> None:
         prim += c["primary"]
     del scratch
 
+    output_stage = measure_output_stage(buf, W, H, stream) if rank == 0 else None
+
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -264,6 +293,7 @@ def main() -> None:
     }
     if world > 1:
         res["gather_ms"] = gather_ms
+    res["output_stage"] = output_stage
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, env)
     print(json.dumps(res))

@@ -10,6 +10,7 @@ torgeiba/CPUPerformanceRayTracer (demofox_path_tracing_scalar.cpp / _simd.cpp / 
 from .config import CONFIGS, Workload, check_valid_settings  # noqa: F401
 from .renderer import (  # noqa: F401
     BeginFrame,
+    CopyOutputToFile,
     DemofoxRenderScalar,
     DemofoxRenderSimd,
     DemofoxRenderSimdTiled,
@@ -26,10 +27,12 @@ from .renderer import (  # noqa: F401
     set_frame,
     shutdown,
     texture,
+    tonemap,
+    WriteImage,
 )
 
 __all__ = [
-    "CONFIGS", "Workload", "check_valid_settings", "BeginFrame", "DemofoxRenderScalar", "DemofoxRenderSimd",
+    "CONFIGS", "Workload", "check_valid_settings", "BeginFrame", "CopyOutputToFile", "DemofoxRenderScalar", "DemofoxRenderSimd",
     "DemofoxRenderSimdTiled", "DemofoxRenderSimtTextured", "LoadTexture", "RenderBufferInfo", "RenderTile", "RenderTileInfo", "get_frame", "init",
-    "make_tiles", "readback", "set_env_map", "set_frame", "shutdown", "texture",
+    "make_tiles", "readback", "set_env_map", "set_frame", "shutdown", "texture", "tonemap", "WriteImage",
 ]

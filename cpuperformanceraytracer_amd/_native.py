@@ -25,12 +25,16 @@ PT_LAYOUT_TILED_PLANAR8 = 2
 PT_FLAG_DEFER_READBACK = 1
 PT_FLAG_PIN_HOST = 2
 
+PT_PIXEL_RGBA8 = 0
+PT_PIXEL_XRGB8 = 1
+
 # Every symbol include/pt_mi355.h declares (tests/test_abi.py checks they are all exported).
 EXPORTED_SYMBOLS = (
     "pt_init", "pt_shutdown", "pt_last_error", "pt_default_config", "pt_set_frame", "pt_get_frame",
     "pt_render_scalar", "pt_render_simd", "pt_render_simd_tiled", "pt_render_tile", "pt_begin_frame",
     "pt_readback", "pt_render_device", "pt_count_device",
     "pt_load_texture", "pt_decode_hdr", "pt_free_texture", "pt_set_env_map", "pt_render_simt_textured",
+    "pt_tonemap", "pt_tonemap_device", "pt_write_bmp",
 )
 
 
@@ -90,6 +94,13 @@ def load() -> ctypes.CDLL:
     path = lib_path()
     if not path.exists():
         raise FileNotFoundError(f"{path} not built: run `python -m cpuperformanceraytracer_amd.build`")
+    # One HIP runtime per process: the ROCm PyTorch wheel bundles its own libamdhip64.so.7 (same
+    # soname as /opt/rocm's).  Loaded first, torch's copy is the one this library binds to; loaded
+    # after /opt/rocm's, torch finds no GPU.  So torch (when installed) is imported before dlopen.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(str(path))
     i32, u32, vp = ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p
     sig = {
@@ -112,6 +123,9 @@ def load() -> ctypes.CDLL:
         "pt_free_texture": (None, [ctypes.POINTER(PtTexture)]),
         "pt_set_env_map": (i32, [ctypes.POINTER(PtTexture)]),
         "pt_render_simt_textured": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, ctypes.POINTER(PtTexture)]),
+        "pt_tonemap": (i32, [vp, i32, i32, i32, i32, i32, vp, i32]),
+        "pt_tonemap_device": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, vp]),
+        "pt_write_bmp": (i32, [ctypes.c_char_p, i32, i32, i32, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

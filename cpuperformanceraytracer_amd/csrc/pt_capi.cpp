@@ -8,6 +8,7 @@
 //     as PT_EINVAL instead of __debugbreak();
 //   - the caller owns the host buffer, the call returns after it is updated (Application.cpp:474).
 #include "pt_kernel.h"
+#include "pt_output.h"
 #include "../../include/pt_mi355.h"
 #include <stdarg.h>
 #include <stdio.h>
@@ -69,6 +70,11 @@ struct State {
     size_t pinned_bytes = 0;
     hipStream_t s_in = nullptr, s_out = nullptr;
     hipEvent_t ev_in[kBands] = {}, ev_done[kBands] = {};
+    // output stage scratch (host-buffer pt_tonemap)
+    float* dtone_in = nullptr;
+    size_t dtone_in_cap = 0;
+    uint32_t* dtone_out = nullptr;
+    size_t dtone_out_cap = 0;
 };
 
 State g;
@@ -330,6 +336,39 @@ int render_frame(float* buf, PtJob j, int32_t row_align)
     return stage_out(buf, 0, bytes);
 }
 
+int grow(void** p, size_t* cap, size_t bytes)
+{
+    if (bytes <= *cap) return PT_OK;
+    if (*p) {
+        HIP_TRY(hipStreamSynchronize(g.stream));
+        (void)hipFree(*p);
+        *p = nullptr;
+        *cap = 0;
+    }
+    if (hipMalloc(p, bytes) != hipSuccess) {
+        *p = nullptr;
+        return fail(PT_ENOMEM, "hipMalloc(%zu) failed", bytes);
+    }
+    *cap = bytes;
+    return PT_OK;
+}
+
+// the accumulator geometry the output stage accepts (the layouts' own constraints)
+int check_tone_args(const void* accum, const void* out, int32_t w, int32_t h, int32_t layout, int32_t tw, int32_t th,
+                    int32_t format)
+{
+    if (!accum || !out) return fail(PT_EINVAL, "null accumulator/output");
+    if (w <= 0 || h <= 0 || (int64_t)w * h > (int64_t)1 << 30) return fail(PT_EINVAL, "invalid size %dx%d", w, h);
+    if (format != PT_PIXEL_RGBA8 && format != PT_PIXEL_XRGB8) return fail(PT_EINVAL, "unknown pixel format %d", format);
+    if (layout == PT_LAYOUT_INTERLEAVED) return PT_OK;
+    if (w % 8) return fail(PT_EINVAL, "planar layouts need width %% 8 == 0 (got %d)", w);
+    if (layout == PT_LAYOUT_PLANAR8) return PT_OK;
+    if (layout != PT_LAYOUT_TILED_PLANAR8) return fail(PT_EINVAL, "unknown layout %d", layout);
+    if (tw <= 0 || th <= 0 || tw % 8 || w % tw || h % th)
+        return fail(PT_EINVAL, "tiles %dx%d do not divide %dx%d (tile width multiple of 8)", tw, th, w, h);
+    return PT_OK;
+}
+
 int check_frame_args(const float* buf, int32_t w, int32_t h, int32_t nc)
 {
     if (!buf) return fail(PT_EINVAL, "null buffer");
@@ -455,6 +494,8 @@ void pt_shutdown(void)
     if (g.dscene) (void)hipFree(g.dscene);
     if (g.dqueue) (void)hipFree(g.dqueue);
     if (g.denv) (void)hipFree(g.denv);
+    if (g.dtone_in) (void)hipFree(g.dtone_in);
+    if (g.dtone_out) (void)hipFree(g.dtone_out);
     for (Sched& sc : g.sched)
         if (sc.used) free_sched(sc);
     unpin();
@@ -643,6 +684,40 @@ static void diag_dump(const unsigned long long* h)
     }
 }
 #endif
+
+int pt_tonemap_device(const float* accum, int32_t w, int32_t h, int32_t layout, int32_t tw, int32_t th, uint32_t* out,
+                      int32_t format, void* stream)
+{
+    int rc;
+    if ((rc = ensure_init()) || (rc = check_tone_args(accum, out, w, h, layout, tw, th, format))) return rc;
+    const PtToneJob j{accum, w, h, layout, tw, th, out, format};
+    hipError_t e = pt_launch_tonemap(j, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(PT_EHIP, "tonemap launch failed: %s", hipGetErrorString(e));
+    return PT_OK;
+}
+
+int pt_tonemap(const float* accum, int32_t w, int32_t h, int32_t layout, int32_t tw, int32_t th, uint32_t* out,
+               int32_t format)
+{
+    int rc;
+    if ((rc = ensure_init()) || (rc = check_tone_args(accum, out, w, h, layout, tw, th, format))) return rc;
+    const size_t in_bytes = (size_t)w * h * 3 * sizeof(float), out_bytes = (size_t)w * h * sizeof(uint32_t);
+    const float* src = nullptr;
+    if (g.mirror_valid && accum == g.mirror_host && g.mirror_bytes == in_bytes) {
+        src = g.dbuf;   // the deferred accumulator is already in HBM
+    } else {
+        if ((rc = grow((void**)&g.dtone_in, &g.dtone_in_cap, in_bytes))) return rc;
+        HIP_TRY(hipMemcpyAsync(g.dtone_in, accum, in_bytes, hipMemcpyHostToDevice, g.stream));
+        src = g.dtone_in;
+    }
+    if ((rc = grow((void**)&g.dtone_out, &g.dtone_out_cap, out_bytes))) return rc;
+    const PtToneJob j{src, w, h, layout, tw, th, g.dtone_out, format};
+    hipError_t e = pt_launch_tonemap(j, g.stream);
+    if (e != hipSuccess) return fail(PT_EHIP, "tonemap launch failed: %s", hipGetErrorString(e));
+    HIP_TRY(hipMemcpyAsync(out, g.dtone_out, out_bytes, hipMemcpyDeviceToHost, g.stream));
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    return PT_OK;
+}
 
 int pt_render_device(const pt_device_job* dj, void* stream)
 {

@@ -61,3 +61,22 @@ void DemofoxRenderSimtTextured(f32* BufferOut, i32 BufferWidth, i32 BufferHeight
                                      NumChannels, &p),
              "DemofoxRenderSimtTextured");
 }
+
+void CopyOutputToFile(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY, i32 TileWidth,
+                      i32 TileHeight, i32 NumChannels, texture Texture, void* ScreenBufferData)
+{
+    (void)Texture;
+    if (NumChannels != 3 || NumTilesX * TileWidth != BufferWidth || NumTilesY * TileHeight != BufferHeight) {
+        fprintf(stderr, "CopyOutputToFile: invalid settings\n");
+        abort();
+    }
+    pt_check(pt_tonemap(BufferOut, BufferWidth, BufferHeight, PT_LAYOUT_TILED_PLANAR8, TileWidth, TileHeight,
+                        (uint32_t*)ScreenBufferData, PT_PIXEL_RGBA8),
+             "CopyOutputToFile");
+}
+
+void WriteImage(char* filename, i32 width, i32 height, i32 components, void* data)
+{
+    if (pt_write_bmp(filename, width, height, components, data) != PT_OK)   // stbi_write_bmp: no abort
+        fprintf(stderr, "WriteImage: %s\n", pt_last_error());
+}

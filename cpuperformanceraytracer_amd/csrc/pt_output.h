@@ -1,0 +1,18 @@
+// pt_output.h -- internal interface of the output-stage kernel (pt_output.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "pt_kernel.h"
+
+#include "../../include/pt_mi355.h"   // PT_PIXEL_RGBA8 / PT_PIXEL_XRGB8
+
+struct PtToneJob {
+    const float* accum;       // device accumulator (PtLayout)
+    int32_t width, height;
+    int32_t layout;
+    int32_t tile_w, tile_h;   // PT_LAYOUT_TILED_PLANAR8
+    uint32_t* out;            // device, width * height packed pixels, row 0 = top
+    int32_t format;           // PT_PIXEL_*
+};
+
+hipError_t pt_launch_tonemap(const PtToneJob& job, hipStream_t stream);

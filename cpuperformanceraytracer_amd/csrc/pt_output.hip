@@ -1,0 +1,105 @@
+// pt_output.hip -- the output stage: linear HDR accumulator -> 8-bit display / file pixels.
+//
+// Reference (CPUPerformanceRayTracer/demofox_path_tracing_optimization_v4.cpp; the defaults of
+// global_preprocessor_flags.h:62-63, USE_FAST_APPROXIMATE_GAMMA = USE_FAST_APPROXIMATE_ACES_TONEMAP = 1):
+//   OutputToScreen :1260-1295 / OutputToFile :1297-1331, called per tile by CopyOutputToFile
+//   :1729-1760 and the frame loop: ACESFilm :165-175 -> LinearToSRGB :177-186 (fast_pow_gamma
+//   :144-155) -> saturate * 255 -> cvtps_epi32 -> packed u32.
+// One thread per pixel, any accumulator layout; 12 B read + 4 B written per pixel: HBM-bound
+// (fused into no other pass: it runs once per presented frame, not per rendered frame).
+// Numerics: the reference's operations in its order, fmadd/fmsub fused (__builtin_fmaf), sqrt
+// correctly rounded (guarded fast path), MAXPS/MINPS NaN rules, round-to-nearest-even conversion.  `rcp` is
+// _mm256_rcp_ps in the reference, whose table is CPU-model specific; here it is the correctly
+// rounded 1/x (as in the oracle, oracle/pt_oracle_output.c): at most 1 LSB from any x86 run.
+#include "pt_output.h"
+#include "pt_exactmath.h"
+#include <algorithm>
+
+namespace {
+
+__device__ __forceinline__ float max_ps(float a, float b) { return a > b ? a : b; }   // b on NaN / equal
+__device__ __forceinline__ float min_ps(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ float saturate(float x) { return min_ps(max_ps(x, 0.0f), 1.0f); }
+// correctly rounded 1/x and sqrt through the guarded fast paths (bit-identical to IEEE '/' and
+// sqrtf for every input, pt_exactmath.h): ~3x fewer instructions than the general sequences
+__device__ __forceinline__ float rcp(float x) { return pt::div_guarded(1.0f, x); }
+__device__ __forceinline__ float sqrt_(float x) { return pt::sqrt_guarded(x); }
+
+__device__ __forceinline__ float fast_pow_gamma(float x)   // :144-155
+{
+    const float sqrtx = sqrt_(x);
+    const float onethird = 1.f / 3.f, twothirds = 2.f / 3.f;
+    const float nit1 = __builtin_fmaf(sqrtx, twothirds, onethird);
+    const float nit2 = __builtin_fmaf(nit1, twothirds, (x * rcp(nit1 * nit1)) * onethird);
+    const float nit3 = __builtin_fmaf(nit2, twothirds, (x * rcp(nit2 * nit2)) * onethird);
+    return sqrt_(sqrtx * nit3);
+}
+
+__device__ __forceinline__ float aces(float X)   // :165-175 (fast fit)
+{
+    const float a = 2.51f, b = 0.03f, c = 2.43f, d = 0.59f, e = 0.14f;
+    const float rcp_denom = rcp(__builtin_fmaf(X, __builtin_fmaf(c, X, d), e));
+    return saturate((X * __builtin_fmaf(a, X, b)) * rcp_denom);
+}
+
+__device__ __forceinline__ float linear_to_srgb(float x)   // :177-186
+{
+    x = saturate(x);
+    return x < 0.0031308f ? x * 12.92f : __builtin_fmaf(1.055f, fast_pow_gamma(x), -0.055f);
+}
+
+__device__ __forceinline__ uint32_t channel(float linear)
+{
+    const float c_exposure = 1.0f;
+    const float v = saturate(linear_to_srgb(aces(linear * c_exposure))) * 255.f;
+    return (uint32_t)(int32_t)__builtin_rintf(v) & 0xFFu;   // cvtps_epi32 (nearest even) & ByteMask
+}
+
+template <int LAYOUT>
+__global__ __launch_bounds__(256) void pt_tonemap_kernel(PtToneJob j)
+{
+    const uint32_t npix = (uint32_t)j.width * (uint32_t)j.height;
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < npix; p += gridDim.x * blockDim.x) {
+        const uint32_t y = p / (uint32_t)j.width, x = p - y * (uint32_t)j.width;
+        size_t base;
+        size_t cs = 8;   // channel stride
+        if (LAYOUT == PT_LAYOUT_INTERLEAVED) {
+            base = (size_t)p * 3u;
+            cs = 1;
+        } else if (LAYOUT == PT_LAYOUT_PLANAR8) {
+            base = ((size_t)y * j.width + (x & ~7u)) * 3u + (x & 7u);
+        } else {   // tiled planar8 (RenderTile, simd_tiled.cpp:499-531; v4 :1266-1290)
+            const uint32_t tx = x / (uint32_t)j.tile_w, ty = y / (uint32_t)j.tile_h;
+            const uint32_t lx = x - tx * j.tile_w, ly = y - ty * j.tile_h;
+            base = (size_t)ty * j.tile_h * j.width * 3u + (size_t)tx * j.tile_w * j.tile_h * 3u +
+                   ((size_t)ly * j.tile_w + (lx & ~7u)) * 3u + (lx & 7u);
+        }
+        const uint32_t r = channel(j.accum[base]), g = channel(j.accum[base + cs]), b = channel(j.accum[base + 2 * cs]);
+        j.out[p] = j.format == PT_PIXEL_XRGB8 ? ((r << 16) | (g << 8) | b)        // OutputToScreen :1282-1285
+                                              : (0xFF000000u | (b << 16) | (g << 8) | r);   // OutputToFile :1319-1323
+    }
+}
+
+}  // namespace
+
+hipError_t pt_launch_tonemap(const PtToneJob& j, hipStream_t st)
+{
+    if (j.width <= 0 || j.height <= 0) return hipSuccess;
+    if (!j.accum || !j.out) return hipErrorInvalidValue;
+    const long npix = (long)j.width * j.height;
+    const unsigned blocks = (unsigned)std::min<long>((npix + 255) / 256, 256L * 16);
+    switch (j.layout) {
+        case PT_LAYOUT_INTERLEAVED:
+            hipLaunchKernelGGL(pt_tonemap_kernel<PT_LAYOUT_INTERLEAVED>, dim3(blocks), dim3(256), 0, st, j);
+            break;
+        case PT_LAYOUT_PLANAR8:
+            hipLaunchKernelGGL(pt_tonemap_kernel<PT_LAYOUT_PLANAR8>, dim3(blocks), dim3(256), 0, st, j);
+            break;
+        case PT_LAYOUT_TILED_PLANAR8:
+            if (j.tile_w <= 0 || j.tile_h <= 0) return hipErrorInvalidValue;
+            hipLaunchKernelGGL(pt_tonemap_kernel<PT_LAYOUT_TILED_PLANAR8>, dim3(blocks), dim3(256), 0, st, j);
+            break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}

@@ -1,4 +1,5 @@
-// pt_texture.cpp -- the env-map texture of config 4: Radiance RGBE (.hdr) decoding on the host.
+// pt_texture.cpp -- host image I/O: the env-map texture of config 4 (Radiance RGBE .hdr decoding)
+// and the output image (24-bit BMP writing, pt_write_bmp at the end of this file).
 //
 // Replaces LoadTexture (asset_loading.cpp:9-16): stbi_loadf(path, &W, &H, &C, 0) with
 // stbi_set_flip_vertically_on_load(true).  stb_image v2.26 (vendored by the reference,
@@ -181,6 +182,53 @@ int pt_load_texture(const char* path, pt_texture* out)
     while ((got = fread(chunk, 1, sizeof(chunk), f)) > 0) bytes.insert(bytes.end(), chunk, chunk + got);
     fclose(f);
     return pt_decode_hdr(bytes.data(), bytes.size(), out);
+}
+
+// WriteImage (asset_loading.cpp:48-54) = stbi_write_bmp of stb_image_write v1.15
+// (stb_image_write.h:348-521), restated: a 54-byte header ('BM', file size, 0, 0, 54 | 40, w, h,
+// 1 plane, 24 bpp, six zero words), then the rows bottom-up, pixels as B, G, R, each row padded
+// to 4 bytes with zeros.  1/2 components: grey (alpha ignored); 3: RGB; 4: RGB composited over
+// the pink (255, 0, 255) background by alpha with integer arithmetic (opaque pixels unchanged).
+// Checked byte for byte against stb compiled from the reference's sources (tests/test_bmp.py).
+int pt_write_bmp(const char* path, int32_t w, int32_t h, int32_t comp, const void* data)
+{
+    if (!path || (!data && w > 0 && h > 0)) return pt_internal_fail(PT_EINVAL, "null argument");
+    if (w < 0 || h < 0) return pt_internal_fail(PT_EINVAL, "invalid size %dx%d", w, h);
+    if (comp < 1 || comp > 4) return pt_internal_fail(PT_EINVAL, "components must be 1..4, got %d", comp);
+    if ((int64_t)w * h > (int64_t)1 << 30) return pt_internal_fail(PT_EINVAL, "image too large");
+    const int pad = (-w * 3) & 3;
+    const uint32_t row_bytes = (uint32_t)w * 3u + (uint32_t)pad;
+    std::vector<unsigned char> f;
+    f.reserve(54 + (size_t)row_bytes * h);
+    auto u8 = [&](uint32_t v) { f.push_back((unsigned char)v); };
+    auto u16 = [&](uint32_t v) { u8(v & 0xff); u8((v >> 8) & 0xff); };
+    auto u32 = [&](uint32_t v) { u16(v & 0xffff); u16(v >> 16); };
+    u8('B'); u8('M'); u32(14 + 40 + row_bytes * (uint32_t)h); u16(0); u16(0); u32(14 + 40);   // file header
+    u32(40); u32((uint32_t)w); u32((uint32_t)h); u16(1); u16(24);                            // bitmap header
+    for (int k = 0; k < 6; ++k) u32(0);
+    const unsigned char* px = (const unsigned char*)data;
+    const int bg[3] = {255, 0, 255};
+    for (int j = h - 1; j >= 0; --j) {
+        for (int i = 0; i < w; ++i) {
+            const unsigned char* d = px + ((size_t)j * w + i) * comp;
+            if (comp <= 2) {
+                u8(d[0]); u8(d[0]); u8(d[0]);
+            } else if (comp == 3) {
+                u8(d[2]); u8(d[1]); u8(d[0]);
+            } else {
+                unsigned char c[3];
+                for (int k = 0; k < 3; ++k) c[k] = (unsigned char)(bg[k] + ((d[k] - bg[k]) * d[3]) / 255);
+                u8(c[2]); u8(c[1]); u8(c[0]);
+            }
+        }
+        for (int k = 0; k < pad; ++k) u8(0);
+    }
+    FILE* fp = fopen(path, "wb");
+    if (!fp) return pt_internal_fail(PT_EINVAL, "cannot write %s", path);
+    const size_t n = fwrite(f.data(), 1, f.size(), fp);
+    const int closed = fclose(fp);
+    if (n != f.size() || closed != 0) return pt_internal_fail(PT_EINVAL, "short write to %s", path);
+    return PT_OK;
 }
 
 void pt_free_texture(pt_texture* t)

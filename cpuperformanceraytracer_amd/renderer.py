@@ -10,6 +10,9 @@ Same names, argument meaning and error behaviour as the reference's frame functi
   texture / LoadTexture(filename)                                 texture.h:6-12, asset_loading.cpp:9-16
   DemofoxRenderSimtTextured(BufferOut, W, H, NTX, NTY, TW, TH, NC, Texture)
                                                                   demofox_path_tracing_simt_textured.h:8
+  CopyOutputToFile(BufferOut, W, H, NTX, NTY, TW, TH, NC, Texture, ScreenBufferData)
+                                                                  demofox_path_tracing_optimization_v4.h:21
+  WriteImage(filename, width, height, components, data)           asset_loading.h:8
 
 `BufferOut` is a float32 numpy array (the host render target of Application.cpp:142-151).  Each
 frame call advances the frame counter first (the reference's `static f32 iFrame`) and returns after
@@ -203,3 +206,39 @@ def DemofoxRenderSimtTextured(BufferOut: np.ndarray, BufferWidth: int, BufferHei
                                              BufferHeight, NumTilesX, NumTilesY, TileWidth, TileHeight, NumChannels,
                                              ctypes.byref(pt)), "DemofoxRenderSimtTextured")
     del keep
+
+
+def tonemap(accum: np.ndarray, width: int, height: int, layout: int = N.PT_LAYOUT_INTERLEAVED,
+            tile_width: int = 0, tile_height: int = 0, fmt: int = N.PT_PIXEL_RGBA8) -> np.ndarray:
+    """The output stage (v4 :1260-1331): accumulator -> height x width packed u32 pixels
+    (PT_PIXEL_RGBA8: bytes R, G, B, 255; PT_PIXEL_XRGB8: 0x00RRGGBB)."""
+    a = np.ascontiguousarray(accum, dtype=np.float32)
+    if a.size < width * height * 3:
+        raise N.PtError(N.PT_EINVAL, "tonemap", "accumulator smaller than width x height x 3")
+    out = np.empty((height, width), np.uint32)
+    N.check(N.load().pt_tonemap(a.ctypes.data, width, height, layout, tile_width, tile_height, out.ctypes.data, fmt),
+            "pt_tonemap")
+    return out
+
+
+def CopyOutputToFile(BufferOut: np.ndarray, BufferWidth: int, BufferHeight: int, NumTilesX: int, NumTilesY: int,
+                     TileWidth: int, TileHeight: int, NumChannels: int, Texture, ScreenBufferData: np.ndarray) -> None:
+    """v4 :1729-1760 (the post-process it documents): the tiled accumulator -> ScreenBufferData,
+    BufferWidth x BufferHeight u32 file pixels (bytes R, G, B, A = 255)."""
+    if NumChannels != 3 or NumTilesX * TileWidth != BufferWidth or NumTilesY * TileHeight != BufferHeight:
+        raise N.PtError(N.PT_EINVAL, "CopyOutputToFile", "invalid tiling / channels")
+    if (not isinstance(ScreenBufferData, np.ndarray) or ScreenBufferData.dtype != np.uint32
+            or not ScreenBufferData.flags["C_CONTIGUOUS"] or ScreenBufferData.size < BufferWidth * BufferHeight):
+        raise N.PtError(N.PT_EINVAL, "CopyOutputToFile", "ScreenBufferData must be a contiguous uint32 array of W*H")
+    a = _buf(BufferOut, BufferWidth, BufferHeight, 3)
+    N.check(N.load().pt_tonemap(a, BufferWidth, BufferHeight, N.PT_LAYOUT_TILED_PLANAR8, TileWidth, TileHeight,
+                                ScreenBufferData.ctypes.data, N.PT_PIXEL_RGBA8), "CopyOutputToFile")
+
+
+def WriteImage(filename, width: int, height: int, components: int, data: np.ndarray) -> None:
+    """asset_loading.cpp:48-54 (stbi_write_bmp): a 24-bit BMP of width x height pixels of
+    `components` bytes each."""
+    d = np.ascontiguousarray(data)
+    if d.nbytes < width * height * components:
+        raise N.PtError(N.PT_EINVAL, "WriteImage", "data smaller than width x height x components bytes")
+    N.check(N.load().pt_write_bmp(str(filename).encode(), width, height, components, d.ctypes.data), "WriteImage")

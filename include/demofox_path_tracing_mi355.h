@@ -8,6 +8,8 @@
 //   demofox_path_tracing_simd_tiled.cpp:473-489  RenderBufferInfo, RenderTileInfo, RenderTile(&, &)
 //   texture.h:6-12, asset_loading.h:6       struct texture, texture LoadTexture(char*)
 //   demofox_path_tracing_simt_textured.h:8  void DemofoxRenderSimtTextured(f32*, i32 x7, texture)
+//   demofox_path_tracing_optimization_v4.h:21  void CopyOutputToFile(f32*, i32 x7, texture, void*)
+//   asset_loading.h:8                          void WriteImage(char*, i32, i32, i32, void*)
 // Like the reference (which __debugbreak()s on bad settings), these have no error return: on
 // failure they print pt_last_error() to stderr and abort().
 #pragma once
@@ -48,3 +50,12 @@ struct texture {
 texture LoadTexture(char* filename);
 void DemofoxRenderSimtTextured(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY,
                                i32 TileWidth, i32 TileHeight, i32 NumChannels, texture Texture);
+
+// The post-process of the tiled accumulator into 32-bit file pixels (bytes R, G, B, A = 255):
+// ACES + sRGB + 8-bit, v4 :1297-1331.  (The reference's function also advances iFrame and, through
+// its pool's callback mix-up (v4 :1588 vs :1756), re-renders; only the documented post-process is
+// performed here.)  Texture is unused, as in the reference.
+void CopyOutputToFile(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY, i32 TileWidth,
+                      i32 TileHeight, i32 NumChannels, texture Texture, void* ScreenBufferData);
+// stbi_write_bmp: a 24-bit BMP (asset_loading.cpp:48-54).  Prints pt_last_error() on failure.
+void WriteImage(char* filename, i32 width, i32 height, i32 components, void* data);

@@ -133,6 +133,20 @@ int pt_set_env_map(const pt_texture* tex);
 int pt_render_simt_textured(float* buf, int32_t width, int32_t height, int32_t num_tiles_x, int32_t num_tiles_y,
                             int32_t tile_width, int32_t tile_height, int32_t num_channels, const pt_texture* tex);
 
+/* --- output stage: ACES + sRGB + 8-bit pack, BMP ---------------------------- */
+#define PT_PIXEL_RGBA8 0   /* OutputToFile   (v4 :1297-1331): bytes R, G, B, A = 255 (u32 0xFFBBGGRR) */
+#define PT_PIXEL_XRGB8 1   /* OutputToScreen (v4 :1260-1295): u32 0x00RRGGBB                          */
+/* replaces the post-process of OutputToScreen / OutputToFile (demofox_path_tracing_optimization_v4.cpp
+ * :1260-1331, ACESFilm :165-175, LinearToSRGB :177-186): accumulator (host buffer in `layout`,
+ * tile sizes for PT_LAYOUT_TILED_PLANAR8) -> width*height packed pixels, row 0 = top.  The
+ * HBM-resident accumulator is used directly when `accum` is the PT_FLAG_DEFER_READBACK buffer. */
+int pt_tonemap(const float* accum, int32_t width, int32_t height, int32_t layout, int32_t tile_width,
+               int32_t tile_height, uint32_t* out, int32_t format);
+int pt_tonemap_device(const float* accum, int32_t width, int32_t height, int32_t layout, int32_t tile_width,
+                      int32_t tile_height, uint32_t* out, int32_t format, void* hip_stream);   /* async */
+/* replaces WriteImage (asset_loading.h:8, .cpp:48-54: stbi_write_bmp, 24-bit BMP) */
+int pt_write_bmp(const char* path, int32_t width, int32_t height, int32_t components, const void* data);
+
 /* --- device-resident entry points -------------------------------------------------------------- */
 int pt_render_device(const pt_device_job* job, void* hip_stream);      /* async on hip_stream     */
 int pt_count_device(const pt_device_job* job, void* hip_stream, pt_work_counts* out); /* sync;    */

@@ -55,4 +55,6 @@ $CXX -shared -o "$OUT/libref_scalar.so" "$GEN/scalar.o" "$GEN/drv.o" -lm
 $CXX -o "$OUT/ref_scalar" "$GEN/scalar.o" "$GEN/drv_main.o" -lm
 # LoadTexture's decoder (config 4): the reference's vendored stb_image.h, compiled where it lies
 $CXX -std=c++17 -O2 -w -I"$REF" "$HERE/ref_hdr.cpp" -o "$OUT/ref_hdr" -lm
-echo "build_ref.sh: built $OUT/libref_scalar.so, $OUT/ref_scalar and $OUT/ref_hdr"
+# WriteImage's encoder (output stage): the reference's vendored stb_image_write.h, where it lies
+$CXX -std=c++17 -O2 -w -I"$REF" "$HERE/ref_bmp.cpp" -o "$OUT/ref_bmp" -lm
+echo "build_ref.sh: built $OUT/libref_scalar.so, $OUT/ref_scalar, $OUT/ref_hdr and $OUT/ref_bmp"

@@ -74,6 +74,13 @@ void pto_random_unit_vector(uint32_t* state, float out3[3]);/* scalar.cpp:42-50 
 uint32_t pto_seed(uint32_t x, uint32_t y, uint32_t frame); /* scalar.cpp:332    */
 void pto_env_sample(const pto_env* env, const float dir[3], float out3[3]); /* texture.cpp:101-139 */
 
+/* Output stage (pt_oracle_output.c): ACES + fast sRGB + 8-bit pack, v4 :144-187, :1260-1331. */
+#define PTO_PIXEL_RGBA8 0   /* OutputToFile:   bytes R, G, B, A = 255 (u32 0xFFBBGGRR) */
+#define PTO_PIXEL_XRGB8 1   /* OutputToScreen: u32 0x00RRGGBB                          */
+uint32_t pto_tonemap_channel(float linear);
+uint32_t pto_tonemap_pixel(const float rgb[3], int32_t format);
+void pto_tonemap(const float* rgb, int32_t w, int32_t h, int32_t format, uint32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

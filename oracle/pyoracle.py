@@ -62,6 +62,10 @@ def load() -> ctypes.CDLL:
         L.pto_seed.argtypes = [ctypes.c_uint32] * 3
         L.pto_seed.restype = ctypes.c_uint32
         L.pto_env_sample.argtypes = [ctypes.POINTER(Env), ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+        L.pto_tonemap_channel.restype = ctypes.c_uint32
+        L.pto_tonemap_channel.argtypes = [ctypes.c_float]
+        L.pto_tonemap.restype = None
+        L.pto_tonemap.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -139,3 +143,20 @@ def ref_render(width: int, height: int, frames: int, tmpdir: Path) -> np.ndarray
     out = Path(tmpdir) / f"ref_{width}x{height}_{frames}.f32"
     subprocess.run([str(REF_BIN), str(width), str(height), str(frames), str(out)], check=True)
     return np.fromfile(out, np.float32).reshape(height, width, 3)
+
+
+PIXEL_RGBA8 = 0   # PTO_PIXEL_RGBA8 (OutputToFile)
+PIXEL_XRGB8 = 1   # PTO_PIXEL_XRGB8 (OutputToScreen)
+
+
+def tonemap(rgb: np.ndarray, fmt: int = PIXEL_RGBA8) -> np.ndarray:
+    """Output stage of v4 (oracle/pt_oracle_output.c) on an interleaved H x W x 3 accumulator."""
+    a = np.ascontiguousarray(rgb, dtype=np.float32)
+    h, w = a.shape[0], a.shape[1]
+    out = np.empty((h, w), np.uint32)
+    load().pto_tonemap(a.ctypes.data, w, h, fmt, out.ctypes.data)
+    return out
+
+
+def tonemap_channel(v: float) -> int:
+    return int(load().pto_tonemap_channel(float(v)))

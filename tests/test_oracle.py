@@ -97,3 +97,17 @@ def test_zero_bounces_and_empty():
     assert not empty.any()
     with pytest.raises(ValueError):
         pyoracle.render(32, 16, frame_first=0)
+
+
+def test_tonemap_oracle_properties():
+    """The output-stage restatement (oracle/pt_oracle_output.c, v4 :144-187, :1260-1331): 0 -> 0,
+    monotone over the displayable range, saturating at 255, 8-bit packing of both formats."""
+    from oracle import pyoracle as po
+    xs = np.concatenate([[0.0], np.geomspace(1e-6, 20.0, 4000)]).astype(np.float32)
+    v = np.array([po.tonemap_channel(x) for x in xs])
+    assert v[0] == 0 and v[-1] == 255
+    assert (np.diff(v) >= 0).all()
+    assert po.tonemap_channel(1.0) == 232 and po.tonemap_channel(0.1) == 99   # KATs of this restatement
+    rgb = np.array([[[1.0, 0.1, 0.0]]], np.float32)
+    assert po.tonemap(rgb, po.PIXEL_RGBA8)[0, 0] == 0xFF000000 | (0 << 16) | (99 << 8) | 232
+    assert po.tonemap(rgb, po.PIXEL_XRGB8)[0, 0] == (232 << 16) | (99 << 8) | 0
