@@ -1,5 +1,6 @@
-"""MI355X (gfx950) backend for the per-pixel diffuse+emissive path-tracing hot path of
-torgeiba/CPUPerformanceRayTracer (demofox_path_tracing_scalar.cpp / _simd.cpp / _simd_tiled.cpp).
+"""MI355X (gfx950) backend for the per-pixel path-tracing hot path of torgeiba/CPUPerformanceRayTracer:
+the diffuse+emissive tracer (demofox_path_tracing_scalar.cpp / _simd.cpp / _simd_tiled.cpp /
+_simt_textured.cpp) and the shipping v4 renderer (demofox_path_tracing_optimization_v4.cpp).
 
   renderer  -- the reference's frame/tile interface on host buffers (drop-in)
   device    -- device-resident rendering on torch tensors (bench, shards)
@@ -15,6 +16,18 @@ from .renderer import (  # noqa: F401
     DemofoxRenderSimd,
     DemofoxRenderSimdTiled,
     DemofoxRenderSimtTextured,
+    DemofoxRenderOptV4,
+    InitializeGlobalRenderResources,
+    ReinitializeRenderTileData,
+    InitializeScene,
+    ClearScene,
+    AddMaterialToScene,
+    AddQuadObjectToScene,
+    AddSphereObjectToScene,
+    LoadCubemapTexture,
+    v4_config,
+    v4_get_frame,
+    v4_set_frame,
     LoadTexture,
     RenderBufferInfo,
     RenderTile,
@@ -35,4 +48,7 @@ __all__ = [
     "CONFIGS", "Workload", "check_valid_settings", "BeginFrame", "CopyOutputToFile", "DemofoxRenderScalar", "DemofoxRenderSimd",
     "DemofoxRenderSimdTiled", "DemofoxRenderSimtTextured", "LoadTexture", "RenderBufferInfo", "RenderTile", "RenderTileInfo", "get_frame", "init",
     "make_tiles", "readback", "set_env_map", "set_frame", "shutdown", "texture", "tonemap", "WriteImage",
+    "DemofoxRenderOptV4", "InitializeGlobalRenderResources", "ReinitializeRenderTileData", "InitializeScene",
+    "ClearScene", "AddMaterialToScene", "AddQuadObjectToScene", "AddSphereObjectToScene", "LoadCubemapTexture",
+    "v4_config", "v4_get_frame", "v4_set_frame",
 ]

@@ -34,8 +34,17 @@ EXPORTED_SYMBOLS = (
     "pt_render_scalar", "pt_render_simd", "pt_render_simd_tiled", "pt_render_tile", "pt_begin_frame",
     "pt_readback", "pt_render_device", "pt_count_device",
     "pt_load_texture", "pt_decode_hdr", "pt_free_texture", "pt_set_env_map", "pt_render_simt_textured",
-    "pt_tonemap", "pt_tonemap_device", "pt_write_bmp",
+    "pt_tonemap", "pt_tonemap_device", "pt_write_bmp", "pt_load_cubemap_texture",
+    "pt_v4_default_config", "pt_v4_set_config", "pt_v4_initialize_global_render_resources",
+    "pt_v4_reinitialize_render_tile_data", "pt_v4_initialize_scene", "pt_v4_clear_scene", "pt_v4_add_material",
+    "pt_v4_add_quad", "pt_v4_add_sphere", "pt_v4_set_frame", "pt_v4_get_frame", "pt_render_opt_v4",
+    "pt_copy_output_to_file", "pt_v4_render_device", "pt_v4_count_device",
 )
+
+PT_V4_ENV_NONE = 0
+PT_V4_ENV_EQUIRECT = 1
+PT_V4_ENV_CUBEMAP = 2
+PT_V4_MAX_OBJECTS = 12
 
 
 class PtConfig(ctypes.Structure):
@@ -71,6 +80,19 @@ class PtTexture(ctypes.Structure):
 class PtWorkCounts(ctypes.Structure):
     _fields_ = [("segments", ctypes.c_uint64), ("lane_slots", ctypes.c_uint64),
                 ("samples", ctypes.c_uint64), ("escaped", ctypes.c_uint64), ("primary", ctypes.c_uint64)]
+
+
+class PtV4Config(ctypes.Structure):
+    _fields_ = [("env_mode", ctypes.c_int32), ("random_jitter", ctypes.c_int32), ("rejection", ctypes.c_int32),
+                ("num_bounces", ctypes.c_int32), ("output_to_screen", ctypes.c_int32)]
+
+
+class PtV4Material(ctypes.Structure):
+    _fields_ = [("albedo", ctypes.c_float * 3), ("emissive", ctypes.c_float * 3),
+                ("specular_chance", ctypes.c_float), ("specular_roughness", ctypes.c_float),
+                ("specular_color", ctypes.c_float * 3), ("ior", ctypes.c_float),
+                ("refraction_chance", ctypes.c_float), ("refraction_roughness", ctypes.c_float),
+                ("refraction_color", ctypes.c_float * 3)]
 
 
 class PtError(RuntimeError):
@@ -126,6 +148,22 @@ def load() -> ctypes.CDLL:
         "pt_tonemap": (i32, [vp, i32, i32, i32, i32, i32, vp, i32]),
         "pt_tonemap_device": (i32, [vp, i32, i32, i32, i32, i32, vp, i32, vp]),
         "pt_write_bmp": (i32, [ctypes.c_char_p, i32, i32, i32, vp]),
+        "pt_load_cubemap_texture": (i32, [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(PtTexture)]),
+        "pt_v4_default_config": (None, [ctypes.POINTER(PtV4Config)]),
+        "pt_v4_set_config": (i32, [ctypes.POINTER(PtV4Config)]),
+        "pt_v4_initialize_global_render_resources": (i32, []),
+        "pt_v4_reinitialize_render_tile_data": (i32, []),
+        "pt_v4_initialize_scene": (i32, []),
+        "pt_v4_clear_scene": (i32, []),
+        "pt_v4_add_material": (i32, [ctypes.POINTER(PtV4Material)]),
+        "pt_v4_add_quad": (i32, [ctypes.POINTER(ctypes.c_float)]),
+        "pt_v4_add_sphere": (i32, [ctypes.POINTER(ctypes.c_float)]),
+        "pt_v4_set_frame": (i32, [u32]),
+        "pt_v4_get_frame": (u32, []),
+        "pt_render_opt_v4": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, ctypes.POINTER(PtTexture), vp]),
+        "pt_copy_output_to_file": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp]),
+        "pt_v4_render_device": (i32, [ctypes.POINTER(PtDeviceJob), vp]),
+        "pt_v4_count_device": (i32, [ctypes.POINTER(PtDeviceJob), vp, ctypes.POINTER(PtWorkCounts)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

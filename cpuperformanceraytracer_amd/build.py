@@ -23,8 +23,9 @@ CSRC = PKG / "csrc"
 LIB = PKG / "libpt_mi355.so"
 ARCH = os.environ.get("PT_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["pt_kernel.hip", "pt_output.hip", "pt_scene.cpp", "pt_capi.cpp", "pt_dropin.cpp", "pt_texture.cpp"]
-HEADERS = ["pt_kernel.h", "pt_output.h", "pt_scene.h", "pt_sincosf.h", "pt_exactmath.h", "pt_invtrig.h"]
+SOURCES = ["pt_kernel.hip", "pt_output.hip", "pt_v4.hip", "pt_scene.cpp", "pt_v4_scene.cpp", "pt_capi.cpp",
+           "pt_dropin.cpp", "pt_texture.cpp"]
+HEADERS = ["pt_kernel.h", "pt_output.h", "pt_v4.h", "pt_scene.h", "pt_sincosf.h", "pt_exactmath.h", "pt_invtrig.h"]
 PARITY_FLAGS = [
     "-ffp-contract=off",
     "-fhip-fp32-correctly-rounded-divide-sqrt",

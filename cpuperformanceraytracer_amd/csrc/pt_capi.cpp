@@ -9,6 +9,7 @@
 //   - the caller owns the host buffer, the call returns after it is updated (Application.cpp:474).
 #include "pt_kernel.h"
 #include "pt_output.h"
+#include "pt_v4.h"
 #include "../../include/pt_mi355.h"
 #include <stdarg.h>
 #include <stdio.h>
@@ -75,6 +76,12 @@ struct State {
     size_t dtone_in_cap = 0;
     uint32_t* dtone_out = nullptr;
     size_t dtone_out_cap = 0;
+    // v4 renderer (demofox_path_tracing_optimization_v4.cpp): its own iFrame (v4 :34) and scene
+    pt_v4_config v4cfg{PT_V4_ENV_EQUIRECT, 1, 1, 8, 1};
+    bool v4_scene_ready = false;
+    PtV4SceneDesc v4desc{};
+    PtV4Scene v4scene{};
+    uint32_t v4_frame = 0;
 };
 
 State g;
@@ -427,6 +434,63 @@ int upload_env(const pt_texture* t)
     return PT_OK;
 }
 
+// ---- v4 helpers ----------------------------------------------------------------------------------
+
+int v4_rebuild()
+{
+    if (pt_v4_build_scene(&g.v4desc, &g.v4scene))
+        return fail(PT_EINVAL, "v4 scene exceeds MAX_OBJECTS (%d quads + %d spheres, %d materials; limit %d)",
+                    g.v4desc.nquads, g.v4desc.nspheres, g.v4desc.nmat, PT_V4_MAX_OBJECTS);
+    g.v4_scene_ready = true;
+    return PT_OK;
+}
+
+int v4_ensure_scene()
+{
+    if (g.v4_scene_ready) return PT_OK;
+    pt_v4_default_scene_desc(&g.v4desc);   // InitializeGlobalRenderResources -> InitializeScene (v4 :1650-1654)
+    return v4_rebuild();
+}
+
+PtV4Job v4_job(float* buf, int32_t w, int32_t h)
+{
+    PtV4Job j{};
+    j.buf = buf;
+    j.width = w;
+    j.height = h;
+    j.col0 = 0;
+    j.ncols = w;
+    j.row_start = 0;
+    j.row_stride = 1;
+    j.nrows = h;
+    j.layout = PT_LAYOUT_INTERLEAVED;
+    j.frame_first = g.v4_frame + 1;
+    j.nframes = 1;   // NUM_SAMPLES_PER_FRAME = 1: one frame per DemofoxRenderOptV4 call
+    j.num_bounces = g.v4cfg.num_bounces;
+    j.env_mode = PT_V4_ENV_NONE;
+    j.random_jitter = g.v4cfg.random_jitter;
+    j.rejection = g.v4cfg.rejection;
+    return j;
+}
+
+int v4_use_env(PtV4Job& j)
+{
+    if (g.v4cfg.env_mode == PT_V4_ENV_NONE) return PT_OK;
+    if (!g.denv) return fail(PT_ESTATE, "v4 env mode %d without an env map", g.v4cfg.env_mode);
+    j.env_mode = g.v4cfg.env_mode;
+    j.env = g.denv;
+    j.env_w = g.env_w;
+    j.env_h = g.env_h;
+    return PT_OK;
+}
+
+int v4_launch(const PtV4Job& j, hipStream_t st, bool count)
+{
+    hipError_t e = pt_launch_v4(j, g.v4scene, st, count);
+    if (e != hipSuccess) return fail(PT_EHIP, "v4 render launch failed: %s", hipGetErrorString(e));
+    return PT_OK;
+}
+
 }  // namespace
 
 int pt_internal_fail(int code, const char* fmt, ...)
@@ -766,6 +830,195 @@ int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
     out->samples = h[PT_CNT_SAMPLES];
     out->escaped = h[PT_CNT_ESCAPED];
     out->primary = h[PT_CNT_PRIMARY];
+    return PT_OK;
+}
+
+// ---- v4 renderer -------------------------------------------------------------------------------
+
+void pt_v4_default_config(pt_v4_config* c)
+{
+    if (!c) return;
+    c->env_mode = PT_V4_ENV_EQUIRECT;   // USE_ENV_MAP 1, USE_ENV_CUBEMAP 0
+    c->random_jitter = 1;               // USE_RANDOM_JITTER_TEXTURE_SAMPLING 1
+    c->rejection = 1;                   // USE_UNIT_VECTOR_REJECTION_SAMPLING 1
+    c->num_bounces = 8;                 // c_numBounces, v4 :23
+    c->output_to_screen = 1;            // OUTPUT_TO_SCREEN = !RENDER_OFFLINE
+}
+
+int pt_v4_set_config(const pt_v4_config* c)
+{
+    if (!c) return fail(PT_EINVAL, "null v4 config");
+    if (c->env_mode < PT_V4_ENV_NONE || c->env_mode > PT_V4_ENV_CUBEMAP) return fail(PT_EINVAL, "unknown env mode %d", c->env_mode);
+    if (c->num_bounces < 0 || c->num_bounces > 1024) return fail(PT_EINVAL, "num_bounces %d out of range", c->num_bounces);
+    g.v4cfg = *c;
+    g.v4cfg.random_jitter = c->random_jitter != 0;
+    g.v4cfg.rejection = c->rejection != 0;
+    g.v4cfg.output_to_screen = c->output_to_screen != 0;
+    return PT_OK;
+}
+
+int pt_v4_initialize_global_render_resources(void)
+{
+    int rc;
+    if ((rc = ensure_init())) return rc;
+    return v4_ensure_scene();
+}
+
+int pt_v4_reinitialize_render_tile_data(void) { return PT_OK; }
+
+int pt_v4_initialize_scene(void)
+{
+    pt_v4_default_scene_desc(&g.v4desc);
+    return v4_rebuild();
+}
+
+int pt_v4_clear_scene(void)
+{
+    memset(&g.v4desc, 0, sizeof(g.v4desc));
+    return v4_rebuild();
+}
+
+int pt_v4_add_material(const pt_v4_material* m)
+{
+    int rc;
+    if (!m) return fail(PT_EINVAL, "null material");
+    if ((rc = v4_ensure_scene())) return rc;
+    if (g.v4desc.nmat >= PT_V4_MAX_OBJECTS) return fail(PT_EINVAL, "more than MAX_MATERIALS (%d) materials", PT_V4_MAX_OBJECTS);
+    static_assert(sizeof(pt_v4_material) == sizeof(PtV4Mat), "material layout");
+    memcpy(&g.v4desc.mat[g.v4desc.nmat], m, sizeof(PtV4Mat));
+    const int idx = g.v4desc.nmat++;
+    if ((rc = v4_rebuild())) return rc;
+    return idx;   // AddMaterialToScene returns scene.NumMaterials++ (v4 :1387)
+}
+
+int pt_v4_add_quad(const float v[12])
+{
+    int rc;
+    if (!v) return fail(PT_EINVAL, "null quad");
+    if ((rc = v4_ensure_scene())) return rc;
+    if (g.v4desc.nquads + g.v4desc.nspheres >= PT_V4_MAX_OBJECTS)
+        return fail(PT_EINVAL, "more than MAX_OBJECTS (%d) objects", PT_V4_MAX_OBJECTS);
+    memcpy(g.v4desc.quad[g.v4desc.nquads++], v, 12 * sizeof(float));
+    if ((rc = v4_rebuild())) return rc;
+    return g.v4desc.nquads;   // v4 :1394
+}
+
+int pt_v4_add_sphere(const float pr[4])
+{
+    int rc;
+    if (!pr) return fail(PT_EINVAL, "null sphere");
+    if ((rc = v4_ensure_scene())) return rc;
+    if (g.v4desc.nquads + g.v4desc.nspheres >= PT_V4_MAX_OBJECTS)
+        return fail(PT_EINVAL, "more than MAX_OBJECTS (%d) objects", PT_V4_MAX_OBJECTS);
+    memcpy(g.v4desc.sphere[g.v4desc.nspheres++], pr, 4 * sizeof(float));
+    if ((rc = v4_rebuild())) return rc;
+    return g.v4desc.nquads;   // v4 :1400 returns NumQuadObjects
+}
+
+int pt_v4_set_frame(uint32_t frame)
+{
+    if (frame >= kMaxFrame) return fail(PT_EINVAL, "frame %u >= 2^24", frame);
+    g.v4_frame = frame;
+    return PT_OK;
+}
+
+uint32_t pt_v4_get_frame(void) { return g.v4_frame; }
+
+int pt_render_opt_v4(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty, int32_t tw, int32_t th, int32_t nc,
+                     const pt_texture* tex, void* screen)
+{
+    int rc;
+    if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
+    if ((rc = tiled_settings(w, h, ntx, nty, tw, th))) return rc;
+    if ((int64_t)ntx * nty > 1024) return fail(PT_EINVAL, "%d x %d tiles exceed NumMaxThreads (1024, v4 :1341)", ntx, nty);
+    if ((rc = v4_ensure_scene())) return rc;
+    if (g.v4_frame + 1u >= kMaxFrame) return fail(PT_EINVAL, "v4 frame counter exceeds the exact f32 range 2^24");
+    if (g.v4cfg.env_mode != PT_V4_ENV_NONE) {
+        if (!tex) return fail(PT_EINVAL, "env mode %d needs a texture", g.v4cfg.env_mode);
+        if ((rc = check_texture(tex))) return rc;
+        if (!g.denv || g.env_src != tex->data || g.env_w != tex->width || g.env_h != tex->height)
+            if ((rc = upload_env(tex))) return rc;
+    }
+    const size_t bytes = (size_t)w * h * 3 * sizeof(float);
+    if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
+    PtV4Job j = v4_job(g.dbuf, w, h);
+    j.layout = PT_LAYOUT_TILED_PLANAR8;   // RenderTile v4 :1186-1191
+    j.tile_w = tw;
+    j.tile_h = th;
+    if ((rc = v4_use_env(j)) || (rc = v4_launch(j, g.stream, false))) return rc;
+    g.v4_frame += 1;   // iFrame += 1.0f (v4 :1703), before rendering
+    if (screen && g.v4cfg.output_to_screen) {   // OutputToScreen per tile (v4 :1562-1564)
+        const size_t out_bytes = (size_t)w * h * sizeof(uint32_t);
+        if ((rc = grow((void**)&g.dtone_out, &g.dtone_out_cap, out_bytes))) return rc;
+        const PtToneJob tj{g.dbuf, w, h, PT_LAYOUT_TILED_PLANAR8, tw, th, g.dtone_out, PT_PIXEL_XRGB8};
+        hipError_t e = pt_launch_tonemap(tj, g.stream);
+        if (e != hipSuccess) return fail(PT_EHIP, "tonemap launch failed: %s", hipGetErrorString(e));
+        HIP_TRY(hipMemcpyAsync(screen, g.dtone_out, out_bytes, hipMemcpyDeviceToHost, g.stream));
+    }
+    return stage_out(buf, 0, bytes);
+}
+
+int pt_copy_output_to_file(const float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty, int32_t tw, int32_t th,
+                           int32_t nc, void* file_pixels)
+{
+    int rc;
+    if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
+    if ((rc = tiled_settings(w, h, ntx, nty, tw, th))) return rc;
+    if (g.v4_frame + 1u >= kMaxFrame) return fail(PT_EINVAL, "v4 frame counter exceeds the exact f32 range 2^24");
+    if ((rc = pt_tonemap(buf, w, h, PT_LAYOUT_TILED_PLANAR8, tw, th, (uint32_t*)file_pixels, PT_PIXEL_RGBA8))) return rc;
+    g.v4_frame += 1;   // v4 :1738
+    return PT_OK;
+}
+
+static int v4_device_job(const pt_device_job* dj, PtV4Job* j4)
+{
+    int rc;
+    if (!dj) return fail(PT_EINVAL, "null device job");
+    pt_device_job geo = *dj;   // geometry / frame checks of the scalar-path jobs
+    geo.use_env = 0;
+    PtJob j;
+    if ((rc = device_job(&geo, &j)) || (rc = v4_ensure_scene())) return rc;
+    *j4 = v4_job(dj->buf, dj->width, dj->height);
+    j4->row_start = dj->row_start;
+    j4->row_stride = dj->row_stride;
+    j4->nrows = dj->nrows;
+    j4->layout = dj->layout;
+    j4->frame_first = dj->frame_first;
+    j4->nframes = dj->nframes;
+    j4->num_bounces = dj->num_bounces;
+    if (dj->use_env) {
+        if (g.v4cfg.env_mode == PT_V4_ENV_NONE) return fail(PT_ESTATE, "use_env with v4 env mode NONE");
+        if ((rc = v4_use_env(*j4))) return rc;
+    }
+    return PT_OK;
+}
+
+int pt_v4_render_device(const pt_device_job* dj, void* stream)
+{
+    int rc;
+    PtV4Job j;
+    if ((rc = ensure_init()) || (rc = v4_device_job(dj, &j))) return rc;
+    return v4_launch(j, (hipStream_t)stream, false);
+}
+
+int pt_v4_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
+{
+    int rc;
+    PtV4Job j;
+    if (!out) return fail(PT_EINVAL, "null counts");
+    if ((rc = ensure_init()) || (rc = v4_device_job(dj, &j))) return rc;
+    hipStream_t st = (hipStream_t)stream;
+    HIP_TRY(hipMemsetAsync(g.dcounters, 0, kCounterSlots * sizeof(unsigned long long), st));
+    j.counters = g.dcounters;
+    if ((rc = v4_launch(j, st, true))) return rc;
+    unsigned long long h[4];
+    HIP_TRY(hipMemcpyAsync(h, g.dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    out->segments = h[0];
+    out->lane_slots = h[3];
+    out->samples = (uint64_t)dj->width * (uint64_t)dj->nrows * (uint64_t)dj->nframes;
+    out->escaped = h[2];
+    out->primary = out->samples;   // one camera ray per sample (jittered)
     return PT_OK;
 }
 

@@ -62,16 +62,40 @@ void DemofoxRenderSimtTextured(f32* BufferOut, i32 BufferWidth, i32 BufferHeight
              "DemofoxRenderSimtTextured");
 }
 
+texture LoadCubemapTexture(char* filename[6])
+{
+    texture t;
+    pt_texture p;
+    if (pt_load_cubemap_texture(filename, &p) != PT_OK) {
+        fprintf(stderr, "LoadCubemapTexture: %s\n", pt_last_error());
+        return t;
+    }
+    t.Data = p.data;
+    t.Width = p.width;
+    t.Height = p.height;
+    t.Components = p.components;
+    return t;
+}
+
+void DemofoxRenderOptV4(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY, i32 TileWidth,
+                        i32 TileHeight, i32 NumChannels, texture Texture, void* ScreenBufferData)
+{
+    const pt_texture p = {Texture.Data, Texture.Width, Texture.Height, Texture.Components};
+    pt_check(pt_render_opt_v4(BufferOut, BufferWidth, BufferHeight, NumTilesX, NumTilesY, TileWidth, TileHeight,
+                              NumChannels, Texture.Data ? &p : nullptr, ScreenBufferData),
+             "DemofoxRenderOptV4");
+}
+
+void InitializeGlobalRenderResources() { pt_check(pt_v4_initialize_global_render_resources(), "InitializeGlobalRenderResources"); }
+
+void ReinitializeRenderTileData() { pt_check(pt_v4_reinitialize_render_tile_data(), "ReinitializeRenderTileData"); }
+
 void CopyOutputToFile(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY, i32 TileWidth,
                       i32 TileHeight, i32 NumChannels, texture Texture, void* ScreenBufferData)
 {
     (void)Texture;
-    if (NumChannels != 3 || NumTilesX * TileWidth != BufferWidth || NumTilesY * TileHeight != BufferHeight) {
-        fprintf(stderr, "CopyOutputToFile: invalid settings\n");
-        abort();
-    }
-    pt_check(pt_tonemap(BufferOut, BufferWidth, BufferHeight, PT_LAYOUT_TILED_PLANAR8, TileWidth, TileHeight,
-                        (uint32_t*)ScreenBufferData, PT_PIXEL_RGBA8),
+    pt_check(pt_copy_output_to_file(BufferOut, BufferWidth, BufferHeight, NumTilesX, NumTilesY, TileWidth, TileHeight,
+                                    NumChannels, ScreenBufferData),
              "CopyOutputToFile");
 }
 

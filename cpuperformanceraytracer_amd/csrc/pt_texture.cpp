@@ -231,6 +231,39 @@ int pt_write_bmp(const char* path, int32_t w, int32_t h, int32_t comp, const voi
     return PT_OK;
 }
 
+// LoadCubemapTexture (asset_loading.cpp:18-44): six faces loaded like LoadTexture (flipped), all
+// assumed to share the LAST face's size (the reference reads Width/Height of the last file and
+// copies faceSize floats from each); stacked vertically in file order (px nx py ny pz nz,
+// Application.cpp:205-211).  Faces of a different size are an error here (the reference would
+// read out of bounds).
+int pt_load_cubemap_texture(const char* const paths[6], pt_texture* out)
+{
+    if (!paths || !out) return pt_internal_fail(PT_EINVAL, "null argument");
+    memset(out, 0, sizeof(*out));
+    pt_texture face[6] = {};
+    int rc = PT_OK;
+    for (int i = 0; i < 6 && rc == PT_OK; ++i) rc = pt_load_texture(paths[i], &face[i]);
+    for (int i = 0; i < 6 && rc == PT_OK; ++i)
+        if (face[i].width != face[5].width || face[i].height != face[5].height || face[i].components != 3)
+            rc = pt_internal_fail(PT_EINVAL, "cubemap face %d is %dx%d, face 5 is %dx%d", i, face[i].width,
+                                  face[i].height, face[5].width, face[5].height);
+    if (rc == PT_OK) {
+        const size_t fs = (size_t)face[5].width * face[5].height * 3;
+        float* data = (float*)malloc(fs * 6 * sizeof(float));
+        if (!data) {
+            rc = pt_internal_fail(PT_ENOMEM, "out of host memory");
+        } else {
+            for (int i = 0; i < 6; ++i) memcpy(data + i * fs, face[i].data, fs * sizeof(float));
+            out->data = data;
+            out->width = face[5].width;
+            out->height = face[5].height * 6;
+            out->components = 3;
+        }
+    }
+    for (int i = 0; i < 6; ++i) pt_free_texture(&face[i]);
+    return rc;
+}
+
 void pt_free_texture(pt_texture* t)
 {
     if (!t) return;

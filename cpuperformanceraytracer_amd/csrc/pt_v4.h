@@ -1,0 +1,67 @@
+// pt_v4.h -- the v4 renderer (demofox_path_tracing_optimization_v4.cpp, the reference's shipping
+// path, Application.cpp:474): scene tables, launch interface, host scene builder.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PT_V4_MAX_OBJECTS 12   // MAX_OBJECTS / MAX_MATERIALS, v4 :351-352
+
+// env modes (global_preprocessor_flags.h:58-59)
+#define PT_V4_ENV_NONE_ 0       // USE_ENV_MAP 0: ambient (0.11, 0.1, 0.15), v4 :782
+#define PT_V4_ENV_EQUIRECT_ 1   // USE_ENV_MAP 1, USE_ENV_CUBEMAP 0 (default)
+#define PT_V4_ENV_CUBEMAP_ 2    // USE_ENV_CUBEMAP 1 (six faces stacked, LoadCubemapTexture)
+
+// QuadSceneObject after PrecomputeQuadData (v4 :256-320): only what TestQuadTrace (:556-637) reads.
+struct PtV4Quad {
+    float v0[3];
+    float n[3];    // normalize(cross(V01, V02))
+    float a0[3];   // NxV01 / DetBot   (bottom triangle 0,1,2)
+    float a1[3];   // NxV20 / DetBot
+    float b0[3];   // NxV30 / DetTop   (top triangle 0,2,3)
+    float b1[3];   // NxV02 / DetTop
+};
+
+// One row of SceneMaterialSOA (v4 :354-373) as GatherMaterials (:389-427) reads it: 17 f32.
+struct PtV4Mat {
+    float albedo[3], emissive[3];
+    float spec_chance, spec_rough, spec_color[3];
+    float ior, refr_chance, refr_rough, refr_color[3];
+};
+static_assert(sizeof(PtV4Mat) == 17 * sizeof(float), "material row");
+
+struct PtV4Scene {
+    int32_t nquads, nspheres;
+    PtV4Quad quad[PT_V4_MAX_OBJECTS];
+    float sph[PT_V4_MAX_OBJECTS][4];     // PositionAndRadius
+    PtV4Mat mat[PT_V4_MAX_OBJECTS];      // by object index (quads first); unused rows zero
+};
+
+struct PtV4Job {
+    float* buf;                 // device accumulator
+    int32_t width, height;      // iResolution
+    int32_t col0, ncols;        // pixel columns [col0, col0 + ncols)
+    int32_t row_start, row_stride, nrows;
+    int32_t layout;             // PtLayout (pt_kernel.h)
+    int32_t tile_w, tile_h;     // PT_LAYOUT_TILED_PLANAR8
+    uint32_t frame_first;       // iFrame of the first frame (>= 1)
+    int32_t nframes;
+    int32_t num_bounces;        // c_numBounces (8)
+    int32_t env_mode;           // PT_V4_ENV_*_
+    int32_t random_jitter;      // USE_RANDOM_JITTER_TEXTURE_SAMPLING
+    int32_t rejection;          // USE_UNIT_VECTOR_REJECTION_SAMPLING
+    const float* env;           // device texture (H x W x 3), nullptr with PT_V4_ENV_NONE_
+    int32_t env_w, env_h;
+    unsigned long long* counters;   // COUNT launches: [0] segments, [1] samples, [2] escaped, [3] lane slots
+};
+
+// Scene description in AddQuad/Sphere/MaterialToScene order (v4 :1368-1401).
+struct PtV4SceneDesc {
+    int32_t nquads, nspheres, nmat;
+    float quad[PT_V4_MAX_OBJECTS][4][3];
+    float sphere[PT_V4_MAX_OBJECTS][4];
+    PtV4Mat mat[PT_V4_MAX_OBJECTS];   // as passed to AddMaterialToScene (before its albedo.x copy)
+};
+
+void pt_v4_default_scene_desc(PtV4SceneDesc* d);                   // InitializeScene, v4 :1403-1496
+int pt_v4_build_scene(const PtV4SceneDesc* d, PtV4Scene* out);     // PrecomputeQuadData + AddMaterialToScene
+hipError_t pt_launch_v4(const PtV4Job& job, const PtV4Scene& scene, hipStream_t stream, bool count);

@@ -1,0 +1,556 @@
+// pt_v4.hip -- the reference's shipping renderer (demofox_path_tracing_optimization_v4.cpp,
+// DemofoxRenderOptV4 :1696-1721 -> RenderTile :1179-1258 -> mainImage :1092-1130 ->
+// GetColorForRay :722-911) as one HIP kernel for gfx950.
+//
+// Materials: diffuse / specular (roughness-lerped reflection) / refraction (Fresnel-Schlick,
+// Beer absorption with approx_exp), Russian-roulette throughput boost, jittered camera, env map
+// (equirect or cubemap, random-jitter or bilinear texel sampling) weighted by the throughput.
+//
+// Mapping: the reference runs 8 pixels per AVX2 register, each with its own RNG state, looping
+// until all 8 paths end.  Here one wave owns an 8x8 tile and the (pixel, frame) samples of the
+// tile form a pool of items: a lane that finishes a path takes the next item (ballot + mbcnt), so
+// no lane idles while paths of the tile remain.  Each sample's radiance goes to LDS; at the end
+// the lane of each pixel accumulates its frames in frame order with the reference's fused lerp
+// (:1243) -- read once, written once per launch.
+//
+// Numerics: the reference's f32 operations in its order, fmadd/fmsub/fnmadd fused, '/' and sqrt
+// correctly rounded; rcp / rsroot are the exact 1/x and 1/sqrtf(x) (mathlib.h:415,437 -- the
+// x86 approximations have no portable bit pattern); atan2/asin/sin/cos are glibc's
+// (pt_invtrig.h, pt_sincosf.h).  Bit-identical to oracle/pt_oracle_v4.c.
+#include "pt_v4.h"
+#include "pt_kernel.h"
+#include "pt_exactmath.h"
+#include "pt_invtrig.h"
+#include "pt_sincosf.h"
+#include <algorithm>
+
+namespace {
+
+constexpr float kMinHit = 0.01f;      // c_minimumRayHitTime  v4 :10
+constexpr float kNudge = 0.01f;       // c_rayPosNormalNudge  v4 :14
+constexpr float kSuperFar = 10000.0f; // c_superFar           v4 :17
+constexpr float kPi = 3.14159265359f; // c_pi                 mathutils.h:5
+constexpr int kWaves = 4;
+#ifndef PT_V4_CHUNK
+#define PT_V4_CHUNK 8
+#endif
+constexpr int kChunk = PT_V4_CHUNK;   // frames per LDS chunk
+
+struct V3 {
+    float x, y, z;
+};
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ V3 mul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ V3 sel(bool c, V3 a, V3 b) { return v3(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z); }
+__device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ float dot(V3 u, V3 v) { return fma_(u.x, v.x, fma_(u.y, v.y, u.z * v.z)); }   // mathlib.h:145
+__device__ __forceinline__ V3 ld3(const float* p) { return v3(p[0], p[1], p[2]); }
+__device__ __forceinline__ float max_ps(float a, float b) { return a > b ? a : b; }   // MAXPS: b on NaN
+__device__ __forceinline__ float min_ps(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ float saturate(float x) { return min_ps(max_ps(x, 0.0f), 1.0f); }
+__device__ __forceinline__ float rcp(float x) { return 1.0f / x; }                      // mathlib.h:415
+__device__ __forceinline__ float sqrt_(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ V3 normalize(V3 v) { return v * (1.0f / sqrt_(dot(v, v))); }  // mathlib.h:759
+
+__device__ __forceinline__ uint32_t wang(uint32_t& s)   // mathutils.h:8-16 (logical shifts)
+{
+    uint32_t x = s;
+    x = (x ^ 61u) ^ (x >> 16);
+    x *= 9u;
+    x = x ^ (x >> 4);
+    x *= 0x27d4eb2du;
+    x = x ^ (x >> 15);
+    s = x;
+    return x;
+}
+// Randomf3201_ps (mathutils.h:18-26): cvtepi32_ps(h & 0x7FFFFFFF) / 2^31 (an exact scaling)
+__device__ __forceinline__ float randf(uint32_t& s) { return (float)(int32_t)(wang(s) & 0x7FFFFFFFu) * 0x1p-31f; }
+
+__device__ __forceinline__ V3 ruv_rejection(uint32_t& s)   // v4 :109-130
+{
+    const float u = fma_(2.0f, randf(s), -1.0f);
+    const float v = fma_(2.0f, randf(s), -1.0f);
+    const float w = fma_(2.0f, randf(s), -1.0f);
+    const float d2 = fma_(w, w, fma_(u, u, v * v));
+    return v3(u, v, w) * (1.0f / sqrt_(d2));   // rsroot -> 1/sqrtf (mathlib.h:437)
+}
+
+__device__ __forceinline__ V3 ruv_angle(uint32_t& s)   // mathutils.h:33-46 (sincos -> glibc sinf/cosf)
+{
+    const float wz = randf(s);
+    const float wa = randf(s);
+    const float z = wz * 2.0f - 1.0f;
+    const float a = wa * (2.0f * kPi);
+    const float r = sqrt_(1.0f - z * z);
+    float sa, ca;
+    pt::sincosf_glibc(a, &sa, &ca);
+    return v3(r * ca, r * sa, z);
+}
+
+// ---- env lookups (texture.cpp) -----------------------------------------------------------------
+
+struct Tex {
+    const float* data;
+    int32_t w, h;
+};
+
+// GatherRGB (:16-26) at f32 element index `f` after cvtps_epi32 (nearest even; INT_MIN when out of
+// range).  Outside the texture the reference reads out of bounds (UB); clamped here exactly like the
+// oracle: negative / INT_MIN -> element 0, past the end -> the last texel.
+__device__ __forceinline__ V3 texel_at(const Tex& t, float f)
+{
+    f = __builtin_rintf(f);
+    const int32_t last = 3 * (t.w * t.h - 1);
+    int32_t e = 0;
+    if (f >= 0.0f && f < 2147483648.0f) {
+        e = (int32_t)f;
+        e = e > last ? last : e;
+    }
+    const float* p = t.data + (uint32_t)e;
+    return v3(p[0], p[1], p[2]);
+}
+
+// TexelSampleRandom's index 3 * cvtps_epi32(texel) (:84): texel clamped to [0, n-1] before the multiply
+__device__ __forceinline__ V3 texel_rn(const Tex& t, float f)
+{
+    f = __builtin_rintf(f);
+    const int32_t nn = t.w * t.h;
+    int32_t i = 0;
+    if (f >= 0.0f && f < 2147483648.0f) {
+        i = (int32_t)f;
+        i = i >= nn ? nn - 1 : i;
+    }
+    const float* p = t.data + 3u * (uint32_t)i;
+    return v3(p[0], p[1], p[2]);
+}
+
+__device__ __forceinline__ V3 sample_random(const Tex& t, float u, float v, uint32_t& s)   // :78-86
+{
+    const float Row = fma_(v, (float)t.h, -v);
+    const float Col = fma_(u, (float)t.w, -u);
+    const float rr = __builtin_floorf(Row + randf(s));
+    const float rc = __builtin_floorf(Col + randf(s));
+    return texel_rn(t, fma_(rr, (float)t.w, rc));
+}
+
+__device__ __forceinline__ V3 sample_bilinear(const Tex& t, float u, float v)   // :38-76
+{
+    const float Row = v * (float)(t.h - 1);
+    const float Col = u * (float)(t.w - 1);
+    float Row0 = __builtin_floorf(Row), Row1 = __builtin_ceilf(Row);
+    float Col0 = __builtin_floorf(Col), Col1 = __builtin_ceilf(Col);
+    const float dV = Row - Row0, dU = Col - Col0;
+    const float tw = 3.0f * (float)t.w;
+    Row0 = Row0 * tw;
+    Row1 = Row1 * tw;
+    Col0 = Col0 * 3.0f;
+    Col1 = Col1 * 3.0f;
+    const V3 C00 = texel_at(t, Col0 + Row0), C10 = texel_at(t, Col1 + Row0);
+    const V3 C01 = texel_at(t, Col0 + Row1), C11 = texel_at(t, Col1 + Row1);
+    const V3 C0 = C00 + (C10 - C00) * dU;   // lerp mathlib.h:763
+    const V3 C1 = C01 + (C11 - C01) * dU;
+    return C0 + (C1 - C0) * dV;
+}
+
+__device__ __forceinline__ V3 equirect(const Tex& t, V3 d, bool random, uint32_t& s)
+{
+    const float at = pt::atan2f_glibc(d.z, d.x), as = pt::asinf_glibc(d.y);
+    if (random) {   // EquirectangularTextureSampleRandom :186-203
+        float u = fma_(0.1591f, at, 0.5f), v = fma_(0.3183f, as, 0.5f);
+        u = saturate(u - __builtin_floorf(u));
+        v = saturate(v - __builtin_floorf(v));
+        return sample_random(t, u, v, s);
+    }
+    float u = at * 0.1591f + 0.5f, v = as * 0.3183f + 0.5f;   // Bilinear :164-184
+    u = u - __builtin_floorf(u);
+    v = v - __builtin_floorf(v);
+    return sample_bilinear(t, saturate(u), saturate(v));
+}
+
+__device__ __forceinline__ V3 cubemap(const Tex& t, V3 d, bool random, uint32_t& s)   // :275-404
+{
+    const float ax = __builtin_fabsf(d.x), ay = __builtin_fabsf(d.y), az = __builtin_fabsf(d.z);
+    const float k = 0.166666666666667f;
+    // face offsets: Random uses multiples of 0.166666666666667f, Bilinear i/6.f
+    const float o1 = random ? k : 1.0f / 6.0f, o2 = random ? 2.0f * k : 2.0f / 6.0f, o3 = random ? 3.0f * k : 3.0f / 6.0f;
+    const float o4 = random ? 4.0f * k : 4.0f / 6.0f, o5 = random ? 5.0f * k : 5.0f / 6.0f;
+    const bool cx = d.x >= 0.0f;
+    float fu = cx ? -d.z : d.z, fv = d.y, voff = cx ? 0.0f : o1;
+    if (ay >= ax) {
+        const bool cy = d.y >= 0.0f;
+        voff = cy ? o2 : o3;
+        fu = d.x;
+        fv = cy ? -d.z : d.z;
+    }
+    if (az >= ax && az >= ay) {
+        const bool cz = d.z >= 0.0f;
+        voff = cz ? o4 : o5;
+        fu = cz ? d.x : -d.x;
+        fv = d.y;
+    }
+    const float m = max_ps(ax, max_ps(ay, az));
+    if (random) {
+        const float r = rcp(m);
+        const float u = saturate(fma_(fu * r, 0.5f, 0.5f));
+        float v = saturate(fma_(fv * r, 0.5f, 0.5f));
+        v = saturate(fma_(v, 0.166666666666667f, voff));
+        return sample_random(t, u, v, s);
+    }
+    const float u = saturate((fu / m) * 0.5f + 0.5f);
+    float v = saturate((fv / m) * 0.5f + 0.5f);
+    v = saturate(fma_(v, 1.0f / 6.0f, voff));
+    return sample_bilinear(t, u, v);
+}
+
+// ---- intersection and shading -------------------------------------------------------------------
+
+__device__ __forceinline__ float fresnel(float n1, float n2, V3 normal, V3 incident, float f0)   // :429-453
+{
+    float r0 = (n1 - n2) * rcp(n1 + n2);
+    r0 = r0 * r0;
+    float cosX = -dot(normal, incident);
+    const bool cond = n1 > n2;
+    const float n = n1 * rcp(n2);
+    const float stc = fma_(-(n * n), fma_(-cosX, cosX, 1.0f), 1.0f);
+    const float ncos = sqrt_(stc);
+    const bool tir = 0.0f > stc;
+    cosX = (cond && !tir) ? ncos : cosX;
+    const float x = 1.0f - cosX;
+    const float x2 = x * x;
+    float ret = fma_(((1.0f - r0) * x2) * x2, x, r0);
+    ret = (cond && tir) ? 1.0f : ret;
+    return fma_(ret, 1.0f - f0, f0);
+}
+
+__device__ __forceinline__ V3 refract(V3 v, V3 n, float ior)   // rfrct, mathlib.h:781-789
+{
+    const float vdn = dot(v, n);
+    const float k = fma_(-ior, ior * fma_(-vdn, vdn, 1.0f), 1.0f);
+    const float s = fma_(ior, vdn, sqrt_(k));
+    const V3 r = v3(fma_(ior, v.x, -(s * n.x)), fma_(ior, v.y, -(s * n.y)), fma_(ior, v.z, -(s * n.z)));
+    return k < 0.0f ? v3(0.0f, 0.0f, 0.0f) : r;
+}
+
+__device__ __forceinline__ float approx_exp(float a)   // mathlib.h:501-516
+{
+    const float b = fma_(a, 0.05995203836930455f, 1.0f);
+    const float b2 = b * b, b4 = b2 * b2, b8 = b4 * b4;
+    return b8 * b8;
+}
+
+struct Hit {
+    float dist;
+    V3 n;
+    bool inside;
+    int mat;
+};
+
+// TestSceneTrace :700-718 with TestQuadTrace :556-637 / TestSphereTrace :641-695
+__device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir)
+{
+    Hit h{kSuperFar, v3(0.0f, 0.0f, 0.0f), false, 0};
+    int obj = 0;
+    for (int i = 0; i < sc.nquads; ++i, ++obj) {
+        const PtV4Quad& q = sc.quad[i];
+        const V3 n = ld3(q.n);
+        const V3 off = ld3(q.v0) - pos;
+        const float rdn = dot(dir, n);
+        const float dist = dot(off, n) * rcp(rdn);
+        const V3 hp = v3(fma_(dist, dir.x, -off.x), fma_(dist, dir.y, -off.y), fma_(dist, dir.z, -off.z));
+        const float A0 = dot(hp, ld3(q.a0)), A1 = dot(hp, ld3(q.a1)), A2 = 1.0f - A0 - A1;
+        const float B0 = dot(hp, ld3(q.b0)), B1 = dot(hp, ld3(q.b1)), B2 = 1.0f - B0 - B1;
+        const bool tri1 = A0 >= 0.0f && A1 >= 0.0f && A2 >= 0.0f;
+        const bool tri2 = B0 >= 0.0f && B1 >= 0.0f && B2 >= 0.0f;
+        if ((tri1 || tri2) && dist > kMinHit && dist < h.dist) {
+            h.inside = false;
+            h.dist = dist;
+            if (rdn > 0.0f) h.n = neg(n);   // only back-side hits write the normal (:630)
+            h.mat = obj;
+        }
+    }
+    for (int i = 0; i < sc.nspheres; ++i, ++obj) {
+        const V3 m = pos - ld3(sc.sph[i]);
+        const float r = sc.sph[i][3];
+        const float b = dot(m, dir);
+        const float c = fma_(-r, r, dot(m, m));
+        const float discr = fma_(b, b, -c);
+        const bool early = discr < 0.0f || (c > 0.0f && b > 0.0f);
+        const float s = sqrt_(discr);
+        const bool inside = -b < s;
+        const float dist = (inside ? s : -s) - b;
+        if (!early && dist > kMinHit && dist < h.dist) {
+            h.inside = inside;
+            h.dist = dist;
+            const V3 p = v3(fma_(dir.x, dist, m.x), fma_(dir.y, dist, m.y), fma_(dir.z, dist, m.z));
+            h.n = normalize(p) * (inside ? -1.0f : 1.0f);
+            h.mat = obj;
+        }
+    }
+    return h;
+}
+
+template <int LAYOUT>
+__device__ __forceinline__ size_t out_index(const PtV4Job& j, int x, int r)   // r = buffer row
+{
+    if (LAYOUT == PT_LAYOUT_INTERLEAVED) return ((size_t)r * j.width + x) * 3u;
+    if (LAYOUT == PT_LAYOUT_PLANAR8) return ((size_t)r * j.width + (size_t)(x & ~7)) * 3u + (size_t)(x & 7);
+    const int tx = x / j.tile_w, ty = r / j.tile_h;   // RenderTile :1186-1191 (tiles of the full image)
+    const int lx = x - tx * j.tile_w, ly = r - ty * j.tile_h;
+    return (size_t)ty * j.tile_h * j.width * 3u + (size_t)tx * j.tile_w * j.tile_h * 3u +
+           ((size_t)ly * j.tile_w + (size_t)(lx & ~7)) * 3u + (size_t)(lx & 7);
+}
+
+template <int ENV, int LAYOUT, bool COUNT>
+__global__ __launch_bounds__(256) void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
+{
+    __shared__ float s_col[kWaves][kChunk * 64 * 3];
+    __shared__ PtV4Mat s_mat[PT_V4_MAX_OBJECTS];
+    if (threadIdx.x < PT_V4_MAX_OBJECTS * 17)
+        reinterpret_cast<float*>(s_mat)[threadIdx.x] = reinterpret_cast<const float*>(sc.mat)[threadIdx.x];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int tiles_x = (job.ncols + 7) >> 3;
+    const int ntiles = tiles_x * ((job.nrows + 7) >> 3);
+    const int tile = (int)blockIdx.x * kWaves + wv;
+    if (tile >= ntiles) return;
+    const int tcol = (tile % tiles_x) * 8, trow = (tile / tiles_x) * 8;
+    float* const col = s_col[wv];
+
+    // this lane's pixel (phase C) and its accumulator
+    const int px = job.col0 + tcol + (lane & 7), pr = trow + (lane >> 3);
+    const bool pvalid = (tcol + (lane & 7)) < job.ncols && pr < job.nrows;
+    const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;
+    float* acc_p = nullptr;
+    V3 acc = v3(0.0f, 0.0f, 0.0f);
+    if (pvalid) {
+        acc_p = job.buf + out_index<LAYOUT>(job, px, pr);
+        acc = v3(acc_p[0], acc_p[cs], acc_p[2 * cs]);
+    }
+    const Tex tex{job.env, job.env_w, job.env_h};
+    const bool random = job.random_jitter != 0, rejection = job.rejection != 0;
+    const int B = job.num_bounces;
+    const float W = (float)job.width, H = (float)job.height;
+    const float rW = rcp(W), rH = rcp(H);
+    const float cam_dist = 1.0f;   // 1 / tanf(c_FOVDegrees * 0.5f * c_pi / 180.0f) == 1.0f exactly (InitializeCamera :1500)
+    unsigned long long n_seg = 0, n_esc = 0, n_slots = 0;
+
+    for (int c0 = 0; c0 < job.nframes; c0 += kChunk) {
+        const int nf = std::min(kChunk, job.nframes - c0);
+        const int total = 64 * nf;
+        int next = 0;      // wave-uniform
+        int item = -1;     // this lane's (pixel, frame) sample, -1 = none
+        V3 pos, dir, T, ret;
+        uint32_t rng = 0;
+        int bounce = 0;
+        for (;;) {
+            // hand out items to idle lanes, in lane order
+            const bool need = item < 0;
+            const unsigned long long m = __ballot(need);
+            if (need) {
+                const int it = next + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                if (it < total) {
+                    const int p = it & 63, f = it >> 6;
+                    const int X = job.col0 + tcol + (p & 7), rb = trow + (p >> 3);
+                    if ((tcol + (p & 7)) < job.ncols && rb < job.nrows) {
+                        item = it;
+                        // mainImage :1092-1130
+                        const int Y = job.row_start + rb * job.row_stride;
+                        const uint32_t frame = job.frame_first + (uint32_t)(c0 + f);
+                        const int fyi = job.height - 1 - Y;
+                        rng = 1u | ((uint32_t)X * 1973u + (uint32_t)fyi * 9277u + frame * 26699u);
+                        const float jx = randf(rng) - 0.5f;
+                        const float jy = randf(rng) - 0.5f;
+                        const float tx = fma_(((float)X + jx) * rW, 2.0f, -1.0f);
+                        float ty = fma_(((float)fyi + jy) * rH, 2.0f, -1.0f);
+                        ty = ty * (rW * H);
+                        dir = normalize(v3(tx, ty, -cam_dist) - v3(0.0f, 0.0f, 0.0f));
+                        pos = v3(0.0f, 0.0f, 1.0f * 40.0f);   // camera.Position :1501
+                        T = v3(1.0f, 1.0f, 1.0f);
+                        ret = v3(0.0f, 0.0f, 0.0f);
+                        bounce = 0;
+                    }
+                }
+            }
+            next += __builtin_popcountll(m);
+            if (__ballot(item >= 0) == 0ull) break;
+            if (COUNT) n_slots += 64;
+            if (item >= 0) {
+                // one iteration of GetColorForRay's bounce loop (:733-909)
+                const Hit h = trace(sc, pos, dir);
+                if (COUNT) ++n_seg;
+                const bool miss = h.dist == kSuperFar;
+                bool done = false;
+                if (miss) {
+                    V3 amb = v3(0.11f, 0.1f, 0.15f);   // :782
+                    if (ENV == PT_V4_ENV_EQUIRECT_) amb = equirect(tex, v3(-dir.x, dir.y, -dir.z), random, rng);
+                    if (ENV == PT_V4_ENV_CUBEMAP_) amb = cubemap(tex, dir, random, rng);
+                    ret = v3(fma_(amb.x, T.x, ret.x), fma_(amb.y, T.y, ret.y), fma_(amb.z, T.z, ret.z));   // :787
+                    done = true;
+                    if (COUNT) ++n_esc;
+                } else {
+                    if (ENV != PT_V4_ENV_NONE_ && random) {   // the env sample's two draws happen on hits too
+                        wang(rng);
+                        wang(rng);
+                    }
+                    const PtV4Mat& M = s_mat[h.mat];
+                    if (h.inside)   // :797
+                        T = mul(T, v3(approx_exp(-M.refr_color[0] * h.dist), approx_exp(-M.refr_color[1] * h.dist),
+                                      approx_exp(-M.refr_color[2] * h.dist)));
+                    const V3 em = ld3(M.emissive);
+                    if (bounce == B) {   // last iteration: only its emissive term is used
+                        ret = v3(fma_(em.x, T.x, ret.x), fma_(em.y, T.y, ret.y), fma_(em.z, T.z, ret.z));
+                        done = true;
+                    } else {
+                        float spec = M.spec_chance, refr = M.refr_chance;
+                        {   // :807-829
+                            const bool has_spec = spec > 0.0f;
+                            const float n1 = h.inside ? M.ior : 1.0f, n2 = h.inside ? 1.0f : M.ior;
+                            const float nspec = fresnel(n1, n2, h.n, dir, M.spec_chance);
+                            const float rscc = rcp(1.0f - M.spec_chance);
+                            const float mult = fma_(-nspec, rscc, rscc);
+                            if (has_spec) {
+                                spec = nspec;
+                                refr = refr * mult;
+                            }
+                        }
+                        const float roll = randf(rng);   // :831
+                        const bool do_spec = spec > 0.0f && roll < spec;
+                        const bool do_refr = !do_spec && refr > 0.0f && roll < spec + refr;
+                        const float diff_chance = max_ps(1.0f - (spec + refr), 0.0f);
+                        float prob = do_spec ? spec : (do_refr ? refr : diff_chance);
+                        prob = max_ps(prob, 0.001f);
+                        const float nudge = kNudge * (do_refr ? -1.0f : 1.0f);   // :848-849
+                        const V3 npos = v3(fma_(nudge, h.n.x, fma_(dir.x, h.dist, pos.x)),
+                                           fma_(nudge, h.n.y, fma_(dir.y, h.dist, pos.y)),
+                                           fma_(nudge, h.n.z, fma_(dir.z, h.dist, pos.z)));
+                        V3 ndir;
+                        {   // :852-888
+                            V3 diffuse;
+                            if (rejection) {
+                                const V3 a = h.n + ruv_rejection(rng);
+                                diffuse = a * (1.0f / sqrt_(dot(a, a)));   // fast_approx_normalize, rsroot -> 1/sqrtf
+                            } else {
+                                diffuse = normalize(h.n + ruv_angle(rng));
+                            }
+                            const float d2 = 2.0f * dot(dir, h.n);
+                            V3 sd = v3(fma_(-d2, h.n.x, dir.x), fma_(-d2, h.n.y, dir.y), fma_(-d2, h.n.z, dir.z));
+                            const float srsq = M.spec_rough * M.spec_rough;
+                            sd = v3(fma_(srsq, diffuse.x - sd.x, sd.x), fma_(srsq, diffuse.y - sd.y, sd.y),
+                                    fma_(srsq, diffuse.z - sd.z, sd.z));
+                            const float ior = h.inside ? M.ior : rcp(M.ior);
+                            const float rrsq = M.refr_rough * M.refr_rough;
+                            V3 rd = refract(dir, h.n, ior);
+                            if (rejection) {
+                                const V3 a = ruv_rejection(rng) - h.n;
+                                const V3 nrd = a * (1.0f / sqrt_(dot(a, a)));
+                                rd = v3(fma_(rrsq, nrd.x - rd.x, rd.x), fma_(rrsq, nrd.y - rd.y, rd.y),
+                                        fma_(rrsq, nrd.z - rd.z, rd.z));
+                            } else {
+                                const V3 nrd = normalize(ruv_angle(rng) - h.n);
+                                rd = normalize(rd + (nrd - rd) * rrsq);
+                            }
+                            ndir = sel(do_spec, sd, diffuse);
+                            ndir = sel(do_refr, rd, ndir);
+                            ndir = normalize(ndir);
+                        }
+                        ret = v3(fma_(em.x, T.x, ret.x), fma_(em.y, T.y, ret.y), fma_(em.z, T.z, ret.z));
+                        const V3 cf = do_spec ? ld3(M.spec_color) : ld3(M.albedo);
+                        if (!do_refr) T = mul(T, cf);
+                        T = T * rcp(prob);
+                        {   // :891-899 (boost only; the path continues either way)
+                            const float pm = max_ps(T.x, max_ps(T.y, T.z));
+                            const bool term = randf(rng) > pm;
+                            if (!term) T = T * rcp(pm);
+                        }
+                        pos = npos;
+                        dir = ndir;
+                        ++bounce;
+                    }
+                }
+                if (done) {
+                    const int p = item & 63, f = item >> 6;
+                    float* o = col + (f * 64 + p) * 3;
+                    // mainImage :1127: fmadd(color, 1/c_numRendersPerFrame, 0)
+                    o[0] = fma_(ret.x, 1.0f, 0.0f);
+                    o[1] = fma_(ret.y, 1.0f, 0.0f);
+                    o[2] = fma_(ret.z, 1.0f, 0.0f);
+                    item = -1;
+                }
+            }
+        }
+        // all radiance of this chunk is in LDS (written by lanes of this wave)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (pvalid) {
+            for (int f = 0; f < nf; ++f) {
+                const float* c = col + (f * 64 + lane) * 3;
+                const float bf = 1.0f / ((float)(job.frame_first + (uint32_t)(c0 + f)) + 1.0f);   // :1200
+                acc = v3(fma_(bf, c[0] - acc.x, acc.x), fma_(bf, c[1] - acc.y, acc.y), fma_(bf, c[2] - acc.z, acc.z));
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (pvalid) {
+        acc_p[0] = acc.x;
+        acc_p[cs] = acc.y;
+        acc_p[2 * cs] = acc.z;
+    }
+    if (COUNT) {
+        // per-lane counts summed over the wave by lane 0's atomics
+        for (int off = 32; off > 0; off >>= 1) {
+            n_seg += __shfl_down(n_seg, off);
+            n_esc += __shfl_down(n_esc, off);
+        }
+        if (lane == 0) {
+            atomicAdd(&job.counters[0], n_seg);
+            atomicAdd(&job.counters[2], n_esc);
+            atomicAdd(&job.counters[3], n_slots);
+        }
+    }
+}
+
+template <int ENV, int LAYOUT>
+hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool count)
+{
+    const int tiles = ((j.ncols + 7) / 8) * ((j.nrows + 7) / 8);
+    const dim3 grid((unsigned)((tiles + kWaves - 1) / kWaves)), block(256);
+    if (count) hipLaunchKernelGGL((pt_v4_kernel<ENV, LAYOUT, true>), grid, block, 0, st, j, sc);
+    else hipLaunchKernelGGL((pt_v4_kernel<ENV, LAYOUT, false>), grid, block, 0, st, j, sc);
+    return hipGetLastError();
+}
+
+template <int ENV>
+hipError_t launch_env(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool count)
+{
+    switch (j.layout) {
+        case PT_LAYOUT_INTERLEAVED: return launch_t<ENV, PT_LAYOUT_INTERLEAVED>(j, sc, st, count);
+        case PT_LAYOUT_PLANAR8: return launch_t<ENV, PT_LAYOUT_PLANAR8>(j, sc, st, count);
+        case PT_LAYOUT_TILED_PLANAR8: return launch_t<ENV, PT_LAYOUT_TILED_PLANAR8>(j, sc, st, count);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+hipError_t pt_launch_v4(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool count)
+{
+    if (j.ncols <= 0 || j.nrows <= 0 || j.nframes <= 0) return hipSuccess;
+    if (sc.nquads < 0 || sc.nspheres < 0 || sc.nquads + sc.nspheres > PT_V4_MAX_OBJECTS) return hipErrorInvalidValue;
+    if (j.env_mode != PT_V4_ENV_NONE_ && (!j.env || j.env_w <= 0 || j.env_h <= 0)) return hipErrorInvalidValue;
+    if (count && !j.counters) return hipErrorInvalidValue;
+    switch (j.env_mode) {
+        case PT_V4_ENV_NONE_: return launch_env<PT_V4_ENV_NONE_>(j, sc, st, count);
+        case PT_V4_ENV_EQUIRECT_: return launch_env<PT_V4_ENV_EQUIRECT_>(j, sc, st, count);
+        case PT_V4_ENV_CUBEMAP_: return launch_env<PT_V4_ENV_CUBEMAP_>(j, sc, st, count);
+        default: return hipErrorInvalidValue;
+    }
+}

@@ -72,3 +72,24 @@ def count_device(buf, width: int, height: int, *, frame_first: int, nframes: int
     N.check(N.load().pt_count_device(ctypes.byref(job), _stream(stream), ctypes.byref(out)), "pt_count_device")
     return {"segments": out.segments, "lane_slots": out.lane_slots, "samples": out.samples, "escaped": out.escaped,
             "primary": out.primary}
+
+
+def render_v4_device(buf, width: int, height: int, *, frame_first: int, nframes: int, num_bounces: int = 8,
+                     row_start: int = 0, row_stride: int = 1, nrows: int | None = None,
+                     layout: int = N.PT_LAYOUT_INTERLEAVED, use_env: bool = False, stream=None) -> None:
+    """The v4 renderer on an HBM-resident accumulator (see render_device); use_env selects the env
+    mode of renderer.v4_config with the map of set_env_map.  Asynchronous on `stream`."""
+    nrows = height if nrows is None else nrows
+    job = _job(buf, width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces, layout, use_env)
+    N.check(N.load().pt_v4_render_device(ctypes.byref(job), _stream(stream)), "pt_v4_render_device")
+
+
+def count_v4_device(buf, width: int, height: int, *, frame_first: int, nframes: int, num_bounces: int = 8,
+                    row_start: int = 0, row_stride: int = 1, nrows: int | None = None,
+                    layout: int = N.PT_LAYOUT_INTERLEAVED, use_env: bool = False, stream=None) -> dict:
+    """render_v4_device + work counters (segments, lane_slots, samples, escaped).  Synchronous."""
+    nrows = height if nrows is None else nrows
+    job = _job(buf, width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces, layout, use_env)
+    out = N.PtWorkCounts()
+    N.check(N.load().pt_v4_count_device(ctypes.byref(job), _stream(stream), ctypes.byref(out)), "pt_v4_count_device")
+    return {"segments": out.segments, "lane_slots": out.lane_slots, "samples": out.samples, "escaped": out.escaped}

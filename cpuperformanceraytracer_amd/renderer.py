@@ -221,18 +221,118 @@ def tonemap(accum: np.ndarray, width: int, height: int, layout: int = N.PT_LAYOU
     return out
 
 
+def _pixels(a, width: int, height: int, what: str) -> int:
+    if (not isinstance(a, np.ndarray) or a.dtype != np.uint32 or not a.flags["C_CONTIGUOUS"]
+            or not a.flags["WRITEABLE"] or a.size < width * height):
+        raise N.PtError(N.PT_EINVAL, what, "pixel buffer must be a writeable contiguous uint32 array of W*H")
+    return a.ctypes.data
+
+
 def CopyOutputToFile(BufferOut: np.ndarray, BufferWidth: int, BufferHeight: int, NumTilesX: int, NumTilesY: int,
                      TileWidth: int, TileHeight: int, NumChannels: int, Texture, ScreenBufferData: np.ndarray) -> None:
-    """v4 :1729-1760 (the post-process it documents): the tiled accumulator -> ScreenBufferData,
-    BufferWidth x BufferHeight u32 file pixels (bytes R, G, B, A = 255)."""
-    if NumChannels != 3 or NumTilesX * TileWidth != BufferWidth or NumTilesY * TileHeight != BufferHeight:
-        raise N.PtError(N.PT_EINVAL, "CopyOutputToFile", "invalid tiling / channels")
-    if (not isinstance(ScreenBufferData, np.ndarray) or ScreenBufferData.dtype != np.uint32
-            or not ScreenBufferData.flags["C_CONTIGUOUS"] or ScreenBufferData.size < BufferWidth * BufferHeight):
-        raise N.PtError(N.PT_EINVAL, "CopyOutputToFile", "ScreenBufferData must be a contiguous uint32 array of W*H")
-    a = _buf(BufferOut, BufferWidth, BufferHeight, 3)
-    N.check(N.load().pt_tonemap(a, BufferWidth, BufferHeight, N.PT_LAYOUT_TILED_PLANAR8, TileWidth, TileHeight,
-                                ScreenBufferData.ctypes.data, N.PT_PIXEL_RGBA8), "CopyOutputToFile")
+    """v4 :1729-1760 (the post-process it documents): advances v4's iFrame (:1738), then the tiled
+    accumulator -> ScreenBufferData, BufferWidth x BufferHeight u32 file pixels (bytes R, G, B, A = 255)."""
+    px = _pixels(ScreenBufferData, BufferWidth, BufferHeight, "CopyOutputToFile")
+    a = _buf(BufferOut, BufferWidth, BufferHeight, NumChannels)
+    N.check(N.load().pt_copy_output_to_file(a, BufferWidth, BufferHeight, NumTilesX, NumTilesY, TileWidth, TileHeight,
+                                            NumChannels, px), "CopyOutputToFile")
+
+
+# ---- v4 renderer (demofox_path_tracing_optimization_v4.cpp) -------------------------------------------
+
+def LoadCubemapTexture(filenames) -> texture:
+    """asset_loading.cpp:18-44: six .hdr faces (px nx py ny pz nz) stacked into W x 6H."""
+    if len(filenames) != 6:
+        raise N.PtError(N.PT_EINVAL, "LoadCubemapTexture", "six face files expected")
+    arr = (ctypes.c_char_p * 6)(*[str(f).encode() for f in filenames])
+    pt = N.PtTexture()
+    N.check(N.load().pt_load_cubemap_texture(arr, ctypes.byref(pt)), "LoadCubemapTexture")
+    return _from_pt_texture(pt)
+
+
+def v4_config(env_mode: int = N.PT_V4_ENV_EQUIRECT, random_jitter: bool = True, rejection: bool = True,
+              num_bounces: int = 8, output_to_screen: bool = True) -> None:
+    """The v4 switches of global_preprocessor_flags.h (USE_ENV_MAP / USE_ENV_CUBEMAP,
+    USE_RANDOM_JITTER_TEXTURE_SAMPLING, USE_UNIT_VECTOR_REJECTION_SAMPLING, OUTPUT_TO_SCREEN) and
+    c_numBounces (v4 :23)."""
+    c = N.PtV4Config(env_mode, int(random_jitter), int(rejection), num_bounces, int(output_to_screen))
+    N.check(N.load().pt_v4_set_config(ctypes.byref(c)), "pt_v4_set_config")
+
+
+def InitializeGlobalRenderResources() -> None:
+    """v4 :1640-1661: camera and InitializeScene on first use."""
+    N.check(N.load().pt_v4_initialize_global_render_resources(), "InitializeGlobalRenderResources")
+
+
+def ReinitializeRenderTileData() -> None:
+    """v4 :1723-1726 (accepted; every call uses its own arguments)."""
+    N.check(N.load().pt_v4_reinitialize_render_tile_data(), "ReinitializeRenderTileData")
+
+
+def InitializeScene() -> None:
+    """v4 :1403-1496: replace the scene by the reference's default (4 quads, 7 glass spheres)."""
+    N.check(N.load().pt_v4_initialize_scene(), "InitializeScene")
+
+
+def ClearScene() -> None:
+    N.check(N.load().pt_v4_clear_scene(), "pt_v4_clear_scene")
+
+
+def AddMaterialToScene(albedo=(0, 0, 0), emissive=(0, 0, 0), specular_chance=0.0, specular_roughness=0.0,
+                       specular_color=(0, 0, 0), ior=0.0, refraction_chance=0.0, refraction_roughness=0.0,
+                       refraction_color=(0, 0, 0)) -> int:
+    """v4 :1368-1388 (SceneMaterial fields; zero defaults like `SceneMaterial{ 0 }`).  Returns its index."""
+    m = N.PtV4Material((ctypes.c_float * 3)(*albedo), (ctypes.c_float * 3)(*emissive), specular_chance,
+                       specular_roughness, (ctypes.c_float * 3)(*specular_color), ior, refraction_chance,
+                       refraction_roughness, (ctypes.c_float * 3)(*refraction_color))
+    rc = N.load().pt_v4_add_material(ctypes.byref(m))
+    if rc < 0:
+        N.check(rc, "AddMaterialToScene")
+    return rc
+
+
+def AddQuadObjectToScene(vertices) -> int:
+    """v4 :1390-1395: four vertices (V0..V3, xyz).  Returns the quad count."""
+    v = np.ascontiguousarray(vertices, dtype=np.float32).reshape(12)
+    rc = N.load().pt_v4_add_quad(v.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    if rc < 0:
+        N.check(rc, "AddQuadObjectToScene")
+    return rc
+
+
+def AddSphereObjectToScene(position_radius) -> int:
+    """v4 :1397-1401: (x, y, z, r).  Returns the quad count, like the reference."""
+    v = np.ascontiguousarray(position_radius, dtype=np.float32).reshape(4)
+    rc = N.load().pt_v4_add_sphere(v.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    if rc < 0:
+        N.check(rc, "AddSphereObjectToScene")
+    return rc
+
+
+def v4_set_frame(frame: int) -> None:
+    N.check(N.load().pt_v4_set_frame(frame), "pt_v4_set_frame")
+
+
+def v4_get_frame() -> int:
+    return int(N.load().pt_v4_get_frame())
+
+
+def DemofoxRenderOptV4(BufferOut: np.ndarray, BufferWidth: int, BufferHeight: int, NumTilesX: int, NumTilesY: int,
+                       TileWidth: int, TileHeight: int, NumChannels: int, Texture=None,
+                       ScreenBufferData: np.ndarray | None = None) -> None:
+    """v4 :1696-1721: advance iFrame, render every tile (tiled planar8 accumulator) and, when
+    ScreenBufferData is given (OUTPUT_TO_SCREEN), write its XRGB8 pixels."""
+    L = N.load()
+    keep = None
+    tp = None
+    if Texture is not None:
+        pt, keep = _pt_texture(Texture)
+        tp = ctypes.byref(pt)
+    scr = None if ScreenBufferData is None else _pixels(ScreenBufferData, BufferWidth, BufferHeight, "DemofoxRenderOptV4")
+    N.check(L.pt_render_opt_v4(_buf(BufferOut, BufferWidth, BufferHeight, NumChannels), BufferWidth, BufferHeight,
+                               NumTilesX, NumTilesY, TileWidth, TileHeight, NumChannels, tp, scr),
+            "DemofoxRenderOptV4")
+    del keep
 
 
 def WriteImage(filename, width: int, height: int, components: int, data: np.ndarray) -> None:

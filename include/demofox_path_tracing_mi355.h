@@ -51,10 +51,24 @@ texture LoadTexture(char* filename);
 void DemofoxRenderSimtTextured(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY,
                                i32 TileWidth, i32 TileHeight, i32 NumChannels, texture Texture);
 
+// asset_loading.h:7: six faces (px nx py ny pz nz) stacked vertically; Data == 0 on failure.
+texture LoadCubemapTexture(char* filename[6]);
+
+// demofox_path_tracing_optimization_v4.h:14-26 -- the shipping renderer (Application.cpp:474).
+// DemofoxRenderOptV4 advances v4's iFrame, renders every tile into the tiled accumulator and, with
+// OUTPUT_TO_SCREEN (pt_v4_config.output_to_screen, default 1) and ScreenBufferData != 0, writes the
+// BufferWidth x BufferHeight XRGB8 screen pixels (OutputToScreen v4 :1260-1295).  The env-map mode
+// and sampling switches of global_preprocessor_flags.h are pt_v4_set_config() (default: equirect,
+// random-jitter texel sampling, rejection-sampled unit vectors).
+void DemofoxRenderOptV4(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY,
+                        i32 TileWidth, i32 TileHeight, i32 NumChannels, texture Texture, void* ScreenBufferData);
+void InitializeGlobalRenderResources();
+void ReinitializeRenderTileData();
+
 // The post-process of the tiled accumulator into 32-bit file pixels (bytes R, G, B, A = 255):
-// ACES + sRGB + 8-bit, v4 :1297-1331.  (The reference's function also advances iFrame and, through
-// its pool's callback mix-up (v4 :1588 vs :1756), re-renders; only the documented post-process is
-// performed here.)  Texture is unused, as in the reference.
+// ACES + sRGB + 8-bit, v4 :1297-1331, after advancing v4's iFrame (:1738).  (Through its pool's
+// callback mix-up (v4 :1588 vs :1756) the reference's function may also re-render tiles; only the
+// documented post-process is performed here.)  Texture is unused, as in the reference.
 void CopyOutputToFile(f32* BufferOut, i32 BufferWidth, i32 BufferHeight, i32 NumTilesX, i32 NumTilesY, i32 TileWidth,
                       i32 TileHeight, i32 NumChannels, texture Texture, void* ScreenBufferData);
 // stbi_write_bmp: a 24-bit BMP (asset_loading.cpp:48-54).  Prints pt_last_error() on failure.

@@ -125,6 +125,9 @@ int pt_readback(float* buf);
 int pt_load_texture(const char* path, pt_texture* out);
 int pt_decode_hdr(const void* bytes, size_t nbytes, pt_texture* out);   /* same, from memory */
 void pt_free_texture(pt_texture* tex);
+/* replaces LoadCubemapTexture (asset_loading.h:7, .cpp:18-44): six .hdr faces (px nx py ny pz nz)
+ * stacked vertically into one width x 6*height texture (the layout the cubemap samplers index) */
+int pt_load_cubemap_texture(const char* const paths[6], pt_texture* out);
 /* copy `tex` into HBM as the env map of device jobs with use_env (NULL: release it) */
 int pt_set_env_map(const pt_texture* tex);
 /* replaces DemofoxRenderSimtTextured, demofox_path_tracing_simt_textured.h:8 / .cpp:560-620:
@@ -146,6 +149,69 @@ int pt_tonemap_device(const float* accum, int32_t width, int32_t height, int32_t
                       int32_t tile_height, uint32_t* out, int32_t format, void* hip_stream);   /* async */
 /* replaces WriteImage (asset_loading.h:8, .cpp:48-54: stbi_write_bmp, 24-bit BMP) */
 int pt_write_bmp(const char* path, int32_t width, int32_t height, int32_t components, const void* data);
+
+/* --- v4 renderer: the reference's shipping path -------------------------------
+ * demofox_path_tracing_optimization_v4.cpp, called by ApplicationState::Render (Application.cpp:474):
+ * diffuse / specular / refraction materials (Fresnel-Schlick, Beer absorption, roughness), Russian-
+ * roulette throughput boost, jittered camera, throughput-weighted env map.  Its own frame counter
+ * (the file's `static f32 iFrame`, v4 :34) and scene (v4 :1403-1496, editable through the Add*
+ * functions).  Results are bit-identical to oracle/pt_oracle_v4.c, which restates v4 with the exact
+ * 1/x and 1/sqrtf(x) for the x86 rcp/rsqrt approximations and glibc atan2f/asinf/sinf/cosf for SVML. */
+#define PT_V4_ENV_NONE 0        /* USE_ENV_MAP 0: ambient (0.11, 0.1, 0.15), v4 :782             */
+#define PT_V4_ENV_EQUIRECT 1    /* USE_ENV_MAP 1, USE_ENV_CUBEMAP 0 (global_preprocessor_flags.h:58-59) */
+#define PT_V4_ENV_CUBEMAP 2     /* USE_ENV_CUBEMAP 1: six faces stacked vertically (LoadCubemapTexture,  */
+                                /*   asset_loading.cpp:18-44, order px nx py ny pz nz)                  */
+#define PT_V4_MAX_OBJECTS 12    /* MAX_OBJECTS / MAX_MATERIALS (v4 :351-352): quads + spheres <= 12     */
+
+/* Runtime form of the v4 compile-time switches (global_preprocessor_flags.h, v4 :23). */
+typedef struct pt_v4_config {
+    int32_t env_mode;            /* PT_V4_ENV_*; default PT_V4_ENV_EQUIRECT                               */
+    int32_t random_jitter;       /* USE_RANDOM_JITTER_TEXTURE_SAMPLING (1) else bilinear texel sampling     */
+    int32_t rejection;           /* USE_UNIT_VECTOR_REJECTION_SAMPLING (1) else RandomUnitVector_ps (sin/cos) */
+    int32_t num_bounces;         /* c_numBounces (v4 :23): 8                                                */
+    int32_t output_to_screen;    /* OUTPUT_TO_SCREEN (flags.h:60, 1): DemofoxRenderOptV4 also writes the    */
+                                 /*   ScreenBufferData pixels (OutputToScreen v4 :1260-1295) when non-NULL  */
+} pt_v4_config;
+
+/* SceneMaterial (v4 :367-378), the argument of AddMaterialToScene. */
+typedef struct pt_v4_material {
+    float albedo[3], emissive[3];
+    float specular_chance, specular_roughness, specular_color[3];
+    float ior, refraction_chance, refraction_roughness, refraction_color[3];
+} pt_v4_material;
+
+void pt_v4_default_config(pt_v4_config* cfg);
+int pt_v4_set_config(const pt_v4_config* cfg);
+/* InitializeGlobalRenderResources (v4 :1640-1661): camera + InitializeScene on first use */
+int pt_v4_initialize_global_render_resources(void);
+/* ReinitializeRenderTileData (v4 :1723-1726); accepted for the call surface -- every
+ * pt_render_opt_v4 call uses its own arguments */
+int pt_v4_reinitialize_render_tile_data(void);
+/* scene editing: the reference's InitializeScene / AddMaterialToScene / AddQuadObjectToScene /
+ * AddSphereObjectToScene (v4 :1403, :1368, :1390, :1397) plus an explicit clear.  Material i shades
+ * object i (quads first, then spheres: TestSceneTrace v4 :700-718). */
+int pt_v4_initialize_scene(void);                     /* the default scene (replaces the current one)   */
+int pt_v4_clear_scene(void);
+int pt_v4_add_material(const pt_v4_material* m);      /* returns its index (>= 0) or PT_E*              */
+int pt_v4_add_quad(const float vertices[12]);         /* V0..V3 xyz; returns the quad count or PT_E*    */
+int pt_v4_add_sphere(const float position_radius[4]); /* returns the quad count (as v4 :1400) or PT_E*  */
+int pt_v4_set_frame(uint32_t frame);
+uint32_t pt_v4_get_frame(void);
+/* replaces DemofoxRenderOptV4 (v4 .h:14, .cpp:1696-1721): advance iFrame, render every tile into the
+ * tiled accumulator (RenderTile v4 :1179-1258 layout), then (output_to_screen, screen != NULL) write
+ * width*height XRGB8 pixels into `screen`.  tex may be NULL with PT_V4_ENV_NONE. */
+int pt_render_opt_v4(float* buf, int32_t width, int32_t height, int32_t num_tiles_x, int32_t num_tiles_y,
+                     int32_t tile_width, int32_t tile_height, int32_t num_channels, const pt_texture* tex,
+                     void* screen);
+/* replaces CopyOutputToFile (v4 .h:19, .cpp:1729-1760): iFrame += 1 (:1738), then the tiled
+ * accumulator -> width*height RGBA8 file pixels (OutputToFile :1297-1331) */
+int pt_copy_output_to_file(const float* buf, int32_t width, int32_t height, int32_t num_tiles_x,
+                           int32_t num_tiles_y, int32_t tile_width, int32_t tile_height, int32_t num_channels,
+                           void* file_pixels);
+/* HBM-resident v4 job (bench / shards): the interleaved or planar8 layout; use_env selects the
+ * config's env mode with the map of pt_set_env_map (else the ambient); num_bounces from the job */
+int pt_v4_render_device(const pt_device_job* job, void* hip_stream);
+int pt_v4_count_device(const pt_device_job* job, void* hip_stream, pt_work_counts* out);   /* sync */
 
 /* --- device-resident entry points -------------------------------------------------------------- */
 int pt_render_device(const pt_device_job* job, void* hip_stream);      /* async on hip_stream     */

@@ -81,6 +81,51 @@ uint32_t pto_tonemap_channel(float linear);
 uint32_t pto_tonemap_pixel(const float rgb[3], int32_t format);
 void pto_tonemap(const float* rgb, int32_t w, int32_t h, int32_t format, uint32_t* out);
 
+/* ---- v4 renderer (pt_oracle_v4.c): demofox_path_tracing_optimization_v4.cpp restated ---------- */
+#define PTO4_MAX_OBJECTS 12      /* MAX_OBJECTS / MAX_MATERIALS, v4 :351-352 (quads + spheres <= 12) */
+#define PTO4_ENV_NONE 0          /* USE_ENV_MAP 0: ambient (0.11, 0.1, 0.15), v4 :782            */
+#define PTO4_ENV_EQUIRECT 1      /* USE_ENV_MAP 1, USE_ENV_CUBEMAP 0 (flags.h:58-59, default)     */
+#define PTO4_ENV_CUBEMAP 2       /* USE_ENV_CUBEMAP 1: six faces stacked (LoadCubemapTexture)     */
+
+typedef struct pto4_material {   /* SceneMaterial, v4 :367-378 */
+    float albedo[3], emissive[3];
+    float spec_chance, spec_rough, spec_color[3];
+    float ior, refr_chance, refr_rough, refr_color[3];
+} pto4_material;
+
+typedef struct pto4_scene {      /* the arguments of AddQuad/Sphere/MaterialToScene, in call order */
+    int32_t nquads, nspheres, nmat;
+    float quad[PTO4_MAX_OBJECTS][4][3];   /* V0..V3, already translated (v4 :1415-1418)          */
+    float sphere[PTO4_MAX_OBJECTS][4];    /* PositionAndRadius                                   */
+    pto4_material mat[PTO4_MAX_OBJECTS];  /* object index order: quads first, then spheres       */
+} pto4_scene;
+
+typedef struct pto4_params {
+    int32_t width, height, row_start, row_stride, nrows;
+    uint32_t frame_first;         /* the static iFrame of the first frame (>= 1)                 */
+    int32_t nframes;
+    int32_t num_bounces;          /* c_numBounces, v4 :23 (8)                                    */
+    int32_t env_mode;             /* PTO4_ENV_*                                                  */
+    int32_t random_jitter;        /* USE_RANDOM_JITTER_TEXTURE_SAMPLING (1) else bilinear         */
+    int32_t rejection;            /* USE_UNIT_VECTOR_REJECTION_SAMPLING (1) else sin/cos          */
+    const pto_env* env;           /* equirect map or stacked cubemap; NULL => ambient             */
+    int32_t nthreads;
+} pto4_params;
+
+typedef struct pto4_counts {
+    uint64_t samples, segments, escaped;
+} pto4_counts;
+
+void pto4_default_scene(pto4_scene* s);   /* InitializeScene, v4 :1403-1496 */
+/* Render into buf (nrows x width x 3 f32, interleaved, accumulating in place); scene NULL =>
+ * the default scene; counts (optional) forces one thread.  0 on success. */
+int pto4_render(float* buf, const pto4_params* p, const pto4_scene* scene, pto4_counts* counts);
+int pto4_scene_tables(const pto4_scene* scene, float* out, int32_t n);
+float pto4_randomf(uint32_t* state);                                          /* mathutils.h:18-26 */
+void pto4_random_unit_vector(uint32_t* state, int rejection, float out[3]);   /* v4 :109 / mathutils.h:33 */
+void pto4_env_sample(const pto_env* env, int32_t env_mode, int32_t random_jitter, const float dir[3],
+                     uint32_t* state, float out[3]);                          /* v4 :769-784 */
+
 #ifdef __cplusplus
 }
 #endif

@@ -160,3 +160,117 @@ def tonemap(rgb: np.ndarray, fmt: int = PIXEL_RGBA8) -> np.ndarray:
 
 def tonemap_channel(v: float) -> int:
     return int(load().pto_tonemap_channel(float(v)))
+
+
+# ---- v4 renderer (pt_oracle_v4.c) -----------------------------------------------------------------
+ENV_NONE, ENV_EQUIRECT, ENV_CUBEMAP = 0, 1, 2
+MAX_OBJECTS = 12
+
+
+class Material4(ctypes.Structure):
+    _fields_ = [("albedo", ctypes.c_float * 3), ("emissive", ctypes.c_float * 3), ("spec_chance", ctypes.c_float),
+                ("spec_rough", ctypes.c_float), ("spec_color", ctypes.c_float * 3), ("ior", ctypes.c_float),
+                ("refr_chance", ctypes.c_float), ("refr_rough", ctypes.c_float), ("refr_color", ctypes.c_float * 3)]
+
+
+class Scene4(ctypes.Structure):
+    _fields_ = [("nquads", ctypes.c_int32), ("nspheres", ctypes.c_int32), ("nmat", ctypes.c_int32),
+                ("quad", ctypes.c_float * 3 * 4 * MAX_OBJECTS), ("sphere", ctypes.c_float * 4 * MAX_OBJECTS),
+                ("mat", Material4 * MAX_OBJECTS)]
+
+
+class Params4(ctypes.Structure):
+    _fields_ = [("width", ctypes.c_int32), ("height", ctypes.c_int32), ("row_start", ctypes.c_int32),
+                ("row_stride", ctypes.c_int32), ("nrows", ctypes.c_int32), ("frame_first", ctypes.c_uint32),
+                ("nframes", ctypes.c_int32), ("num_bounces", ctypes.c_int32), ("env_mode", ctypes.c_int32),
+                ("random_jitter", ctypes.c_int32), ("rejection", ctypes.c_int32), ("env", ctypes.POINTER(Env)),
+                ("nthreads", ctypes.c_int32)]
+
+
+class Counts4(ctypes.Structure):
+    _fields_ = [("samples", ctypes.c_uint64), ("segments", ctypes.c_uint64), ("escaped", ctypes.c_uint64)]
+
+
+def _load4() -> ctypes.CDLL:
+    L = load()
+    if not getattr(L, "_v4", False):
+        L.pto4_default_scene.argtypes = [ctypes.POINTER(Scene4)]
+        L.pto4_render.argtypes = [ctypes.c_void_p, ctypes.POINTER(Params4), ctypes.POINTER(Scene4),
+                                  ctypes.POINTER(Counts4)]
+        L.pto4_render.restype = ctypes.c_int
+        L.pto4_scene_tables.argtypes = [ctypes.POINTER(Scene4), ctypes.c_void_p, ctypes.c_int32]
+        L.pto4_scene_tables.restype = ctypes.c_int
+        L.pto4_randomf.argtypes = [ctypes.POINTER(ctypes.c_uint32)]
+        L.pto4_randomf.restype = ctypes.c_float
+        L.pto4_random_unit_vector.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
+                                              ctypes.POINTER(ctypes.c_float)]
+        L.pto4_env_sample.argtypes = [ctypes.POINTER(Env), ctypes.c_int32, ctypes.c_int32,
+                                      ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_uint32),
+                                      ctypes.POINTER(ctypes.c_float)]
+        L._v4 = True
+    return L
+
+
+def default_scene4() -> Scene4:
+    s = Scene4()
+    _load4().pto4_default_scene(ctypes.byref(s))
+    return s
+
+
+def render4(width: int, height: int, *, frame_first: int = 1, nframes: int = 1, num_bounces: int = 8,
+            row_start: int = 0, row_stride: int = 1, nrows: int | None = None, env_mode: int = ENV_EQUIRECT,
+            env: np.ndarray | None = None, random_jitter: bool = True, rejection: bool = True,
+            scene: Scene4 | None = None, nthreads: int | None = None, buf: np.ndarray | None = None,
+            counts: bool = False):
+    """v4 renderer (DemofoxRenderOptV4): accumulate frames [frame_first, +nframes) into buf
+    (nrows x width x 3, interleaved).  env None => ambient (USE_ENV_MAP 0).  counts=True returns
+    (buf, {samples, segments, escaped}) and renders single-threaded."""
+    nrows = height if nrows is None else nrows
+    if buf is None:
+        buf = np.zeros((nrows, width, 3), np.float32)
+    assert buf.dtype == np.float32 and buf.flags["C_CONTIGUOUS"] and buf.size >= nrows * width * 3
+    nthreads = nthreads if nthreads is not None else min(os.cpu_count() or 1, 16)
+    p = Params4(width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces,
+                env_mode if env is not None else ENV_NONE, int(random_jitter), int(rejection), None, nthreads)
+    keep = None
+    if env is not None:
+        env = np.ascontiguousarray(env, dtype=np.float32)
+        keep = (env, Env(env.ctypes.data, env.shape[1], env.shape[0]))
+        p.env = ctypes.pointer(keep[1])
+    c = Counts4()
+    rc = _load4().pto4_render(buf.ctypes.data, ctypes.byref(p), ctypes.byref(scene) if scene is not None else None,
+                              ctypes.byref(c) if counts else None)
+    del keep
+    if rc:
+        raise ValueError("pto4_render rejected the parameters")
+    if counts:
+        return buf, {k: int(getattr(c, k)) for k, _ in Counts4._fields_}
+    return buf
+
+
+def scene4_tables(scene: Scene4 | None = None) -> np.ndarray:
+    out = np.zeros(18 * MAX_OBJECTS + 17 * MAX_OBJECTS, np.float32)
+    n = _load4().pto4_scene_tables(ctypes.byref(scene) if scene is not None else None, out.ctypes.data, out.size)
+    if n < 0:
+        raise ValueError("invalid scene")
+    return out[:n]
+
+
+def env_sample4(env: np.ndarray | None, env_mode: int, random_jitter: bool, dirs: np.ndarray, seed_value: int = 1):
+    """Per-direction env lookups (v4 :769-784), one RNG state threaded through all of them."""
+    keep = None
+    ep = None
+    if env is not None:
+        env = np.ascontiguousarray(env, dtype=np.float32)
+        keep = (env, Env(env.ctypes.data, env.shape[1], env.shape[0]))
+        ep = ctypes.pointer(keep[1])
+    s = ctypes.c_uint32(seed_value)
+    d = np.ascontiguousarray(dirs, dtype=np.float32).reshape(-1, 3)
+    out = np.zeros_like(d)
+    o = (ctypes.c_float * 3)()
+    for i in range(d.shape[0]):
+        v = (ctypes.c_float * 3)(*d[i])
+        _load4().pto4_env_sample(ep, env_mode, int(random_jitter), v, ctypes.byref(s), o)
+        out[i] = list(o)
+    del keep
+    return out
