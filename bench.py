@@ -57,6 +57,8 @@ def cpu_baseline(wl, seconds: float, env=None) -> dict:
     except AttributeError:
         ncpu = os.cpu_count() or 1
     cores = max(1, min(16, ncpu))
+    if wl.renderer == "v4":
+        return cpu_baseline_v4(wl, seconds, env, cores, ncpu)
     kw = dict(num_bounces=wl.num_bounces, nthreads=cores, env=env)
     t0 = time.perf_counter()
     pyoracle.render(wl.width, wl.height, frame_first=1, nframes=1, **kw)      # calibration frame
@@ -92,6 +94,25 @@ def cpu_baseline(wl, seconds: float, env=None) -> dict:
                                    f"c_numBounces), DemofoxRenderScalar built unmodified by oracle/build_ref.sh; "
                                    f"{dt:.2f} s wall"}
     return out
+
+
+def cpu_baseline_v4(wl, seconds: float, env, cores: int, ncpu: int) -> dict:
+    """The v4 oracle (oracle/pt_oracle_v4.c, the restatement the kernel matches bit for bit) on
+    this host's cores, whole frames of the workload for about `seconds`."""
+    from oracle import pyoracle
+    kw = dict(num_bounces=wl.num_bounces, nthreads=cores, env=env)
+    t0 = time.perf_counter()
+    pyoracle.render4(wl.width, wl.height, frame_first=1, nframes=1, **kw)
+    t1 = time.perf_counter() - t0
+    frames = int(max(1, min(1024, round(seconds / max(t1, 1e-6)))))
+    t0 = time.perf_counter()
+    pyoracle.render4(wl.width, wl.height, frame_first=2, nframes=frames, **kw)
+    dt = time.perf_counter() - t0
+    samples = wl.width * wl.height * frames
+    return {"value": samples * wl.num_bounces / dt, "unit": "ray-samples/s", "cores": cores, "kind": "port",
+            "sample": f"{wl.width}x{wl.height}, {frames} frames (spp), {wl.num_bounces} bounces, v4 default scene + "
+                      f"env map, oracle/pt_oracle_v4.c (gcc -O2, {cores} threads, row-cyclic); {dt:.2f} s wall",
+            "primary_samples_per_s": samples / dt, "host_cpus_visible": ncpu, "cpu_model": _cpu_model()}
 
 
 def _cpu_model() -> str:
@@ -148,7 +169,8 @@ def main() -> None:
 
     from cpuperformanceraytracer_amd import roofline as RL
     from cpuperformanceraytracer_amd.config import CONFIGS, synthetic_env
-    from cpuperformanceraytracer_amd.device import count_device, ensure_backend, render_device, set_env_map
+    from cpuperformanceraytracer_amd.device import (count_device, count_v4_device, ensure_backend, render_device,
+                                                    render_v4_device, set_env_map)
     from cpuperformanceraytracer_amd.shard import gather_rows, max_rows, rows_of
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -171,14 +193,19 @@ def main() -> None:
     env = synthetic_env() if wl.env else None
     if env is not None:
         set_env_map(env, dev.index, B)
+    v4 = wl.renderer == "v4"
+    if v4:
+        from cpuperformanceraytracer_amd.renderer import v4_config
+        v4_config(num_bounces=B)   # the reference's default flags (equirect, random jitter, rejection)
+    render_fn, count_fn = (render_v4_device, count_v4_device) if v4 else (render_device, count_device)
 
     buf = torch.zeros(mr * W * 3, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     frame = 1
 
     def step(f):
-        render_device(buf, W, Hg, frame_first=f, nframes=S, num_bounces=B, row_start=row_start,
-                      row_stride=row_stride, nrows=nrows, use_env=wl.env, stream=stream)
+        render_fn(buf, W, Hg, frame_first=f, nframes=S, num_bounces=B, row_start=row_start,
+                  row_stride=row_stride, nrows=nrows, use_env=wl.env, stream=stream)
 
     for _ in range(args.warmup):
         step(frame)
@@ -221,13 +248,13 @@ def main() -> None:
     scratch = torch.zeros_like(buf)
     segs = samples = slots = prim = escaped = 0
     for k in range(K):
-        c = count_device(scratch, W, Hg, frame_first=timed_first + k * S, nframes=S, num_bounces=B,
-                         row_start=row_start, row_stride=row_stride, nrows=nrows, use_env=wl.env, stream=stream)
+        c = count_fn(scratch, W, Hg, frame_first=timed_first + k * S, nframes=S, num_bounces=B,
+                     row_start=row_start, row_stride=row_stride, nrows=nrows, use_env=wl.env, stream=stream)
         escaped += c["escaped"]
         segs += c["segments"]
         samples += c["samples"]
         slots += c["lane_slots"]
-        prim += c["primary"]
+        prim += c.get("primary", c["samples"])
     del scratch
 
     output_stage = measure_output_stage(buf, W, H, stream) if rank == 0 else None
@@ -240,8 +267,17 @@ def main() -> None:
     total_ray_samples = W * H * S * B * K * world
     value = total_ray_samples / elapsed
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-    flops_launch = RL.launch_flops_exec(segs, prim, samples) / K
-    flops_launch_ref = RL.launch_flops_ref(segs, prim, samples) / K
+    if v4:   # every frame traces its own jittered camera ray: executed == reference work
+        flops_launch = flops_launch_ref = RL.v4_launch_flops(segs, samples) / K
+        flop_model = (f"segments x V4_F_SEGMENT + samples x V4_F_SAMPLE; F = {RL.V4_F_SEGMENT}/{RL.V4_F_SAMPLE} "
+                      "(roofline.py, counted by oracle/pt_oracle_v4.c)")
+        kernel_name = "pt_v4_kernel<EQUIRECT, INTERLEAVED>"
+    else:
+        flops_launch = RL.launch_flops_exec(segs, prim, samples) / K
+        flops_launch_ref = RL.launch_flops_ref(segs, prim, samples) / K
+        flop_model = ("executed = (segments_ref x F_SEGMENT + samples x F_SAMPLE) - (samples - pixels) x "
+                      f"F_SHARED; F = {RL.F_SEGMENT}/{RL.F_SAMPLE}/{RL.F_SHARED} (roofline.py)")
+        kernel_name = "pt_render_env_kernel<INTERLEAVED>" if wl.env else "pt_render_kernel<INTERLEAVED>"
     achieved_tf = flops_launch / avg_kernel_s / 1e12
     hbm_launch, traffic_src = load_traffic(wl.name)
     # config 4: one 12-byte texel gather per escaping path
@@ -258,7 +294,8 @@ def main() -> None:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (the reference's fixed demofox quad+sphere scene; no dataset)" + (
+        "data": ("synthetic (the reference's v4 InitializeScene: 4 quads + 7 glass spheres; no dataset)" if v4 else
+                 "synthetic (the reference's fixed demofox quad+sphere scene; no dataset)") + (
             "; env map: 2048x1024 log-normal f32, seed 0xC0FFEE, standing in for the missing chinese_garden_2k.hdr"
             if wl.env else ""),
         "config": {"workload": wl.name, "width": W, "height": H, "spp": S, "bounces": B,
@@ -268,7 +305,7 @@ def main() -> None:
         "ms_per_frame_1spp": ms_step / S,
         "traced_segments_per_s": segs * world / (avg_kernel_s * K),
         "segments_per_sample": segs / samples,
-        "ref_segments_per_sample": RL.ref_segments(segs, prim, samples) / samples,
+        "ref_segments_per_sample": (segs if v4 else RL.ref_segments(segs, prim, samples)) / samples,
         "simd_lane_efficiency": segs / slots if slots else None,
         "kernel_ms_avg": avg_kernel_s * 1e3,
         "kernel_ms_min": min(kernel_ms),
@@ -279,10 +316,9 @@ def main() -> None:
             "unit": "TFLOP/s",
             "frac": achieved_tf / RL.PEAK_FP32_TFLOPS,
             "traffic": hbm_launch,
-            "kernel": "pt_render_env_kernel<INTERLEAVED>" if wl.env else "pt_render_kernel<INTERLEAVED>",
+            "kernel": kernel_name,
             "flops_per_launch": flops_launch,
-            "flop_model": "executed = (segments_ref x F_SEGMENT + samples x F_SAMPLE) - (samples - pixels) x "
-                          f"F_SHARED; F = {RL.F_SEGMENT}/{RL.F_SAMPLE}/{RL.F_SHARED} (roofline.py)",
+            "flop_model": flop_model,
             "flops_per_launch_ref_equivalent": flops_launch_ref,
             "achieved_ref_equivalent": flops_launch_ref / avg_kernel_s / 1e12,
             "algorithmic_bytes_per_launch": RL.BYTES_PER_PIXEL_PER_LAUNCH * W * H + env_bytes,

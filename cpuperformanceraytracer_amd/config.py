@@ -38,6 +38,7 @@ class Workload:
     spp: int
     num_bounces: int
     env: bool = False   # miss radiance = env-map sample (config 4) instead of the ambient
+    renderer: str = "scalar"   # "scalar": the diffuse+emissive path (configs 1-5); "v4": optimization_v4
 
     @property
     def primary_samples(self) -> int:
@@ -55,6 +56,9 @@ CONFIGS = {
     "c3_4k": Workload("c3_4k", 3840, 2160, 64, 8),               # configs[2]
     "c4_env_1080p": Workload("c4_env_1080p", 1920, 1080, 16, 8, env=True),  # configs[3] (env map)
     "c5_8k": Workload("c5_8k", 7680, 4320, 256, 8),              # configs[4] (8 GPUs)
+    # the shipping v4 renderer (Application.cpp:474) at the headline size, its
+    # default flags (equirect env map, random-jitter texel sampling, rejection-sampled directions)
+    "v4_1080p": Workload("v4_1080p", 1920, 1080, 8, 8, env=True, renderer="v4"),
 }
 
 

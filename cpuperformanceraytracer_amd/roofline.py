@@ -56,3 +56,18 @@ def launch_flops_ref(traced: int, camera_rays: int, samples: int) -> float:
 
 def launch_flops_exec(traced: int, camera_rays: int, samples: int) -> float:
     return launch_flops_ref(traced, camera_rays, samples) - (samples - camera_rays) * F_SHARED
+
+
+# ---- v4 renderer (demofox_path_tracing_optimization_v4.cpp) ------------------------------------
+# Mean executed f32 FLOP per traced segment (TestSceneTrace over 4 quads + 7 spheres, then either
+# the env miss term or the material shading), counted by the instrumented oracle
+# (oracle/pt_oracle_v4.c, per-function totals documented there) over 1920x1080, 8 bounces,
+# default scene + 2k synthetic env, rows 0::8 / 3::8, frames 1-2: 496.01 / 495.84.  Every frame
+# traces its own jittered camera ray, so executed == reference work (nothing is shared).
+V4_F_SEGMENT = 495.9
+# Per sample: camera ray 23 + c_numRendersPerFrame scale 6 + fused accumulate 9 (exact).
+V4_F_SAMPLE = 38.0
+
+
+def v4_launch_flops(segments: int, samples: int) -> float:
+    return segments * V4_F_SEGMENT + samples * V4_F_SAMPLE

@@ -114,6 +114,8 @@ typedef struct pto4_params {
 
 typedef struct pto4_counts {
     uint64_t samples, segments, escaped;
+    uint64_t flops;             /* executed f32 FLOP (convention in pt_oracle_v4.c)          */
+    uint64_t transcendentals;   /* atan2f/asinf/sinf/cosf calls                              */
 } pto4_counts;
 
 void pto4_default_scene(pto4_scene* s);   /* InitializeScene, v4 :1403-1496 */

@@ -392,13 +392,21 @@ static inline int sphere_trace(v3 pos, v3 dir, hit4* h, const float* sp)   /* Te
     return check;
 }
 
-static inline void scene_trace(const s4* s, v3 pos, v3 dir, hit4* h)   /* TestSceneTrace :700-718 */
+static inline uint64_t scene_trace(const s4* s, v3 pos, v3 dir, hit4* h)   /* TestSceneTrace :700-718 */
 {
     int obj = 0;
+    uint64_t flops = 53u * (uint64_t)s->nq + 25u * (uint64_t)s->ns;
     for (int i = 0; i < s->nq; ++i, ++obj)
-        if (quad_trace(pos, dir, h, &s->quad[i])) h->mat = obj;
+        if (quad_trace(pos, dir, h, &s->quad[i])) {
+            h->mat = obj;
+            flops += 6;
+        }
     for (int i = 0; i < s->ns; ++i, ++obj)
-        if (sphere_trace(pos, dir, h, s->sph[i])) h->mat = obj;
+        if (sphere_trace(pos, dir, h, s->sph[i])) {
+            h->mat = obj;
+            flops += 19;
+        }
+    return flops;
 }
 
 static inline float fresnel(float n1, float n2, v3 normal, v3 incident, float f0, float f90)   /* :429-453 */
@@ -442,6 +450,21 @@ typedef struct {
     pto4_counts* cnt;
 } ctx4;
 
+/* FLOP accounting (SURVEY.md §8d convention: 1 per f32 add/sub/mul/div/sqrt/compare/min/max the
+ * reference executes, an fmadd/fmsub/fnmadd = 2, negation/abs/select/floor/conversions 0; scene-
+ * and frame-constant work (PrecomputeQuadData, rcp of the resolution, 1/(iFrame+1)) excluded;
+ * atan2/asin/sin/cos counted as transcendentals).  Per-function totals, counted by hand from the
+ * code above and below:
+ *   TestQuadTrace   53 (+6 on a hit: the facing dot + compare)            v4 :556-637
+ *   TestSphereTrace 25 (+19 on a hit: hit point, normalize, sign)        v4 :641-695
+ *   miss            6 (throughput-weighted ambient) + env lookup: equirect 10 + 2T, cubemap 23
+ *                   (bilinear 22), then the texel sampler: random 8, bilinear 39
+ *   hit shading     absorption 24 (inside only); last bounce 6 (emissive); otherwise 199
+ *                   (Fresnel 31, chances 15, nudge 13, diffuse 29, specular 22, refraction 63,
+ *                   normalize 10, emissive + throughput + roulette 16..20 (+4 on a boost))
+ *   per sample      camera 23, c_numRendersPerFrame scale 6, accumulate 9 = 38 */
+#define CNT(c, n) do { if ((c)->cnt) (c)->cnt->flops += (uint64_t)(n); } while (0)
+
 /* GetColorForRay, v4 :722-911 (USE_FAST_APPROXIMATE_EXP = 1) */
 static v3 color_for_ray(const ctx4* c, v3 pos, v3 dir, uint32_t* rng)
 {
@@ -450,7 +473,7 @@ static v3 color_for_ray(const ctx4* c, v3 pos, v3 dir, uint32_t* rng)
     v3 ret = mk(0.0f, 0.0f, 0.0f), T = mk(1.0f, 1.0f, 1.0f);
     for (int bounce = 0; bounce <= p->num_bounces; ++bounce) {
         hit4 h = {0, V4_SUPER_FAR, {0.0f, 0.0f, 0.0f}, 0};
-        scene_trace(s, pos, dir, &h);
+        CNT(c, scene_trace(s, pos, dir, &h));
         if (c->cnt) c->cnt->segments++;
         const int miss = h.dist == V4_SUPER_FAR;
         /* the ambient / env term is evaluated every iteration (:769-784): its RNG draws happen on
@@ -460,18 +483,31 @@ static v3 color_for_ray(const ctx4* c, v3 pos, v3 dir, uint32_t* rng)
         pto4_env_sample(p->env, p->env ? p->env_mode : PTO4_ENV_NONE, p->random_jitter, dv, rng, amb);
         if (miss) {
             ret = mk(fmaf(amb[0], T.x, ret.x), fmaf(amb[1], T.y, ret.y), fmaf(amb[2], T.z, ret.z));   /* :787 */
-            if (c->cnt) c->cnt->escaped++;
+            if (c->cnt) {
+                c->cnt->escaped++;
+                const int mode = p->env ? p->env_mode : PTO4_ENV_NONE;
+                uint64_t f = 6;
+                if (mode == PTO4_ENV_EQUIRECT) f += 10, c->cnt->transcendentals += 2;
+                if (mode == PTO4_ENV_CUBEMAP) f += p->random_jitter ? 23 : 22;
+                if (mode != PTO4_ENV_NONE) f += p->random_jitter ? 8 : 39;
+                c->cnt->flops += f;
+            }
             break;
         }
         const m4* M = &s->mat[h.mat];   /* GatherMaterials :389-427 */
         const v3 rc = mk(M->refr_color[0], M->refr_color[1], M->refr_color[2]);
-        if (h.from_inside)   /* :797 (Beer's law, approx_exp) */
+        if (h.from_inside) {   /* :797 (Beer's law, approx_exp) */
             T = mul3(T, mk(approx_exp(-rc.x * h.dist), approx_exp(-rc.y * h.dist), approx_exp(-rc.z * h.dist)));
+            CNT(c, 24);
+        }
 
         if (bounce == p->num_bounces) {   /* last iteration: only the emissive term below is used */
             ret = mk(fmaf(M->emissive[0], T.x, ret.x), fmaf(M->emissive[1], T.y, ret.y), fmaf(M->emissive[2], T.z, ret.z));
+            CNT(c, 6);
             break;
         }
+        CNT(c, 199);
+        if (c->cnt && !p->rejection) c->cnt->transcendentals += 4;
         float spec = M->spec_chance, refr = M->refr_chance;
         {   /* :807-829 */
             const int has_spec = spec > 0.0f;
@@ -532,7 +568,10 @@ static v3 color_for_ray(const ctx4* c, v3 pos, v3 dir, uint32_t* rng)
         {   /* :891-899 */
             const float pm = max_ps(T.x, max_ps(T.y, T.z));
             const int term = randf(rng) > pm;
-            if (!term) T = muls(T, rcpf_(pm));
+            if (!term) {
+                T = muls(T, rcpf_(pm));
+                CNT(c, 4);
+            }
         }
         pos = npos;
         dir = ndir;
@@ -556,6 +595,7 @@ static v3 main_image(const ctx4* c, int32_t X, int32_t Y, uint32_t frame)
     const float cam_dist = 1.0f / tanf(90.0f * 0.5f * V4_PI / 180.0f);   /* InitializeCamera :1500 */
     const v3 dir = normalize3(sub3(mk(tx, ty, -cam_dist), mk(0.0f, 0.0f, 0.0f)));
     if (c->cnt) c->cnt->samples++;
+    CNT(c, 38);
     const v3 col = color_for_ray(c, mk(0.0f, 0.0f, 1.0f * 40.0f), dir, &rng);
     return mk(fmaf(col.x, 1.0f, 0.0f), fmaf(col.y, 1.0f, 0.0f), fmaf(col.z, 1.0f, 0.0f));   /* :1127 */
 }

@@ -188,7 +188,8 @@ class Params4(ctypes.Structure):
 
 
 class Counts4(ctypes.Structure):
-    _fields_ = [("samples", ctypes.c_uint64), ("segments", ctypes.c_uint64), ("escaped", ctypes.c_uint64)]
+    _fields_ = [("samples", ctypes.c_uint64), ("segments", ctypes.c_uint64), ("escaped", ctypes.c_uint64),
+                ("flops", ctypes.c_uint64), ("transcendentals", ctypes.c_uint64)]
 
 
 def _load4() -> ctypes.CDLL:

@@ -33,3 +33,14 @@ def test_counted_render_equals_plain_render():
     img, _ = pyoracle.render_counted(64, 48, nframes=2, num_bounces=8)
     ref = pyoracle.render(64, 48, nframes=2, num_bounces=8)
     assert (img.view("u4") == ref.view("u4")).all()
+
+
+@pytest.mark.parametrize("rs", [0, 3])
+def test_v4_flop_constants(rs):
+    """v4 renderer: V4_F_SAMPLE exact, V4_F_SEGMENT within 0.5 % (default scene, 2k synthetic env)."""
+    from cpuperformanceraytracer_amd.config import synthetic_env
+    _, c = pyoracle.render4(1920, 1080, nframes=1, env=synthetic_env(), counts=True, row_start=rs, row_stride=16,
+                            nrows=67)
+    f_seg = (c["flops"] - RL.V4_F_SAMPLE * c["samples"]) / c["segments"]
+    assert abs(f_seg - RL.V4_F_SEGMENT) / RL.V4_F_SEGMENT < 0.005, f_seg
+    assert RL.v4_launch_flops(c["segments"], c["samples"]) == pytest.approx(c["flops"], rel=0.005)
