@@ -37,7 +37,7 @@ EXPORTED_SYMBOLS = (
     "pt_tonemap", "pt_tonemap_device", "pt_write_bmp", "pt_load_cubemap_texture",
     "pt_v4_default_config", "pt_v4_set_config", "pt_v4_initialize_global_render_resources",
     "pt_v4_reinitialize_render_tile_data", "pt_v4_initialize_scene", "pt_v4_clear_scene", "pt_v4_add_material",
-    "pt_v4_add_quad", "pt_v4_add_sphere", "pt_v4_set_frame", "pt_v4_get_frame", "pt_render_opt_v4",
+    "pt_v4_add_quad", "pt_v4_add_sphere", "pt_v4_set_frame", "pt_v4_get_frame", "pt_v4_get_scene_tables", "pt_render_opt_v4",
     "pt_copy_output_to_file", "pt_v4_render_device", "pt_v4_count_device",
 )
 
@@ -160,6 +160,7 @@ def load() -> ctypes.CDLL:
         "pt_v4_add_sphere": (i32, [ctypes.POINTER(ctypes.c_float)]),
         "pt_v4_set_frame": (i32, [u32]),
         "pt_v4_get_frame": (u32, []),
+        "pt_v4_get_scene_tables": (i32, [vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "pt_render_opt_v4": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, ctypes.POINTER(PtTexture), vp]),
         "pt_copy_output_to_file": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp]),
         "pt_v4_render_device": (i32, [ctypes.POINTER(PtDeviceJob), vp]),

@@ -470,6 +470,7 @@ PtV4Job v4_job(float* buf, int32_t w, int32_t h)
     j.env_mode = PT_V4_ENV_NONE;
     j.random_jitter = g.v4cfg.random_jitter;
     j.rejection = g.v4cfg.rejection;
+    j.default_scene = pt_v4_is_default_geometry(g.v4scene) ? 1 : 0;
     return j;
 }
 
@@ -923,6 +924,28 @@ int pt_v4_set_frame(uint32_t frame)
 }
 
 uint32_t pt_v4_get_frame(void) { return g.v4_frame; }
+
+int pt_v4_get_scene_tables(float* out, int32_t n, int32_t* nq, int32_t* ns)
+{
+    int rc;
+    if ((rc = v4_ensure_scene())) return rc;
+    const PtV4Scene& s = g.v4scene;
+    const int32_t need = 18 * s.nquads + 4 * s.nspheres + 17 * PT_V4_MAX_OBJECTS;
+    if (nq) *nq = s.nquads;
+    if (ns) *ns = s.nspheres;
+    if (!out || n < need) return need;
+    float* o = out;
+    for (int i = 0; i < s.nquads; ++i) {
+        memcpy(o, &s.quad[i], sizeof(PtV4Quad));
+        o += 18;
+    }
+    for (int i = 0; i < s.nspheres; ++i) {
+        memcpy(o, s.sph[i], 4 * sizeof(float));
+        o += 4;
+    }
+    memcpy(o, s.mat, sizeof(s.mat));
+    return need;
+}
 
 int pt_render_opt_v4(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty, int32_t tw, int32_t th, int32_t nc,
                      const pt_texture* tex, void* screen)

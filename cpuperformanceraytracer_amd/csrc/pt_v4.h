@@ -52,6 +52,7 @@ struct PtV4Job {
     const float* env;           // device texture (H x W x 3), nullptr with PT_V4_ENV_NONE_
     int32_t env_w, env_h;
     unsigned long long* counters;   // COUNT launches: [0] segments, [1] samples, [2] escaped, [3] lane slots
+    int32_t default_scene;          // the scene is InitializeScene's: literal-geometry instantiation
 };
 
 // Scene description in AddQuad/Sphere/MaterialToScene order (v4 :1368-1401).
@@ -64,4 +65,5 @@ struct PtV4SceneDesc {
 
 void pt_v4_default_scene_desc(PtV4SceneDesc* d);                   // InitializeScene, v4 :1403-1496
 int pt_v4_build_scene(const PtV4SceneDesc* d, PtV4Scene* out);     // PrecomputeQuadData + AddMaterialToScene
+bool pt_v4_is_default_geometry(const PtV4Scene& s);                // geometry == pt_v4_default_scene.h
 hipError_t pt_launch_v4(const PtV4Job& job, const PtV4Scene& scene, hipStream_t stream, bool count);

@@ -20,8 +20,13 @@
 #include "pt_v4.h"
 #include "pt_kernel.h"
 #include "pt_exactmath.h"
-#include "pt_invtrig.h"
 #include "pt_sincosf.h"
+// atan2f/asinf with the guarded fast '/' and sqrt (bit-identical to IEEE, pt_exactmath.h)
+#define PT_IT_HD __device__ __forceinline__
+#define PT_IT_DIV(a, b) pt::div_guarded((a), (b))
+#define PT_IT_SQRT(x) pt::sqrt_guarded(x)
+#include "pt_invtrig.h"
+#include "pt_v4_default_scene.h"
 #include <algorithm>
 
 namespace {
@@ -52,9 +57,21 @@ __device__ __forceinline__ V3 ld3(const float* p) { return v3(p[0], p[1], p[2]);
 __device__ __forceinline__ float max_ps(float a, float b) { return a > b ? a : b; }   // MAXPS: b on NaN
 __device__ __forceinline__ float min_ps(float a, float b) { return a < b ? a : b; }
 __device__ __forceinline__ float saturate(float x) { return min_ps(max_ps(x, 0.0f), 1.0f); }
-__device__ __forceinline__ float rcp(float x) { return 1.0f / x; }                      // mathlib.h:415
-__device__ __forceinline__ float sqrt_(float x) { return __builtin_sqrtf(x); }
-__device__ __forceinline__ V3 normalize(V3 v) { return v * (1.0f / sqrt_(dot(v, v))); }  // mathlib.h:759
+// correctly rounded 1/x and sqrt: the fast sequences of pt_exactmath.h inside their verified
+// ranges, IEEE outside (bit-identical to '1.0f / x' and sqrtf for every input)
+#ifndef PT_V4_IEEE_DIV
+#define PT_V4_IEEE_DIV 0   // A/B / debug builds: the compiler's IEEE sequences
+#endif
+__device__ __forceinline__ float rcp(float x)   // rcp -> 1.f / x (mathlib.h:415)
+{
+    if (PT_V4_IEEE_DIV) return 1.0f / x;
+    float r = pt::rcp_rn(x);
+    const float ax = __builtin_fabsf(x);
+    if (__builtin_expect(!(ax >= 0x1p-125f && ax <= 0x1p125f), 0)) r = 1.0f / x;
+    return r;
+}
+__device__ __forceinline__ float sqrt_(float x) { return PT_V4_IEEE_DIV ? __builtin_sqrtf(x) : pt::sqrt_guarded(x); }
+__device__ __forceinline__ V3 normalize(V3 v) { return v * rcp(sqrt_(dot(v, v))); }  // mathlib.h:759
 
 __device__ __forceinline__ uint32_t wang(uint32_t& s)   // mathutils.h:8-16 (logical shifts)
 {
@@ -67,6 +84,10 @@ __device__ __forceinline__ uint32_t wang(uint32_t& s)   // mathutils.h:8-16 (log
     s = x;
     return x;
 }
+__device__ __forceinline__ void rng_skip(uint32_t& s, int n)   // draws whose values are not used
+{
+    for (int i = 0; i < n; ++i) wang(s);
+}
 // Randomf3201_ps (mathutils.h:18-26): cvtepi32_ps(h & 0x7FFFFFFF) / 2^31 (an exact scaling)
 __device__ __forceinline__ float randf(uint32_t& s) { return (float)(int32_t)(wang(s) & 0x7FFFFFFFu) * 0x1p-31f; }
 
@@ -76,7 +97,7 @@ __device__ __forceinline__ V3 ruv_rejection(uint32_t& s)   // v4 :109-130
     const float v = fma_(2.0f, randf(s), -1.0f);
     const float w = fma_(2.0f, randf(s), -1.0f);
     const float d2 = fma_(w, w, fma_(u, u, v * v));
-    return v3(u, v, w) * (1.0f / sqrt_(d2));   // rsroot -> 1/sqrtf (mathlib.h:437)
+    return v3(u, v, w) * rcp(sqrt_(d2));   // rsroot -> 1/sqrtf (mathlib.h:437)
 }
 
 __device__ __forceinline__ V3 ruv_angle(uint32_t& s)   // mathutils.h:33-46 (sincos -> glibc sinf/cosf)
@@ -200,8 +221,8 @@ __device__ __forceinline__ V3 cubemap(const Tex& t, V3 d, bool random, uint32_t&
         v = saturate(fma_(v, 0.166666666666667f, voff));
         return sample_random(t, u, v, s);
     }
-    const float u = saturate((fu / m) * 0.5f + 0.5f);
-    float v = saturate((fv / m) * 0.5f + 0.5f);
+    const float u = saturate(pt::div_guarded(fu, m) * 0.5f + 0.5f);
+    float v = saturate(pt::div_guarded(fv, m) * 0.5f + 0.5f);
     v = saturate(fma_(v, 1.0f / 6.0f, voff));
     return sample_bilinear(t, u, v);
 }
@@ -249,46 +270,104 @@ struct Hit {
     int mat;
 };
 
-// TestSceneTrace :700-718 with TestQuadTrace :556-637 / TestSphereTrace :641-695
-__device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir)
+// TestQuadTrace :556-637 for one quad (the reference's operations; `dk` evaluates its fused dots)
+template <class DOT>
+__device__ __forceinline__ void quad_test(V3 pos, V3 dir, Hit& h, int obj, V3 v0, V3 n, const DOT& dk, int q)
 {
-    Hit h{kSuperFar, v3(0.0f, 0.0f, 0.0f), false, 0};
-    int obj = 0;
-    for (int i = 0; i < sc.nquads; ++i, ++obj) {
-        const PtV4Quad& q = sc.quad[i];
-        const V3 n = ld3(q.n);
-        const V3 off = ld3(q.v0) - pos;
-        const float rdn = dot(dir, n);
-        const float dist = dot(off, n) * rcp(rdn);
+    const V3 off = v0 - pos;
+    const float rdn = dk(dir, q, 1);   // dot(dir, normal)
+    const float dist = dk(off, q, 1) * rcp(rdn);
+    // the hit needs (tri1 || tri2) && 0.01 < dist < best: the barycentric tests only run for
+    // distances in range (a wave whose lanes all fail skips them)
+    if (dist > kMinHit && dist < h.dist) {
         const V3 hp = v3(fma_(dist, dir.x, -off.x), fma_(dist, dir.y, -off.y), fma_(dist, dir.z, -off.z));
-        const float A0 = dot(hp, ld3(q.a0)), A1 = dot(hp, ld3(q.a1)), A2 = 1.0f - A0 - A1;
-        const float B0 = dot(hp, ld3(q.b0)), B1 = dot(hp, ld3(q.b1)), B2 = 1.0f - B0 - B1;
+        const float A0 = dk(hp, q, 2), A1 = dk(hp, q, 3), A2 = 1.0f - A0 - A1;
+        const float B0 = dk(hp, q, 4), B1 = dk(hp, q, 5), B2 = 1.0f - B0 - B1;
         const bool tri1 = A0 >= 0.0f && A1 >= 0.0f && A2 >= 0.0f;
         const bool tri2 = B0 >= 0.0f && B1 >= 0.0f && B2 >= 0.0f;
-        if ((tri1 || tri2) && dist > kMinHit && dist < h.dist) {
+        if (tri1 || tri2) {
             h.inside = false;
             h.dist = dist;
             if (rdn > 0.0f) h.n = neg(n);   // only back-side hits write the normal (:630)
             h.mat = obj;
         }
     }
-    for (int i = 0; i < sc.nspheres; ++i, ++obj) {
-        const V3 m = pos - ld3(sc.sph[i]);
-        const float r = sc.sph[i][3];
-        const float b = dot(m, dir);
-        const float c = fma_(-r, r, dot(m, m));
-        const float discr = fma_(b, b, -c);
-        const bool early = discr < 0.0f || (c > 0.0f && b > 0.0f);
+}
+
+// TestSphereTrace :641-695
+__device__ __forceinline__ void sphere_test(V3 pos, V3 dir, Hit& h, int obj, V3 c, float r)
+{
+    const V3 m = pos - c;
+    const float b = dot(m, dir);
+    const float cc = fma_(-r, r, dot(m, m));
+    const float discr = fma_(b, b, -cc);
+    const bool early = discr < 0.0f || (cc > 0.0f && b > 0.0f);
+    if (!early) {   // the root and the distance only for candidates (most rays miss most spheres)
         const float s = sqrt_(discr);
         const bool inside = -b < s;
         const float dist = (inside ? s : -s) - b;
-        if (!early && dist > kMinHit && dist < h.dist) {
+        if (dist > kMinHit && dist < h.dist) {
             h.inside = inside;
             h.dist = dist;
             const V3 p = v3(fma_(dir.x, dist, m.x), fma_(dir.y, dist, m.y), fma_(dir.z, dist, m.z));
             h.n = normalize(p) * (inside ? -1.0f : 1.0f);
             h.mat = obj;
         }
+    }
+}
+
+// the reference's dot fma(x,x', fma(y,y', z*z')) against a COMPILE-TIME vector with its zero
+// components dropped.  Exact for every use in quad_test: dropping a term v*0 can only change the
+// sign of a zero result, or a NaN from inf*0; the dots feed `>= 0` / `> 0` tests and 1 - A0 - A1
+// (where +0 and -0 behave alike), and dist = ron * rcp(rdn), where a signed-zero rdn or ron gives
+// +-inf or +-0 and a non-finite hit point needs a non-finite dist -- all of which fail the
+// reference's 0.01 < dist < best test either way.
+__device__ __forceinline__ float dot_k(V3 v, float cx, float cy, float cz)
+{
+    if (cz != 0.0f) {
+        float t = v.z * cz;
+        if (cy != 0.0f) t = fma_(v.y, cy, t);
+        if (cx != 0.0f) t = fma_(v.x, cx, t);
+        return t;
+    }
+    if (cy != 0.0f) {
+        float t = v.y * cy;
+        if (cx != 0.0f) t = fma_(v.x, cx, t);
+        return t;
+    }
+    return cx != 0.0f ? v.x * cx : 0.0f;
+}
+
+// TestSceneTrace :700-718: quads in order, then spheres (object index = material index).
+// DEF: the reference's InitializeScene, geometry as instruction literals (pt_v4_default_scene.h,
+// generated from pt_v4_build_scene and checked by tests/test_oracle_v4.py); otherwise the scene
+// table of the kernel arguments (scalar loads per primitive).
+template <bool DEF>
+__device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir)
+{
+    Hit h{kSuperFar, v3(0.0f, 0.0f, 0.0f), false, 0};
+    if constexpr (DEF) {
+        namespace D = pt_v4_default;
+        const auto dk = [](V3 v, int q, int k) {
+            return dot_k(v, D::kQuad[q][3 * k], D::kQuad[q][3 * k + 1], D::kQuad[q][3 * k + 2]);
+        };
+#pragma unroll
+        for (int i = 0; i < D::kQuads; ++i)
+            quad_test(pos, dir, h, i, v3(D::kQuad[i][0], D::kQuad[i][1], D::kQuad[i][2]),
+                      v3(D::kQuad[i][3], D::kQuad[i][4], D::kQuad[i][5]), dk, i);
+#pragma unroll
+        for (int i = 0; i < D::kSpheres; ++i)
+            sphere_test(pos, dir, h, D::kQuads + i, v3(D::kSphere[i][0], D::kSphere[i][1], D::kSphere[i][2]),
+                        D::kSphere[i][3]);
+    } else {
+        int obj = 0;
+        for (int i = 0; i < sc.nquads; ++i, ++obj) {
+            const PtV4Quad& q = sc.quad[i];
+            const float* t = &q.v0[0];
+            const auto dk = [t](V3 v, int, int k) { return dot(v, ld3(t + 3 * k)); };
+            quad_test(pos, dir, h, obj, ld3(q.v0), ld3(q.n), dk, i);
+        }
+        for (int i = 0; i < sc.nspheres; ++i, ++obj) sphere_test(pos, dir, h, obj, ld3(sc.sph[i]), sc.sph[i][3]);
     }
     return h;
 }
@@ -304,7 +383,7 @@ __device__ __forceinline__ size_t out_index(const PtV4Job& j, int x, int r)   //
            ((size_t)ly * j.tile_w + (size_t)(lx & ~7)) * 3u + (size_t)(lx & 7);
 }
 
-template <int ENV, int LAYOUT, bool COUNT>
+template <int ENV, int LAYOUT, bool COUNT, bool DEF>
 __global__ __launch_bounds__(256) void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
 {
     __shared__ float s_col[kWaves][kChunk * 64 * 3];
@@ -382,7 +461,7 @@ __global__ __launch_bounds__(256) void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
             if (COUNT) n_slots += 64;
             if (item >= 0) {
                 // one iteration of GetColorForRay's bounce loop (:733-909)
-                const Hit h = trace(sc, pos, dir);
+                const Hit h = trace<DEF>(sc, pos, dir);
                 if (COUNT) ++n_seg;
                 const bool miss = h.dist == kSuperFar;
                 bool done = false;
@@ -408,16 +487,12 @@ __global__ __launch_bounds__(256) void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
                         done = true;
                     } else {
                         float spec = M.spec_chance, refr = M.refr_chance;
-                        {   // :807-829
-                            const bool has_spec = spec > 0.0f;
+                        if (spec > 0.0f) {   // :807-829 (the Fresnel result is used only with a specular chance)
                             const float n1 = h.inside ? M.ior : 1.0f, n2 = h.inside ? 1.0f : M.ior;
                             const float nspec = fresnel(n1, n2, h.n, dir, M.spec_chance);
                             const float rscc = rcp(1.0f - M.spec_chance);
-                            const float mult = fma_(-nspec, rscc, rscc);
-                            if (has_spec) {
-                                spec = nspec;
-                                refr = refr * mult;
-                            }
+                            spec = nspec;
+                            refr = refr * fma_(-nspec, rscc, rscc);
                         }
                         const float roll = randf(rng);   // :831
                         const bool do_spec = spec > 0.0f && roll < spec;
@@ -429,36 +504,49 @@ __global__ __launch_bounds__(256) void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
                         const V3 npos = v3(fma_(nudge, h.n.x, fma_(dir.x, h.dist, pos.x)),
                                            fma_(nudge, h.n.y, fma_(dir.y, h.dist, pos.y)),
                                            fma_(nudge, h.n.z, fma_(dir.z, h.dist, pos.z)));
+                        // :852-888.  The reference evaluates the diffuse, specular and refraction
+                        // directions and selects one; only the selected one (and the diffuse direction
+                        // the specular one lerps towards) is evaluated here.  Both random unit vectors
+                        // are still drawn, in the reference's order (diffuse first).
+                        const uint32_t s_diff = rng;
+                        rng_skip(rng, rejection ? 3 : 2);
+                        const uint32_t s_refr = rng;
+                        rng_skip(rng, rejection ? 3 : 2);
                         V3 ndir;
-                        {   // :852-888
+                        if (!do_refr) {
+                            uint32_t r = s_diff;
                             V3 diffuse;
                             if (rejection) {
-                                const V3 a = h.n + ruv_rejection(rng);
-                                diffuse = a * (1.0f / sqrt_(dot(a, a)));   // fast_approx_normalize, rsroot -> 1/sqrtf
+                                const V3 a = h.n + ruv_rejection(r);
+                                diffuse = a * rcp(sqrt_(dot(a, a)));   // fast_approx_normalize, rsroot -> 1/sqrtf
                             } else {
-                                diffuse = normalize(h.n + ruv_angle(rng));
+                                diffuse = normalize(h.n + ruv_angle(r));
                             }
-                            const float d2 = 2.0f * dot(dir, h.n);
-                            V3 sd = v3(fma_(-d2, h.n.x, dir.x), fma_(-d2, h.n.y, dir.y), fma_(-d2, h.n.z, dir.z));
-                            const float srsq = M.spec_rough * M.spec_rough;
-                            sd = v3(fma_(srsq, diffuse.x - sd.x, sd.x), fma_(srsq, diffuse.y - sd.y, sd.y),
-                                    fma_(srsq, diffuse.z - sd.z, sd.z));
+                            ndir = diffuse;
+                            if (do_spec) {
+                                const float d2 = 2.0f * dot(dir, h.n);
+                                const V3 sd = v3(fma_(-d2, h.n.x, dir.x), fma_(-d2, h.n.y, dir.y), fma_(-d2, h.n.z, dir.z));
+                                const float srsq = M.spec_rough * M.spec_rough;
+                                ndir = v3(fma_(srsq, diffuse.x - sd.x, sd.x), fma_(srsq, diffuse.y - sd.y, sd.y),
+                                          fma_(srsq, diffuse.z - sd.z, sd.z));
+                            }
+                        } else {
+                            uint32_t r = s_refr;
                             const float ior = h.inside ? M.ior : rcp(M.ior);
                             const float rrsq = M.refr_rough * M.refr_rough;
                             V3 rd = refract(dir, h.n, ior);
                             if (rejection) {
-                                const V3 a = ruv_rejection(rng) - h.n;
-                                const V3 nrd = a * (1.0f / sqrt_(dot(a, a)));
+                                const V3 a = ruv_rejection(r) - h.n;
+                                const V3 nrd = a * rcp(sqrt_(dot(a, a)));
                                 rd = v3(fma_(rrsq, nrd.x - rd.x, rd.x), fma_(rrsq, nrd.y - rd.y, rd.y),
                                         fma_(rrsq, nrd.z - rd.z, rd.z));
                             } else {
-                                const V3 nrd = normalize(ruv_angle(rng) - h.n);
+                                const V3 nrd = normalize(ruv_angle(r) - h.n);
                                 rd = normalize(rd + (nrd - rd) * rrsq);
                             }
-                            ndir = sel(do_spec, sd, diffuse);
-                            ndir = sel(do_refr, rd, ndir);
-                            ndir = normalize(ndir);
+                            ndir = rd;
                         }
+                        ndir = normalize(ndir);
                         ret = v3(fma_(em.x, T.x, ret.x), fma_(em.y, T.y, ret.y), fma_(em.z, T.z, ret.z));
                         const V3 cf = do_spec ? ld3(M.spec_color) : ld3(M.albedo);
                         if (!do_refr) T = mul(T, cf);
@@ -491,7 +579,7 @@ __global__ __launch_bounds__(256) void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
         if (pvalid) {
             for (int f = 0; f < nf; ++f) {
                 const float* c = col + (f * 64 + lane) * 3;
-                const float bf = 1.0f / ((float)(job.frame_first + (uint32_t)(c0 + f)) + 1.0f);   // :1200
+                const float bf = rcp((float)(job.frame_first + (uint32_t)(c0 + f)) + 1.0f);   // :1200
                 acc = v3(fma_(bf, c[0] - acc.x, acc.x), fma_(bf, c[1] - acc.y, acc.y), fma_(bf, c[2] - acc.z, acc.z));
             }
         }
@@ -523,8 +611,16 @@ hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool 
 {
     const int tiles = ((j.ncols + 7) / 8) * ((j.nrows + 7) / 8);
     const dim3 grid((unsigned)((tiles + kWaves - 1) / kWaves)), block(256);
-    if (count) hipLaunchKernelGGL((pt_v4_kernel<ENV, LAYOUT, true>), grid, block, 0, st, j, sc);
-    else hipLaunchKernelGGL((pt_v4_kernel<ENV, LAYOUT, false>), grid, block, 0, st, j, sc);
+#ifndef PT_V4_FORCE_GENERIC
+#define PT_V4_FORCE_GENERIC 0   // A/B builds: the scene-table path even for the default scene
+#endif
+    if (j.default_scene && !PT_V4_FORCE_GENERIC) {
+        if (count) hipLaunchKernelGGL((pt_v4_kernel<ENV, LAYOUT, true, true>), grid, block, 0, st, j, sc);
+        else hipLaunchKernelGGL((pt_v4_kernel<ENV, LAYOUT, false, true>), grid, block, 0, st, j, sc);
+    } else {
+        if (count) hipLaunchKernelGGL((pt_v4_kernel<ENV, LAYOUT, true, false>), grid, block, 0, st, j, sc);
+        else hipLaunchKernelGGL((pt_v4_kernel<ENV, LAYOUT, false, false>), grid, block, 0, st, j, sc);
+    }
     return hipGetLastError();
 }
 

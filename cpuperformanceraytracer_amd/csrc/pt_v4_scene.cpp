@@ -3,6 +3,7 @@
 // operations (fused where it wrote fmadd/fmsub: cross mathlib.h:770-778, dot :145).  The kernel reads
 // the resulting tables; nothing per pixel is precomputed beyond what the reference precomputes.
 #include "pt_v4.h"
+#include "pt_v4_default_scene.h"
 #include <cmath>
 #include <cstring>
 
@@ -104,4 +105,15 @@ int pt_v4_build_scene(const PtV4SceneDesc* d, PtV4Scene* s)
         s->mat[i].albedo[1] = s->mat[i].albedo[2] = d->mat[i].albedo[0];
     }
     return 0;
+}
+
+bool pt_v4_is_default_geometry(const PtV4Scene& s)
+{
+    namespace D = pt_v4_default;
+    if (s.nquads != D::kQuads || s.nspheres != D::kSpheres) return false;
+    for (int i = 0; i < D::kQuads; ++i)
+        if (std::memcmp(&s.quad[i], D::kQuad[i], sizeof(D::kQuad[i]))) return false;   // bit patterns (signed zeros)
+    for (int i = 0; i < D::kSpheres; ++i)
+        if (std::memcmp(s.sph[i], D::kSphere[i], sizeof(D::kSphere[i]))) return false;
+    return true;
 }

@@ -309,6 +309,19 @@ def AddSphereObjectToScene(position_radius) -> int:
     return rc
 
 
+def v4_scene_tables() -> tuple[np.ndarray, int, int]:
+    """The current v4 scene's precomputed tables (pt_v4_get_scene_tables): (floats, nquads, nspheres)."""
+    L = N.load()
+    nq, ns = ctypes.c_int32(), ctypes.c_int32()
+    need = L.pt_v4_get_scene_tables(None, 0, ctypes.byref(nq), ctypes.byref(ns))
+    if need < 0:
+        N.check(need, "pt_v4_get_scene_tables")
+    out = np.zeros(need, np.float32)
+    N.check(0 if L.pt_v4_get_scene_tables(out.ctypes.data, need, ctypes.byref(nq), ctypes.byref(ns)) == need else -1,
+            "pt_v4_get_scene_tables")
+    return out, nq.value, ns.value
+
+
 def v4_set_frame(frame: int) -> None:
     N.check(N.load().pt_v4_set_frame(frame), "pt_v4_set_frame")
 

@@ -197,6 +197,12 @@ int pt_v4_add_quad(const float vertices[12]);         /* V0..V3 xyz; returns the
 int pt_v4_add_sphere(const float position_radius[4]); /* returns the quad count (as v4 :1400) or PT_E*  */
 int pt_v4_set_frame(uint32_t frame);
 uint32_t pt_v4_get_frame(void);
+/* introspection: the current scene's precomputed tables (PrecomputeQuadData v4 :269-320 +
+ * AddMaterialToScene :1368-1388): per quad V0, normal, NxV01/DetBot, NxV20/DetBot, NxV30/DetTop,
+ * NxV02/DetTop (18 f32), per sphere x y z r (4 f32), then PT_V4_MAX_OBJECTS material rows (17 f32,
+ * pt_v4_material order).  Returns the number of floats written (or needed, when n is too small),
+ * with *nquads / *nspheres set; PT_E* on error. */
+int pt_v4_get_scene_tables(float* out, int32_t n, int32_t* nquads, int32_t* nspheres);
 /* replaces DemofoxRenderOptV4 (v4 .h:14, .cpp:1696-1721): advance iFrame, render every tile into the
  * tiled accumulator (RenderTile v4 :1179-1258 layout), then (output_to_screen, screen != NULL) write
  * width*height XRGB8 pixels into `screen`.  tex may be NULL with PT_V4_ENV_NONE. */

@@ -473,7 +473,8 @@ static v3 color_for_ray(const ctx4* c, v3 pos, v3 dir, uint32_t* rng)
     v3 ret = mk(0.0f, 0.0f, 0.0f), T = mk(1.0f, 1.0f, 1.0f);
     for (int bounce = 0; bounce <= p->num_bounces; ++bounce) {
         hit4 h = {0, V4_SUPER_FAR, {0.0f, 0.0f, 0.0f}, 0};
-        CNT(c, scene_trace(s, pos, dir, &h));
+        const uint64_t trace_flops = scene_trace(s, pos, dir, &h);
+        CNT(c, trace_flops);
         if (c->cnt) c->cnt->segments++;
         const int miss = h.dist == V4_SUPER_FAR;
         /* the ambient / env term is evaluated every iteration (:769-784): its RNG draws happen on

@@ -29,7 +29,7 @@ dst.mkdir(exist_ok=True)
 ENV = workload.startswith("c4")
 KERNEL = "pt_render_env_kernel<0, false>" if ENV else "pt_render_kernel<0, false>"
 if workload.startswith("v4"):
-    KERNEL = "pt_v4_kernel<1, 0, false>"   # <PT_V4_ENV_EQUIRECT_, PT_LAYOUT_INTERLEAVED, COUNT = false>
+    KERNEL = "pt_v4_kernel<1, 0, false, true>"   # <EQUIRECT, INTERLEAVED, COUNT = false, default-scene literals>
 SUMMARY = "pmc_summary.json" if workload == "c2_1080p" else f"pmc_summary_{workload}.json"
 
 stats = glob.glob(str(src / "trace" / "**" / "*kernel_stats.csv"), recursive=True)

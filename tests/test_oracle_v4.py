@@ -148,3 +148,12 @@ def test_counts_and_scene_limits():
     s.nspheres = 9   # 4 quads + 9 spheres > MAX_OBJECTS
     with pytest.raises(ValueError):
         po.render4(8, 8, scene=s)
+
+
+def test_counted_render_equals_plain_render():
+    """Instrumentation never changes a pixel (counting on/off, threads)."""
+    env = np.random.default_rng(8).random((16, 32, 3), dtype=np.float32)
+    a, _ = po.render4(64, 48, nframes=3, env=env, counts=True)
+    b = po.render4(64, 48, nframes=3, env=env, nthreads=4)
+    assert bits_equal(a, b)
+    assert (b != 0).any() and len(np.unique(b.reshape(-1, 3), axis=0)) > 100   # the scene is traced
