@@ -26,7 +26,12 @@ from .renderer import (  # noqa: F401
     AddSphereObjectToScene,
     LoadCubemapTexture,
     v4_config,
+    v4_begin_frame,
     v4_get_frame,
+    MakeWorkQueue,
+    AddWorkQueueEntry,
+    CompleteAllWork,
+    WorkQueue,
     v4_set_frame,
     LoadTexture,
     RenderBufferInfo,
@@ -50,5 +55,6 @@ __all__ = [
     "make_tiles", "readback", "set_env_map", "set_frame", "shutdown", "texture", "tonemap", "WriteImage",
     "DemofoxRenderOptV4", "InitializeGlobalRenderResources", "ReinitializeRenderTileData", "InitializeScene",
     "ClearScene", "AddMaterialToScene", "AddQuadObjectToScene", "AddSphereObjectToScene", "LoadCubemapTexture",
-    "v4_config", "v4_get_frame", "v4_set_frame",
+    "v4_config", "v4_begin_frame", "v4_get_frame", "v4_set_frame", "MakeWorkQueue", "AddWorkQueueEntry",
+    "CompleteAllWork", "WorkQueue",
 ]

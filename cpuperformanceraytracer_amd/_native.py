@@ -38,8 +38,14 @@ EXPORTED_SYMBOLS = (
     "pt_v4_default_config", "pt_v4_set_config", "pt_v4_initialize_global_render_resources",
     "pt_v4_reinitialize_render_tile_data", "pt_v4_initialize_scene", "pt_v4_clear_scene", "pt_v4_add_material",
     "pt_v4_add_quad", "pt_v4_add_sphere", "pt_v4_set_frame", "pt_v4_get_frame", "pt_v4_get_scene_tables", "pt_render_opt_v4",
-    "pt_copy_output_to_file", "pt_v4_render_device", "pt_v4_count_device",
+    "pt_copy_output_to_file", "pt_v4_render_device", "pt_v4_count_device", "pt_v4_begin_frame",
+    "pt_make_work_queue", "pt_add_work_queue_entry", "pt_complete_all_work", "pt_complete_all_work_async",
+    "pt_wait_work", "pt_work_queue_size", "pt_free_work_queue",
 )
+
+PT_RENDERER_SIMD_TILED = 0
+PT_RENDERER_SIMT_TEXTURED = 1
+PT_RENDERER_V4 = 2
 
 PT_V4_ENV_NONE = 0
 PT_V4_ENV_EQUIRECT = 1
@@ -165,6 +171,14 @@ def load() -> ctypes.CDLL:
         "pt_copy_output_to_file": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp]),
         "pt_v4_render_device": (i32, [ctypes.POINTER(PtDeviceJob), vp]),
         "pt_v4_count_device": (i32, [ctypes.POINTER(PtDeviceJob), vp, ctypes.POINTER(PtWorkCounts)]),
+        "pt_v4_begin_frame": (i32, []),
+        "pt_make_work_queue": (vp, [i32]),
+        "pt_add_work_queue_entry": (i32, [vp, ctypes.POINTER(PtBufferInfo), ctypes.POINTER(PtTileInfo)]),
+        "pt_complete_all_work": (i32, [vp]),
+        "pt_complete_all_work_async": (i32, [vp]),
+        "pt_wait_work": (i32, [vp]),
+        "pt_work_queue_size": (i32, [vp]),
+        "pt_free_work_queue": (None, [vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -15,6 +15,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <new>
+#include <vector>
 
 namespace {
 
@@ -434,6 +436,48 @@ int upload_env(const pt_texture* t)
     return PT_OK;
 }
 
+// RenderTile argument checks (simd_tiled.cpp:489-535 assumptions; Application.cpp:36-94)
+int check_tile(const pt_buffer_info* b, const pt_tile_info* t)
+{
+    int rc;
+    if (!b || !t) return fail(PT_EINVAL, "null tile/buffer info");
+    if ((rc = check_frame_args(b->data, b->width, b->height, b->num_channels))) return rc;
+    const int32_t tw = t->tile_width, th = t->tile_height;
+    if (tw <= 0 || th <= 0 || tw % 8) return fail(PT_EINVAL, "tile width %d must be a positive multiple of 8", tw);
+    if (t->tile_x < 0 || t->tile_y < 0) return fail(PT_EINVAL, "negative tile index");
+    if (t->tile_min_x != t->tile_x * tw || t->tile_max_x != t->tile_min_x + tw - 1 ||
+        t->tile_min_y != t->tile_y * th || t->tile_max_y != t->tile_min_y + th - 1)
+        return fail(PT_EINVAL, "tile bounds inconsistent with (TileX, TileY, TileWidth, TileHeight)");
+    if (t->tile_max_x >= b->width || t->tile_max_y >= b->height) return fail(PT_EINVAL, "tile outside the buffer");
+    if (b->width % tw) return fail(PT_EINVAL, "buffer width %d not a multiple of tile width %d", b->width, tw);
+    return PT_OK;
+}
+
+size_t tile_offset(const pt_buffer_info* b, const pt_tile_info* t)   // in floats (simd_tiled.cpp:499-502)
+{
+    return (size_t)t->tile_y * t->tile_height * b->width * 3 + (size_t)t->tile_x * t->tile_width * t->tile_height * 3;
+}
+
+// the diffuse-path job of one tile at the current frame (env: the config-4 miss term or nullptr)
+PtJob tile_job(const pt_buffer_info* b, const pt_tile_info* t, const float* env)
+{
+    PtJob j = base_job(g.dbuf, b->width, b->height);
+    j.layout = PT_LAYOUT_TILED_PLANAR8;
+    j.tile_w = t->tile_width;
+    j.tile_h = t->tile_height;
+    j.col0 = t->tile_min_x;
+    j.ncols = t->tile_width;
+    j.row_start = t->tile_min_y;
+    j.nrows = t->tile_height;
+    j.frame_first = g.frame - (uint32_t)g.cfg.samples_per_frame + 1;
+    if (env) {
+        j.env = env;
+        j.env_w = g.env_w;
+        j.env_h = g.env_h;
+    }
+    return j;
+}
+
 // ---- v4 helpers ----------------------------------------------------------------------------------
 
 int v4_rebuild()
@@ -660,33 +704,16 @@ int pt_begin_frame(void)
 int pt_render_tile(const pt_buffer_info* b, const pt_tile_info* t)
 {
     int rc;
-    if (!b || !t) return fail(PT_EINVAL, "null tile/buffer info");
-    if ((rc = check_frame_args(b->data, b->width, b->height, b->num_channels)) || (rc = ensure_init())) return rc;
-    const int32_t tw = t->tile_width, th = t->tile_height;
-    if (tw <= 0 || th <= 0 || tw % 8) return fail(PT_EINVAL, "tile width %d must be a positive multiple of 8", tw);
-    if (t->tile_x < 0 || t->tile_y < 0) return fail(PT_EINVAL, "negative tile index");
-    if (t->tile_min_x != t->tile_x * tw || t->tile_max_x != t->tile_min_x + tw - 1 ||
-        t->tile_min_y != t->tile_y * th || t->tile_max_y != t->tile_min_y + th - 1)
-        return fail(PT_EINVAL, "tile bounds inconsistent with (TileX, TileY, TileWidth, TileHeight)");
-    if (t->tile_max_x >= b->width || t->tile_max_y >= b->height) return fail(PT_EINVAL, "tile outside the buffer");
-    if (b->width % tw) return fail(PT_EINVAL, "buffer width %d not a multiple of tile width %d", b->width, tw);
+    if ((rc = check_tile(b, t)) || (rc = ensure_init())) return rc;
     if (g.frame < (uint32_t)g.cfg.samples_per_frame)
         return fail(PT_ESTATE, "RenderTile before the first frame was started (pt_begin_frame)");
+    const int32_t tw = t->tile_width, th = t->tile_height;
     const size_t bytes = (size_t)b->width * b->height * 3 * sizeof(float);
     // simd_tiled.cpp:499-502: the tile is one contiguous slice
-    const size_t off = ((size_t)t->tile_y * th * b->width * 3 + (size_t)t->tile_x * tw * th * 3) * sizeof(float);
+    const size_t off = tile_offset(b, t) * sizeof(float);
     const size_t len = (size_t)tw * th * 3 * sizeof(float);
     if ((rc = stage_in(b->data, bytes, off, len))) return rc;
-    PtJob j = base_job(g.dbuf, b->width, b->height);
-    j.layout = PT_LAYOUT_TILED_PLANAR8;
-    j.tile_w = tw;
-    j.tile_h = th;
-    j.col0 = t->tile_min_x;
-    j.ncols = tw;
-    j.row_start = t->tile_min_y;
-    j.nrows = th;
-    j.frame_first = g.frame - (uint32_t)g.cfg.samples_per_frame + 1;
-    if ((rc = launch(j, g.stream, false))) return rc;
+    if ((rc = launch(tile_job(b, t, nullptr), g.stream, false))) return rc;
     return stage_out(b->data, off, len);
 }
 
@@ -1043,6 +1070,200 @@ int pt_v4_count_device(const pt_device_job* dj, void* stream, pt_work_counts* ou
     out->escaped = h[2];
     out->primary = out->samples;   // one camera ray per sample (jittered)
     return PT_OK;
+}
+
+int pt_v4_begin_frame(void)
+{
+    if (g.v4_frame + 1u >= kMaxFrame) return fail(PT_EINVAL, "v4 frame counter exceeds the exact f32 range 2^24");
+    g.v4_frame += 1;
+    return PT_OK;
+}
+
+// ---- tile work queue ------------------------------------------------------------------------------
+
+}  // extern "C"
+
+struct pt_work_queue {
+    int32_t renderer = PT_RENDERER_SIMD_TILED;
+    std::vector<std::pair<pt_buffer_info, pt_tile_info>> entries;
+    bool pending = false;   // an async completion not yet waited for
+};
+
+namespace {
+
+// Render the queued entries: per buffer (in first-use order) either one full-frame launch (the
+// entries are exactly the buffer's NTX x NTY tiles) or one launch per tile; uploads / downloads of
+// only what is rendered.  Everything is enqueued on g.stream; `wait` synchronises at the end.
+int run_queue(pt_work_queue* q, bool wait)
+{
+    int rc;
+    if ((rc = ensure_init())) return rc;
+    const bool v4 = q->renderer == PT_RENDERER_V4;
+    if (v4) {
+        if (g.v4_frame < 1) return fail(PT_ESTATE, "v4 work queue before the first frame (pt_v4_begin_frame)");
+        if ((rc = v4_ensure_scene())) return rc;
+    } else if (g.frame < (uint32_t)g.cfg.samples_per_frame) {
+        return fail(PT_ESTATE, "work queue before the first frame was started (pt_begin_frame)");
+    }
+    const float* env = nullptr;
+    if (q->renderer == PT_RENDERER_SIMT_TEXTURED) {
+        if (!g.denv) return fail(PT_ESTATE, "textured work queue without an env map (pt_set_env_map)");
+        env = g.denv;
+    }
+    std::vector<bool> done(q->entries.size(), false);
+    for (size_t i = 0; i < q->entries.size(); ++i) {
+        if (done[i]) continue;
+        const pt_buffer_info& b = q->entries[i].first;
+        std::vector<size_t> mine;
+        for (size_t k = i; k < q->entries.size(); ++k)
+            if (!done[k] && q->entries[k].first.data == b.data) {
+                const pt_buffer_info& bk = q->entries[k].first;
+                if (bk.width != b.width || bk.height != b.height)
+                    return fail(PT_EINVAL, "entries of one buffer disagree on its size");
+                mine.push_back(k);
+                done[k] = true;
+            }
+        const pt_tile_info& t0 = q->entries[mine[0]].second;
+        const int32_t tw = t0.tile_width, th = t0.tile_height;
+        bool full = b.width % tw == 0 && b.height % th == 0 &&
+                    mine.size() == (size_t)(b.width / tw) * (size_t)(b.height / th);
+        if (full) {   // exactly every tile once?
+            std::vector<char> seen((size_t)(b.width / tw) * (b.height / th), 0);
+            for (size_t k : mine) {
+                const pt_tile_info& t = q->entries[k].second;
+                const size_t id = (size_t)t.tile_y * (b.width / tw) + t.tile_x;
+                if (t.tile_width != tw || t.tile_height != th || seen[id]) {
+                    full = false;
+                    break;
+                }
+                seen[id] = 1;
+            }
+        }
+        const size_t bytes = (size_t)b.width * b.height * 3 * sizeof(float);
+        const size_t tlen = (size_t)tw * th * 3 * sizeof(float);
+        if (full) {
+            if ((rc = stage_in(b.data, bytes, 0, bytes))) return rc;
+        } else {
+            for (size_t k : mine) {
+                const pt_tile_info& t = q->entries[k].second;
+                if ((rc = stage_in(b.data, bytes, tile_offset(&b, &t) * sizeof(float),
+                                   (size_t)t.tile_width * t.tile_height * 3 * sizeof(float))))
+                    return rc;
+            }
+        }
+        // one job for the whole frame, or one per tile
+        const size_t njobs = full ? 1 : mine.size();
+        for (size_t n = 0; n < njobs; ++n) {
+            pt_tile_info t = q->entries[mine[n]].second;
+            if (full) {   // the frame as one "tile" region in the tiled layout
+                t.tile_min_x = 0;
+                t.tile_min_y = 0;
+            }
+            if (v4) {
+                PtV4Job j = v4_job(g.dbuf, b.width, b.height);
+                j.layout = PT_LAYOUT_TILED_PLANAR8;
+                j.tile_w = t.tile_width;
+                j.tile_h = t.tile_height;
+                j.col0 = t.tile_min_x;
+                j.ncols = full ? b.width : t.tile_width;
+                j.row_start = t.tile_min_y;
+                j.nrows = full ? b.height : t.tile_height;
+                j.frame_first = g.v4_frame;   // the frame pt_v4_begin_frame started
+                if ((rc = v4_use_env(j)) || (rc = v4_launch(j, g.stream, false))) return rc;
+            } else {
+                PtJob j = tile_job(&b, &t, env);
+                if (full) {
+                    j.ncols = b.width;
+                    j.nrows = b.height;
+                }
+                if ((rc = launch(j, g.stream, false))) return rc;
+            }
+        }
+        if (!(g.cfg.flags & PT_FLAG_DEFER_READBACK)) {
+            if (full) {
+                HIP_TRY(hipMemcpyAsync(b.data, g.dbuf, bytes, hipMemcpyDeviceToHost, g.stream));
+            } else {
+                for (size_t k : mine) {
+                    const pt_tile_info& t = q->entries[k].second;
+                    const size_t off = tile_offset(&b, &t) * sizeof(float);
+                    HIP_TRY(hipMemcpyAsync((char*)b.data + off, (const char*)g.dbuf + off,
+                                           (size_t)t.tile_width * t.tile_height * 3 * sizeof(float),
+                                           hipMemcpyDeviceToHost, g.stream));
+                }
+            }
+        }
+        (void)tlen;
+        // the mirror holds one buffer at a time: another buffer of the queue must not start
+        // overwriting it before this one's downloads are done (stream order guarantees that)
+    }
+    q->entries.clear();
+    if (wait) {
+        HIP_TRY(hipStreamSynchronize(g.stream));
+        q->pending = false;
+    } else {
+        q->pending = true;
+    }
+    return PT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+pt_work_queue* pt_make_work_queue(int32_t renderer)
+{
+    if (renderer < PT_RENDERER_SIMD_TILED || renderer > PT_RENDERER_V4) {
+        fail(PT_EINVAL, "unknown renderer %d", renderer);
+        return nullptr;
+    }
+    pt_work_queue* q = new (std::nothrow) pt_work_queue;
+    if (!q) {
+        fail(PT_ENOMEM, "out of host memory");
+        return nullptr;
+    }
+    q->renderer = renderer;
+    q->entries.reserve(1024);   // WORK_QUEUE_MAX_ENTRIES (work_queue.h:16)
+    return q;
+}
+
+int pt_add_work_queue_entry(pt_work_queue* q, const pt_buffer_info* b, const pt_tile_info* t)
+{
+    int rc;
+    if (!q) return fail(PT_EINVAL, "null queue");
+    if ((rc = check_tile(b, t))) return rc;
+    if (q->entries.size() >= 1023)   // the ring holds MaxEntryCount - 1 (work_queue.cpp:42 assert)
+        return fail(PT_EINVAL, "work queue full (WORK_QUEUE_MAX_ENTRIES 1024)");
+    q->entries.emplace_back(*b, *t);
+    return PT_OK;
+}
+
+int pt_complete_all_work(pt_work_queue* q)
+{
+    if (!q) return fail(PT_EINVAL, "null queue");
+    return run_queue(q, true);
+}
+
+int pt_complete_all_work_async(pt_work_queue* q)
+{
+    if (!q) return fail(PT_EINVAL, "null queue");
+    return run_queue(q, false);
+}
+
+int pt_wait_work(pt_work_queue* q)
+{
+    if (!q) return fail(PT_EINVAL, "null queue");
+    if (q->pending && g.inited) HIP_TRY(hipStreamSynchronize(g.stream));
+    q->pending = false;
+    return PT_OK;
+}
+
+int32_t pt_work_queue_size(const pt_work_queue* q) { return q ? (int32_t)q->entries.size() : 0; }
+
+void pt_free_work_queue(pt_work_queue* q)
+{
+    if (!q) return;
+    if (q->pending && g.inited) (void)hipStreamSynchronize(g.stream);
+    delete q;
 }
 
 }  // extern "C"

@@ -383,8 +383,13 @@ __device__ __forceinline__ size_t out_index(const PtV4Job& j, int x, int r)   //
            ((size_t)ly * j.tile_w + (size_t)(lx & ~7)) * 3u + (size_t)(lx & 7);
 }
 
+#ifdef PT_V4_WAVES   // A/B builds: force the occupancy (waves per SIMD)
+#define PT_V4_OCC __attribute__((amdgpu_waves_per_eu(PT_V4_WAVES, PT_V4_WAVES)))
+#else
+#define PT_V4_OCC
+#endif
 template <int ENV, int LAYOUT, bool COUNT, bool DEF>
-__global__ __launch_bounds__(256) void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
+__global__ __launch_bounds__(256) PT_V4_OCC void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
 {
     __shared__ float s_col[kWaves][kChunk * 64 * 3];
     __shared__ PtV4Mat s_mat[PT_V4_MAX_OBJECTS];
@@ -407,7 +412,9 @@ __global__ __launch_bounds__(256) void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
     float* acc_p = nullptr;
     V3 acc = v3(0.0f, 0.0f, 0.0f);
     if (pvalid) {
-        acc_p = job.buf + out_index<LAYOUT>(job, px, pr);
+        // compact layouts index the buffer row; the tiled layout indexes the full image (global row)
+        const int orow = LAYOUT == PT_LAYOUT_TILED_PLANAR8 ? job.row_start + pr * job.row_stride : pr;
+        acc_p = job.buf + out_index<LAYOUT>(job, px, orow);
         acc = v3(acc_p[0], acc_p[cs], acc_p[2 * cs]);
     }
     const Tex tex{job.env, job.env_w, job.env_h};

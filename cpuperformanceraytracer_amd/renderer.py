@@ -120,14 +120,79 @@ def BeginFrame() -> None:
     N.check(N.load().pt_begin_frame(), "pt_begin_frame")
 
 
-def RenderTile(BufferInfo: RenderBufferInfo, TileInfo: RenderTileInfo) -> None:
-    """Render one tile at the current frame into its tile-major slice (simd_tiled.cpp:489-535)."""
+def _tile_args(BufferInfo: RenderBufferInfo, TileInfo: RenderTileInfo):
     b = N.PtBufferInfo(_buf(BufferInfo.BufferDataPtr, BufferInfo.BufferWidth, BufferInfo.BufferHeight,
                             BufferInfo.NumChannels),
                        BufferInfo.BufferWidth, BufferInfo.BufferHeight, BufferInfo.NumChannels)
     t = N.PtTileInfo(TileInfo.TileX, TileInfo.TileY, TileInfo.TileWidth, TileInfo.TileHeight,
                      TileInfo.TileMinX, TileInfo.TileMaxX, TileInfo.TileMinY, TileInfo.TileMaxY)
+    return b, t
+
+
+def RenderTile(BufferInfo: RenderBufferInfo, TileInfo: RenderTileInfo) -> None:
+    """Render one tile at the current frame into its tile-major slice (simd_tiled.cpp:489-535)."""
+    b, t = _tile_args(BufferInfo, TileInfo)
     N.check(N.load().pt_render_tile(ctypes.byref(b), ctypes.byref(t)), "RenderTile")
+
+
+class WorkQueue:
+    """work_queue.cpp (MakeWorkQueue / AddWorkQueueEntry / CompleteAllWork) for the renderers' one
+    use of it: a frame's RenderTile entries, rendered on the GPU at completion -- one launch for a
+    whole frame of tiles.  renderer: N.PT_RENDERER_SIMD_TILED / _SIMT_TEXTURED / _V4."""
+
+    def __init__(self, renderer: int = N.PT_RENDERER_SIMD_TILED):
+        L = N.load()
+        self._q = L.pt_make_work_queue(renderer)
+        if not self._q:
+            raise N.PtError(N.PT_EINVAL, "MakeWorkQueue", L.pt_last_error().decode(errors="replace"))
+        self._keep = []   # host buffers referenced by queued entries
+
+    def add(self, BufferInfo: RenderBufferInfo, TileInfo: RenderTileInfo) -> None:
+        b, t = _tile_args(BufferInfo, TileInfo)
+        N.check(N.load().pt_add_work_queue_entry(self._q, ctypes.byref(b), ctypes.byref(t)), "AddWorkQueueEntry")
+        self._keep.append(BufferInfo.BufferDataPtr)
+
+    def complete(self, wait: bool = True) -> None:
+        L = N.load()
+        if wait:
+            N.check(L.pt_complete_all_work(self._q), "CompleteAllWork")
+            self._keep = []
+        else:
+            N.check(L.pt_complete_all_work_async(self._q), "pt_complete_all_work_async")
+
+    def wait(self) -> None:
+        N.check(N.load().pt_wait_work(self._q), "pt_wait_work")
+        self._keep = []
+
+    def __len__(self) -> int:
+        return int(N.load().pt_work_queue_size(self._q))
+
+    def close(self) -> None:
+        if self._q:
+            N.load().pt_free_work_queue(self._q)
+            self._q = None
+            self._keep = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def MakeWorkQueue(renderer: int = N.PT_RENDERER_SIMD_TILED) -> WorkQueue:
+    """work_queue.cpp:84-108 (the GPU takes the place of the NUM_THREADS workers)."""
+    return WorkQueue(renderer)
+
+
+def AddWorkQueueEntry(Queue: WorkQueue, BufferInfo: RenderBufferInfo, TileInfo: RenderTileInfo) -> None:
+    """work_queue.cpp:37-56 with the RenderTile callback (DoWorkerThreadWork, v4 :1350-1358)."""
+    Queue.add(BufferInfo, TileInfo)
+
+
+def CompleteAllWork(Queue: WorkQueue) -> None:
+    """work_queue.cpp:63-71: every queued tile rendered, buffers updated on return."""
+    Queue.complete(wait=True)
 
 
 def make_tiles(width: int, height: int, num_tiles_x: int, num_tiles_y: int):
@@ -320,6 +385,11 @@ def v4_scene_tables() -> tuple[np.ndarray, int, int]:
     N.check(0 if L.pt_v4_get_scene_tables(out.ctypes.data, need, ctypes.byref(nq), ctypes.byref(ns)) == need else -1,
             "pt_v4_get_scene_tables")
     return out, nq.value, ns.value
+
+
+def v4_begin_frame() -> None:
+    """iFrame += 1 of DemofoxRenderOptV4 (v4 :1703) without rendering (hosts that queue tiles)."""
+    N.check(N.load().pt_v4_begin_frame(), "pt_v4_begin_frame")
 
 
 def v4_set_frame(frame: int) -> None:

@@ -214,10 +214,35 @@ int pt_render_opt_v4(float* buf, int32_t width, int32_t height, int32_t num_tile
 int pt_copy_output_to_file(const float* buf, int32_t width, int32_t height, int32_t num_tiles_x,
                            int32_t num_tiles_y, int32_t tile_width, int32_t tile_height, int32_t num_channels,
                            void* file_pixels);
+/* advance v4's iFrame once without rendering (the `iFrame += 1.0f` of DemofoxRenderOptV4 :1703) -- for
+ * hosts that queue the frame's tiles themselves (pt_make_work_queue(PT_RENDERER_V4)) */
+int pt_v4_begin_frame(void);
 /* HBM-resident v4 job (bench / shards): the interleaved or planar8 layout; use_env selects the
  * config's env mode with the map of pt_set_env_map (else the ambient); num_bounces from the job */
 int pt_v4_render_device(const pt_device_job* job, void* hip_stream);
 int pt_v4_count_device(const pt_device_job* job, void* hip_stream, pt_work_counts* out);   /* sync */
+
+/* --- tile work queue: the host tile scheduler, on the GPU ------------------------
+ * Replaces work_queue.cpp (MakeWorkQueue :84-108, AddWorkQueueEntry :37-56, CompleteAllWork :63-71) for
+ * its one use by the renderers: a frame's RenderTile entries (simd_tiled.cpp:549-571, simt_pooled,
+ * v4 :1696-1721, DoWorkerThreadWork :1350-1358).  Entries only record (buffer, tile); completion renders
+ * them all at the renderer's CURRENT frame (pt_begin_frame / pt_v4_begin_frame advance it): a queue
+ * holding every tile of a buffer becomes ONE launch over the frame with one upload and one download,
+ * otherwise one launch per tile, back to back on one stream.  Results equal one RenderTile call per
+ * entry.  Not thread-safe (one host thread, like the rest of the library). */
+#define PT_RENDERER_SIMD_TILED 0      /* RenderTile of demofox_path_tracing_simd_tiled.cpp:489-535      */
+#define PT_RENDERER_SIMT_TEXTURED 1   /* its env-map variant (simt_textured.cpp:491-533; pt_set_env_map)  */
+#define PT_RENDERER_V4 2              /* RenderTile of optimization_v4.cpp:1179-1258 (pt_v4_set_config)   */
+typedef struct pt_work_queue pt_work_queue;
+pt_work_queue* pt_make_work_queue(int32_t renderer);          /* NULL on error (pt_last_error)          */
+int pt_add_work_queue_entry(pt_work_queue* q, const pt_buffer_info* buffer, const pt_tile_info* tile);
+int pt_complete_all_work(pt_work_queue* q);                    /* render every entry, wait, empty queue  */
+/* enqueue the same work and return: the host buffers are updated once pt_wait_work returns (keep them
+ * alive and untouched meanwhile) -- a progressive host presents frame k while frame k+1 renders */
+int pt_complete_all_work_async(pt_work_queue* q);
+int pt_wait_work(pt_work_queue* q);
+int32_t pt_work_queue_size(const pt_work_queue* q);
+void pt_free_work_queue(pt_work_queue* q);
 
 /* --- device-resident entry points -------------------------------------------------------------- */
 int pt_render_device(const pt_device_job* job, void* hip_stream);      /* async on hip_stream     */

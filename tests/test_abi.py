@@ -28,7 +28,8 @@ def lib_path():
 def header_functions() -> set[str]:
     text = (ROOT / "include" / "pt_mi355.h").read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return set(re.findall(r"^\s*(?:int|void|uint32_t|const char\*)\s+(pt_\w+)\s*\(", text, flags=re.M))
+    return set(re.findall(r"^\s*(?:int|int32_t|void|uint32_t|const char\*|pt_work_queue\*)\s+(pt_\w+)\s*\(", text,
+                          flags=re.M))
 
 
 def test_header_declares_the_abi():
