@@ -49,8 +49,10 @@ def parse():
 def cpu_baseline(wl, seconds: float, env=None) -> dict:
     """The oracle (C restatement of demofox_path_tracing_scalar.cpp, bit-identical to it) timed on
     this host's cores on a bounded sample of the same workload -- full-size frames, as many as fit
-    in about `seconds` of wall time -- plus the reference's own scalar build (oracle/_ref,
-    c_numBounces=4 compiled in) single-threaded, for calibration."""
+    in about `seconds` of wall time; beside it the reference's CPU SIMD path (an AVX2 port of
+    simt_pooled, `simd_port`; the value reported is the faster of the two CPU paths, which is the
+    scalar restatement: the SIMD file traces every bounce of every lane under masks) and the
+    reference's own scalar build (oracle/_ref, c_numBounces=4 compiled in) single-threaded."""
     from oracle import pyoracle
     try:
         ncpu = len(os.sched_getaffinity(0))
@@ -74,6 +76,8 @@ def cpu_baseline(wl, seconds: float, env=None) -> dict:
                      f"{dt:.2f} s wall",
            "primary_samples_per_s": samples / dt, "host_cpus_visible": ncpu,
            "cpu_model": _cpu_model()}
+    if env is None:
+        out["simd_port"] = cpu_simd_port(wl, seconds / 2, cores)
     ref = ROOT / "oracle" / "_ref" / "libref_scalar.so"
     if ref.exists() and env is None:
         import ctypes
@@ -94,6 +98,28 @@ def cpu_baseline(wl, seconds: float, env=None) -> dict:
                                    f"c_numBounces), DemofoxRenderScalar built unmodified by oracle/build_ref.sh; "
                                    f"{dt:.2f} s wall"}
     return out
+
+
+def cpu_simd_port(wl, seconds: float, cores: int) -> dict:
+    """The reference's CPU SIMD path (demofox_path_tracing_simt_pooled.cpp: 8 pixels per AVX2 register,
+    per-lane RNG, all bounces under masks, a thread pool over tiles) as an AVX2 port
+    (oracle/pt_cpu_simd.c; the MSVC/SVML original cannot be built here), same workload, NUM_TILES 10x15."""
+    from oracle import pyoracle
+    if not pyoracle.simd_supported():
+        return {"skipped": "host CPU lacks AVX2/FMA"}
+    kw = dict(num_bounces=wl.num_bounces, nthreads=cores)
+    t0 = time.perf_counter()
+    buf = pyoracle.render_simd_tiled(wl.width, wl.height, 10, 15, frame_first=1, nframes=1, **kw)
+    t1 = time.perf_counter() - t0
+    frames = int(max(1, min(1024, round(seconds / max(t1, 1e-6)))))
+    t0 = time.perf_counter()
+    pyoracle.render_simd_tiled(wl.width, wl.height, 10, 15, frame_first=2, nframes=frames, buf=buf, **kw)
+    dt = time.perf_counter() - t0
+    samples = wl.width * wl.height * frames
+    return {"value": samples * wl.num_bounces / dt, "unit": "ray-samples/s", "cores": cores, "kind": "port",
+            "sample": f"{wl.width}x{wl.height}, {frames} frames, {wl.num_bounces} bounces, AVX2+FMA port of "
+                      f"demofox_path_tracing_simt_pooled.cpp (oracle/pt_cpu_simd.c, {cores} threads); {dt:.2f} s wall",
+            "primary_samples_per_s": samples / dt}
 
 
 def cpu_baseline_v4(wl, seconds: float, env, cores: int, ncpu: int) -> dict:

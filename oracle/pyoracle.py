@@ -275,3 +275,40 @@ def env_sample4(env: np.ndarray | None, env_mode: int, random_jitter: bool, dirs
         out[i] = list(o)
     del keep
     return out
+
+
+# ---- CPU baseline: AVX2 port of demofox_path_tracing_simt_pooled.cpp (pt_cpu_simd.c) -----------------
+SIMD_LIB = HERE / "libcpusimd.so"
+_simd = None
+
+
+def simd_load():
+    global _simd
+    if _simd is None:
+        if not SIMD_LIB.exists():
+            build()
+        L = ctypes.CDLL(str(SIMD_LIB))
+        L.ptc_simd_supported.restype = ctypes.c_int
+        L.ptc_render_simd_tiled.restype = ctypes.c_int
+        L.ptc_render_simd_tiled.argtypes = [ctypes.c_void_p] + [ctypes.c_int32] * 4 + [ctypes.c_uint32] + \
+            [ctypes.c_int32] * 3
+        _simd = L
+    return _simd
+
+
+def simd_supported() -> bool:
+    return bool(simd_load().ptc_simd_supported())
+
+
+def render_simd_tiled(width: int, height: int, num_tiles_x: int, num_tiles_y: int, *, frame_first: int = 1,
+                      nframes: int = 1, num_bounces: int = 8, nthreads: int | None = None,
+                      buf: np.ndarray | None = None) -> np.ndarray:
+    """The AVX2 simt_pooled port: accumulate frames into buf (tile-major planar8 layout)."""
+    if buf is None:
+        buf = np.zeros(width * height * 3, np.float32)
+    nthreads = nthreads if nthreads is not None else min(os.cpu_count() or 1, 16)
+    rc = simd_load().ptc_render_simd_tiled(buf.ctypes.data, width, height, num_tiles_x, num_tiles_y, frame_first,
+                                           nframes, num_bounces, nthreads)
+    if rc:
+        raise ValueError(f"ptc_render_simd_tiled failed ({rc})")
+    return buf
