@@ -82,6 +82,19 @@ def build_variant(name: str, defines=(), extra=()) -> Path:
     return out
 
 
+def build_examples(verbose: bool = False) -> Path:
+    """examples/reference_host: a reference-shaped C++ host linked against libpt_mi355.so through
+    the reference-named header only (the drop-in boundary exercised as a real link)."""
+    src = ROOT / "examples" / "reference_host.cpp"
+    out = ROOT / "examples" / "reference_host"
+    cmd = ["g++", "-std=c++17", "-O2", "-Wall", f"-I{ROOT / 'include'}", str(src), f"-L{PKG}", "-lpt_mi355",
+           "-Wl,-rpath,$ORIGIN/../cpuperformanceraytracer_amd", "-o", str(out)]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build_oracle(verbose: bool = False) -> None:
     """Test infrastructure: the C restatement (oracle/liboracle.so) and, when the reference is
     present in this container, its own scalar build (oracle/_ref/).  Building the checker is not
@@ -95,5 +108,6 @@ def build_oracle(verbose: bool = False) -> None:
 
 if __name__ == "__main__":
     build_lib(force="--force" in sys.argv, verbose=True)
+    build_examples(verbose=True)
     build_oracle(verbose=True)
     print(LIB)

@@ -87,3 +87,13 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(N.PtTileInfo) == 8 * 4
     assert ctypes.sizeof(N.PtDeviceJob) == 8 + 9 * 4 + 4
     assert ctypes.sizeof(N.PtWorkCounts) == 5 * 8
+
+
+def test_reference_shaped_host_compiles_and_links(tmp_path):
+    """examples/reference_host.cpp uses only the reference's names (demofox_path_tracing_mi355.h)
+    and links libpt_mi355.so (running it needs a GPU: tests/test_gpu_host.py)."""
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    from cpuperformanceraytracer_amd.build import build_examples
+    exe = build_examples()
+    assert exe.exists()
