@@ -35,7 +35,10 @@ constexpr float kMinHit = 0.01f;      // c_minimumRayHitTime  v4 :10
 constexpr float kNudge = 0.01f;       // c_rayPosNormalNudge  v4 :14
 constexpr float kSuperFar = 10000.0f; // c_superFar           v4 :17
 constexpr float kPi = 3.14159265359f; // c_pi                 mathutils.h:5
-constexpr int kWaves = 4;
+#ifndef PT_V4_BLOCK_WAVES
+#define PT_V4_BLOCK_WAVES 4
+#endif
+constexpr int kWaves = PT_V4_BLOCK_WAVES;   // waves (tiles) per workgroup
 #ifndef PT_V4_CHUNK
 #define PT_V4_CHUNK 8
 #endif
@@ -389,18 +392,18 @@ __device__ __forceinline__ size_t out_index(const PtV4Job& j, int x, int r)   //
 #define PT_V4_OCC
 #endif
 template <int ENV, int LAYOUT, bool COUNT, bool DEF>
-__global__ __launch_bounds__(256) PT_V4_OCC void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
+__global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
 {
     __shared__ float s_col[kWaves][kChunk * 64 * 3];
     __shared__ PtV4Mat s_mat[PT_V4_MAX_OBJECTS];
-    if (threadIdx.x < PT_V4_MAX_OBJECTS * 17)
-        reinterpret_cast<float*>(s_mat)[threadIdx.x] = reinterpret_cast<const float*>(sc.mat)[threadIdx.x];
+    for (int t = threadIdx.x; t < PT_V4_MAX_OBJECTS * 17; t += 64 * kWaves)
+        reinterpret_cast<float*>(s_mat)[t] = reinterpret_cast<const float*>(sc.mat)[t];
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int tiles_x = (job.ncols + 7) >> 3;
     const int ntiles = tiles_x * ((job.nrows + 7) >> 3);
-    const int tile = (int)blockIdx.x * kWaves + wv;
+    const int tile = (int)blockIdx.x * kWaves + wv;   // raster order (reversed / 1-2 wave blocks measured slower)
     if (tile >= ntiles) return;
     const int tcol = (tile % tiles_x) * 8, trow = (tile / tiles_x) * 8;
     float* const col = s_col[wv];
@@ -617,7 +620,7 @@ template <int ENV, int LAYOUT>
 hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool count)
 {
     const int tiles = ((j.ncols + 7) / 8) * ((j.nrows + 7) / 8);
-    const dim3 grid((unsigned)((tiles + kWaves - 1) / kWaves)), block(256);
+    const dim3 grid((unsigned)((tiles + kWaves - 1) / kWaves)), block(64 * kWaves);
 #ifndef PT_V4_FORCE_GENERIC
 #define PT_V4_FORCE_GENERIC 0   // A/B builds: the scene-table path even for the default scene
 #endif
