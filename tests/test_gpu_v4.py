@@ -276,3 +276,13 @@ def test_v4_4k_sampled_rows():
     ref = po.render4(w, h, nframes=frames, env=env, row_start=5, row_stride=97, nrows=len(rows))
     assert bits_equal(got[5::97], ref), mismatch_report(got[5::97], ref)
     assert np.isfinite(got).all()
+
+
+def test_v4_planar8_device_layout():
+    """The planar8 layout of DemofoxRenderSimd (simd.cpp:496-511) for a v4 device job."""
+    from layouts import planar8_to_interleaved
+    env = _tex(32, 64, seed=29)
+    got = _device_v4(96, 40, 3, env=env, layout=N.PT_LAYOUT_PLANAR8)
+    got = planar8_to_interleaved(got.reshape(-1), 96, 40)
+    ref = _oracle(96, 40, 3, env=env)
+    assert bits_equal(got, ref), mismatch_report(got, ref)
