@@ -302,38 +302,55 @@ bool pin(const float* p, size_t bytes)
     return true;
 }
 
+// PT_FLAG_PIN_HOST (without deferred readback) and `buf` page-locked: the frame job `j` (whole
+// image, either renderer) is split into kBands row bands (multiples of row_align rows: contiguous
+// in every layout) whose upload, render (`run(band_job)` on g.stream) and download overlap on three
+// streams.  Returns with the downloads queued on g.s_out; *used = false if the path does not apply.
+template <typename Job, typename Run>
+int render_bands(float* buf, const Job& j, int32_t row_align, Run&& run, bool* used)
+{
+    int rc;
+    const size_t bytes = (size_t)j.width * j.height * 3 * sizeof(float);
+    *used = false;
+    if (!(g.cfg.flags & PT_FLAG_PIN_HOST) || (g.cfg.flags & PT_FLAG_DEFER_READBACK) || !pin(buf, bytes)) return PT_OK;
+    *used = true;
+    if ((rc = ensure_dbuf(bytes))) return rc;
+    g.mirror_valid = false;
+    g.mirror_host = nullptr;
+    const int32_t w = j.width, h = j.height;
+    int32_t rows = (h + kBands - 1) / kBands;
+    rows = (rows + row_align - 1) / row_align * row_align;
+    int k = 0;
+    for (int32_t r0 = 0; r0 < h && k < kBands; r0 += rows, ++k) {
+        const int32_t r1 = r0 + rows < h ? r0 + rows : h;
+        const size_t off = (size_t)r0 * w * 3, len = (size_t)(r1 - r0) * w * 3 * sizeof(float);
+        HIP_TRY(hipMemcpyAsync(g.dbuf + off, buf + off, len, hipMemcpyHostToDevice, g.s_in));
+        HIP_TRY(hipEventRecord(g.ev_in[k], g.s_in));
+        HIP_TRY(hipStreamWaitEvent(g.stream, g.ev_in[k], 0));
+        Job b = j;
+        b.row_start = r0;
+        b.nrows = r1 - r0;
+        b.buf = j.layout == PT_LAYOUT_TILED_PLANAR8 ? g.dbuf : g.dbuf + off;   // tiled: global offsets
+        if ((rc = run(b))) return rc;
+        HIP_TRY(hipEventRecord(g.ev_done[k], g.stream));
+        HIP_TRY(hipStreamWaitEvent(g.s_out, g.ev_done[k], 0));
+        HIP_TRY(hipMemcpyAsync(buf + off, g.dbuf + off, len, hipMemcpyDeviceToHost, g.s_out));
+    }
+    return PT_OK;
+}
+
 // One frame call on a host buffer: the job `j` (whole image) is rendered into the device mirror
-// of `buf`.  With PT_FLAG_PIN_HOST (and without deferred readback) the frame is split into
-// kBands row bands (multiples of row_align rows: contiguous in every layout) whose upload,
-// render and download overlap on three streams; otherwise upload, render, download in turn.
+// of `buf` -- pipelined in row bands with PT_FLAG_PIN_HOST, otherwise upload, render, download in
+// turn.
 int render_frame(float* buf, PtJob j, int32_t row_align)
 {
     int rc;
     const size_t bytes = (size_t)j.width * j.height * 3 * sizeof(float);
     const uint32_t spf = (uint32_t)g.cfg.samples_per_frame;
-    if ((g.cfg.flags & PT_FLAG_PIN_HOST) && !(g.cfg.flags & PT_FLAG_DEFER_READBACK) && pin(buf, bytes)) {
-        if ((rc = ensure_dbuf(bytes))) return rc;
-        g.mirror_valid = false;
-        g.mirror_host = nullptr;
-        const int32_t w = j.width, h = j.height;
-        int32_t rows = (h + kBands - 1) / kBands;
-        rows = (rows + row_align - 1) / row_align * row_align;
-        int k = 0;
-        for (int32_t r0 = 0; r0 < h && k < kBands; r0 += rows, ++k) {
-            const int32_t r1 = r0 + rows < h ? r0 + rows : h;
-            const size_t off = (size_t)r0 * w * 3, len = (size_t)(r1 - r0) * w * 3 * sizeof(float);
-            HIP_TRY(hipMemcpyAsync(g.dbuf + off, buf + off, len, hipMemcpyHostToDevice, g.s_in));
-            HIP_TRY(hipEventRecord(g.ev_in[k], g.s_in));
-            HIP_TRY(hipStreamWaitEvent(g.stream, g.ev_in[k], 0));
-            PtJob b = j;
-            b.row_start = r0;
-            b.nrows = r1 - r0;
-            b.buf = j.layout == PT_LAYOUT_TILED_PLANAR8 ? g.dbuf : g.dbuf + off;   // tiled: global offsets
-            if ((rc = launch(b, g.stream, false))) return rc;
-            HIP_TRY(hipEventRecord(g.ev_done[k], g.stream));
-            HIP_TRY(hipStreamWaitEvent(g.s_out, g.ev_done[k], 0));
-            HIP_TRY(hipMemcpyAsync(buf + off, g.dbuf + off, len, hipMemcpyDeviceToHost, g.s_out));
-        }
+    bool banded = false;
+    if ((rc = render_bands(buf, j, row_align, [](const PtJob& b) { return launch(b, g.stream, false); }, &banded)))
+        return rc;
+    if (banded) {
         g.frame += spf;
         HIP_TRY(hipStreamSynchronize(g.s_out));
         return PT_OK;
@@ -990,12 +1007,19 @@ int pt_render_opt_v4(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty,
             if ((rc = upload_env(tex))) return rc;
     }
     const size_t bytes = (size_t)w * h * 3 * sizeof(float);
-    if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
-    PtV4Job j = v4_job(g.dbuf, w, h);
+    PtV4Job j = v4_job(nullptr, w, h);
     j.layout = PT_LAYOUT_TILED_PLANAR8;   // RenderTile v4 :1186-1191
     j.tile_w = tw;
     j.tile_h = th;
-    if ((rc = v4_use_env(j)) || (rc = v4_launch(j, g.stream, false))) return rc;
+    if ((rc = v4_use_env(j))) return rc;
+    bool banded = false;   // PT_FLAG_PIN_HOST: bands of whole tile rows
+    if ((rc = render_bands(buf, j, th, [](const PtV4Job& b) { return v4_launch(b, g.stream, false); }, &banded)))
+        return rc;
+    if (!banded) {
+        if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
+        j.buf = g.dbuf;
+        if ((rc = v4_launch(j, g.stream, false))) return rc;
+    }
     g.v4_frame += 1;   // iFrame += 1.0f (v4 :1703), before rendering
     if (screen && g.v4cfg.output_to_screen) {   // OutputToScreen per tile (v4 :1562-1564)
         const size_t out_bytes = (size_t)w * h * sizeof(uint32_t);
@@ -1004,6 +1028,11 @@ int pt_render_opt_v4(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty,
         hipError_t e = pt_launch_tonemap(tj, g.stream);
         if (e != hipSuccess) return fail(PT_EHIP, "tonemap launch failed: %s", hipGetErrorString(e));
         HIP_TRY(hipMemcpyAsync(screen, g.dtone_out, out_bytes, hipMemcpyDeviceToHost, g.stream));
+    }
+    if (banded) {
+        HIP_TRY(hipStreamSynchronize(g.s_out));
+        HIP_TRY(hipStreamSynchronize(g.stream));
+        return PT_OK;
     }
     return stage_out(buf, 0, bytes);
 }

@@ -200,10 +200,12 @@ def test_v4_scene_limits():
         pt.InitializeScene()
 
 
-def test_drop_in_opt_v4_tiled_and_screen():
+@pytest.mark.parametrize("pin_host", [False, True])
+def test_drop_in_opt_v4_tiled_and_screen(pin_host):
     """DemofoxRenderOptV4 on a host buffer: tiled accumulator (RenderTile layout), frame counter,
-    OutputToScreen pixels, CopyOutputToFile (+1 frame, RGBA8)."""
-    pt.init()
+    OutputToScreen pixels, CopyOutputToFile (+1 frame, RGBA8).  With PT_FLAG_PIN_HOST the frame
+    is uploaded, rendered and downloaded in row bands of whole tile rows (same bits)."""
+    pt.init(pin_host=pin_host)
     pt.v4_config()   # defaults: equirect, random jitter, rejection sampling, 8 bounces
     pt.InitializeGlobalRenderResources()
     w, h, ntx, nty = 320, 240, 10, 15
