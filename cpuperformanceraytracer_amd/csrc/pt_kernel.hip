@@ -372,7 +372,16 @@ constexpr int kMaxWeights = 64;    // LDS table of the lerp weights 1/(iFrame+1)
 #endif
 constexpr int kChunk = PT_CHUNK;   // frames per phase-B/C chunk (LDS colour slots per pixel)
 
-constexpr int kWavesPerBlock = 4;
+// Waves (8x8 tiles in flight) per workgroup.  LDS is allocated per workgroup in 1280-B granules
+// on gfx950 (measured, scripts/lds_probe.hip; hipOccupancyMaxActiveBlocksPerMultiprocessor does not
+// model it and over-reports 5 blocks for 32001..32768 B), so the 4-wave workgroup (32 720 B -> 26
+// granules) runs 4 per CU: 4 waves per SIMD, although the ambient kernel's 96 VGPRs would allow 5.
+// 5-wave workgroups (40 656 B -> 32 granules) were placed only 3 per CU (15 waves): slower.
+#ifndef PT_AMBIENT_BLOCK_WAVES
+#define PT_AMBIENT_BLOCK_WAVES 4
+#endif
+template <bool ENV>
+constexpr int waves_per_block() { return ENV ? 4 : PT_AMBIENT_BLOCK_WAVES; }
 
 // Env variant: a phase-B miss adds EquirectangularTextureSample(dir) to the sample's radiance
 // (simt_textured.cpp:408), two glibc inverse-trig calls and a texel gather.  Evaluated where the
@@ -403,13 +412,13 @@ template <int LAYOUT, bool ENV, bool COUNT>
 __device__ __forceinline__ void render_body(const PtJob& job)
 {
     const PtScene* __restrict__ sc = job.scene;
+    constexpr int kWavesPerBlock = waves_per_block<ENV>();
     __shared__ PtLdsPrim s_prim[PT_NPRIMS];
     __shared__ AxisRow s_axis[PT_NQUADS * 3];
     __shared__ float s_w[kMaxWeights];
     constexpr int CH = kChunk;
     __shared__ float s_col[kWavesPerBlock][64 * CH * 3];   // phase-B radiance per (pixel, frame)
-    // per item pixel: P1.xyz + (id | lane << 8) and n1 (planar), 28 B: with kChunk 8 the block
-    // fits 32 KiB of LDS, so 5 blocks (5 waves per SIMD) stay resident per CU
+    // per item pixel: P1.xyz + (id | lane << 8) and n1 (planar), 28 B
     __shared__ float4 s_rec[kWavesPerBlock][64];
     __shared__ float s_nrm[kWavesPerBlock][3][64];
     // env variant: the misses of phase B queue their direction (+ colour slot) here, and the queue
@@ -467,7 +476,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 #endif
 
     // (built with the atomic optimizer off: a single-lane atomic needs no wave reduction, and its
-    // return value is then only waited for where it is used, one tile later)
+    // return value is then only waited for where it is used, at the next tile)
     // Tile schedule.  The launch's work is a list of UNITS -- runs of tiles in schedule order
     // (job.order: the previous launch's tiles sorted by descending cost, so the long tiles start
     // first and the tail is made of short ones; job.units: run boundaries, each run worth about
@@ -476,8 +485,9 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     // Units are dealt to PT_NQUEUES groups of blocks (block b -> group b % 8, the XCD it is
     // dispatched to): group x owns unit slots x, x+8, ...  Each wave's first unit is static (its
     // index in the group), later ones come from the group's own counter (one returning atomic per
-    // unit, requested one unit ahead); a group whose units are used up takes the others'.  One
-    // counter for the whole chip saturated (~90 dequeues/us, MI355X_MICROARCH.md "dequeue").
+    // unit, issued when the last tile of the current unit has finished its pool); a group whose
+    // units are used up takes the others'.  One counter for the whole chip saturated (~90
+    // dequeues/us, MI355X_MICROARCH.md "dequeue").
     constexpr uint32_t kNone = 0xffffffffu;
     const uint32_t nunits = job.units ? *job.nunits : total_tiles;
     const uint32_t ngroups = gridDim.x < PT_NQUEUES ? gridDim.x : PT_NQUEUES;   // small grids: fewer
@@ -492,9 +502,15 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     // plain load of a counter screens it first (a counter only grows, so a load that shows it used
     // up is right; without the screening the tail's atomics tripled the launch time).
     uint32_t dead = 0;   // lane 0: groups known to be exhausted
+#ifndef PT_STEAL_SPREAD
+#define PT_STEAL_SPREAD 1
+#endif
+    // victims in a per-wave rotation, so the waves of a group that runs dry do not all queue on
+    // the same neighbour's counter
+    const uint32_t steal0 = PT_STEAL_SPREAD ? (blockIdx.x / ngroups) * kWavesPerBlock + (uint32_t)wv : 0u;
     auto steal = [&]() {
         for (uint32_t k = 1; k < ngroups; ++k) {
-            const uint32_t g = (qg + k) % ngroups;
+            const uint32_t g = ngroups > 1 ? (qg + 1 + (steal0 + k - 1) % (ngroups - 1)) % ngroups : qg;
             if ((dead >> g) & 1u) continue;
             unsigned int* const c = job.queue + g * 32u;
             if (slot_of(g, __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == kNone) {
@@ -511,23 +527,22 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     auto unit_hi = [&](uint32_t u) { return job.units ? job.units[u + 1] : u + 1; };
     auto tile_at = [&](uint32_t i) { return job.order ? job.order[i] : i; };
     unsigned int* const q = job.queue + qg * 32u;
-    // lane 0: the current unit's remaining schedule positions [c_pos, c_end), the next unit's
-    // [n_pos, n_end) (bounds loaded one unit ahead), the raw counter of the unit after it, and the
-    // next tile (its schedule entry loaded one tile ahead)
-    uint32_t c_pos = kNone, c_end = kNone, n_pos = kNone, n_end = kNone, pending = 0;
+    // lane 0: the current unit's remaining schedule positions [c_pos, c_end).  The next unit is
+    // claimed only when the current one is used up, after the pool of its last tile has drained
+    // (its returning atomic and schedule loads overlap that tile's phase C): a claim made earlier
+    // reserves a long tile for a wave that is still busy, and the longest-first order comes apart
+    // at the end of the launch.
+    uint32_t c_pos = kNone, c_end = kNone;
     auto take_next = [&]() -> uint32_t {
-        if (c_pos == c_end) {   // current unit done: switch to the prefetched one
-            c_pos = n_pos;
-            c_end = n_end;
-            if (c_pos == kNone) return kNone;
-            uint32_t u = ((dead >> qg) & 1u) ? kNone : slot_of(qg, pending);
+        if (c_pos == c_end) {
+            uint32_t u = ((dead >> qg) & 1u) ? kNone : slot_of(qg, atomicAdd(q, 1u));
             if (u == kNone) {
                 dead |= 1u << qg;
                 u = steal();
             }
-            n_pos = u == kNone ? kNone : unit_lo(u);
-            n_end = u == kNone ? kNone : unit_hi(u);
-            if (!((dead >> qg) & 1u)) pending = atomicAdd(q, 1u);
+            if (u == kNone) return kNone;
+            c_pos = unit_lo(u);
+            c_end = unit_hi(u);
         }
         return tile_at(c_pos++);
     };
@@ -537,16 +552,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         if (u0 < nunits) {   // static first unit
             c_pos = unit_lo(u0);
             c_end = unit_hi(u0);
-            uint32_t u1 = slot_of(qg, atomicAdd(q, 1u));
-            if (u1 == kNone) {
-                dead |= 1u << qg;
-                u1 = steal();
-            }
-            n_pos = u1 == kNone ? kNone : unit_lo(u1);
-            n_end = u1 == kNone ? kNone : unit_hi(u1);
-            if (!((dead >> qg) & 1u)) pending = atomicAdd(q, 1u);
             tile = take_next();
-            next_tile = take_next();
         }
     }
     tile = __builtin_amdgcn_readfirstlane(tile);
@@ -603,8 +609,6 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         // advance the queue now (this tile's coordinates are already taken): the prefetched slot
         // becomes the next tile and the following slot is requested, hidden behind phases B/C
         const uint32_t this_tile = tile;
-        tile = __builtin_amdgcn_readfirstlane(next_tile);
-        if (tile != kNone && lane == 0) next_tile = take_next();
         uint32_t tile_work = 1;   // trace iterations of this tile (the schedule's cost)
 
         for (int f0 = 0; f0 < S; f0 += CH) {
@@ -721,6 +725,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 }
             }
             if (DEFER && qn > 0) drain(0, qn);
+            if (f0 + CH >= S && lane == 0) next_tile = take_next();   // the last chunk's pool is done
             // ---------------- phase C: progressive lerp in frame order ----------------
             DIAG_MARK(t_c);
             if (kind >= 0) {
@@ -745,6 +750,8 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             px[2 * cs] = acc.z;
         }
         if (job.cost && lane == 0) job.cost[this_tile] = tile_work;
+        if (S <= 0 && lane == 0) next_tile = take_next();   // no chunk ran (nframes 0)
+        tile = __builtin_amdgcn_readfirstlane(next_tile);
 #if PT_DIAG
         if (job.counters && lane == 0 && n_tiles_diag <= 32) {
             unsigned long long* tl = job.counters + 32 + 4 * 65536 + 96 * (size_t)(blockIdx.x * kWavesPerBlock + wv);
@@ -792,20 +799,21 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 #endif
 }
 
-// Kernel entry points.  The ambient kernel is held to 96 VGPRs (5 waves per SIMD; measured
-// 4 % faster than 4 waves at 106); the env-map kernel needs ~116 and runs at 4.
+// Kernel entry points.  The ambient kernel is held to 96 VGPRs (the 5-waves-per-SIMD budget, 3
+// spilled); its LDS keeps it at 4 waves per SIMD anyway, where the 128-VGPR build (no spills)
+// measures the same (PT_AMBIENT_WAVES=4).  The env-map kernel needs ~117 and runs at 4.
 #ifndef PT_AMBIENT_WAVES
 #define PT_AMBIENT_WAVES 5
 #endif
 template <int LAYOUT, bool COUNT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PT_AMBIENT_WAVES, PT_AMBIENT_WAVES))) void
+__global__ __launch_bounds__(64 * waves_per_block<false>()) __attribute__((amdgpu_waves_per_eu(PT_AMBIENT_WAVES, PT_AMBIENT_WAVES))) void
 pt_render_kernel(PtJob job)
 {
     render_body<LAYOUT, false, COUNT>(job);
 }
 
 template <int LAYOUT, bool COUNT>
-__global__ __launch_bounds__(256) void pt_render_env_kernel(PtJob job)
+__global__ __launch_bounds__(64 * waves_per_block<true>()) void pt_render_env_kernel(PtJob job)
 {
     render_body<LAYOUT, true, COUNT>(job);
 }
@@ -817,11 +825,15 @@ constexpr auto kernel_of()
     else return pt_render_kernel<LAYOUT, COUNT>;
 }
 
-// Persistent grid: as many 256-thread blocks as the device keeps resident (every wave then pulls
-// tiles until the queue is drained), capped by the tile count.  Blocks beyond residency would
-// only find an empty queue, so an over-estimate costs nothing but a launch slot.
+// Persistent grid: as many blocks as the device keeps resident (every wave then pulls tiles until
+// the queue is drained), capped by the tile count.  The count must be exact: a block beyond
+// residency starts only when a resident one ends, and its waves' static first units -- the most
+// expensive tiles of the schedule -- then run last (measured: 1024 of 5120 waves born 270-460 us
+// into a 470 us launch).  hipOccupancyMaxActiveBlocksPerMultiprocessor is capped here by the LDS
+// rule measured on gfx950: 1280-B allocation granules out of the CU's 160 KiB.
+constexpr int kLdsGranule = 1280;
 template <typename K>
-int resident_blocks(K kern)
+int resident_blocks(K kern, int threads)
 {
     struct Entry {
         const void* kern;
@@ -833,9 +845,17 @@ int resident_blocks(K kern)
     if (hipGetDevice(&dev) != hipSuccess) return 1024;
     for (int i = 0; i < used; ++i)
         if (cache[i].kern == (const void*)kern && cache[i].dev == dev) return cache[i].blocks;
-    int nb = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 256, 0) != hipSuccess || nb <= 0) nb = 4;
+    int nb = 0, cus = 0, lds_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, threads, 0) != hipSuccess || nb <= 0) nb = 4;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
+        lds_cu <= 0)
+        lds_cu = 160 * 1024;
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, (const void*)kern) == hipSuccess && fa.sharedSizeBytes > 0) {
+        const int granules = (int)((fa.sharedSizeBytes + kLdsGranule - 1) / kLdsGranule);
+        nb = std::min(nb, std::max(1, lds_cu / (granules * kLdsGranule)));
+    }
     if (used < 64) cache[used++] = Entry{(const void*)kern, dev, nb * cus};
     return nb * cus;
 }
@@ -843,17 +863,18 @@ int resident_blocks(K kern)
 template <int LAYOUT, bool ENV>
 hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 {
+    constexpr int wpb = waves_per_block<ENV>();
     const unsigned tiles = (unsigned)((job.ncols + 7) / 8) * (unsigned)((job.nrows + 7) / 8);
     hipError_t e = hipMemsetAsync(job.queue, 0, PT_QUEUE_WORDS * sizeof(unsigned), st);
     if (e != hipSuccess) return e;
     if (count) {
         auto k = kernel_of<LAYOUT, ENV, true>();
-        const unsigned blocks = (unsigned)std::min<long>(resident_blocks(k), (tiles + 3) / 4);
-        hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, job);
+        const unsigned blocks = (unsigned)std::min<long>(resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
+        hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
     } else {
         auto k = kernel_of<LAYOUT, ENV, false>();
-        const unsigned blocks = (unsigned)std::min<long>(resident_blocks(k), (tiles + 3) / 4);
-        hipLaunchKernelGGL(k, dim3(blocks), dim3(256), 0, st, job);
+        const unsigned blocks = (unsigned)std::min<long>(resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
+        hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
     }
     return hipGetLastError();
 }
@@ -865,7 +886,10 @@ hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 //       tiles -- expensive tiles are units of their own, cheap ones are dequeued in runs.  Built
 //       from the histogram alone (no per-tile prefix pass).
 constexpr int kCostBins = 1024;
-constexpr uint32_t kUnitCost = 12;
+#ifndef PT_UNIT_COST
+#define PT_UNIT_COST 12
+#endif
+constexpr uint32_t kUnitCost = PT_UNIT_COST;
 static_assert(kCostBins == 1024, "the schedule kernel scans one histogram bin per thread");
 
 // In-place exclusive scan of a[0..1023] by a 1024-thread workgroup (one entry per thread);

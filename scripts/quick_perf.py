@@ -34,4 +34,4 @@ print(json.dumps({"lib": __import__("os").environ.get("PT_MI355_LIB", "default")
                   "primary_samples_per_s": W * H * S / ms * 1e3, "ray_samples_per_s": W * H * S * B / ms * 1e3,
                   "segments_per_sample": cnt["segments"] / cnt["samples"],
                   "ref_segments_per_sample": (cnt["segments"] - cnt["primary"]) / cnt["samples"] + 1,
-                  "simd_eff": cnt["segments"] / cnt["lane_slots"], "counts": cnt, "count_launch_ms": count_ms}))
+                  "simd_eff": cnt["segments"] / max(1, cnt["lane_slots"]), "counts": cnt, "count_launch_ms": count_ms}))
