@@ -24,12 +24,23 @@ namespace {
 // built from them (longest tiles first) for the next launch on the same stream.  Per-pixel work
 // varies ~10x across the image (rays inside the box bounce, sky rays stop), and with the tiles
 // taken in raster order the last-dequeued expensive tiles left most of the chip idle at the end.
-struct Sched {
-    bool used = false;
-    hipStream_t stream = nullptr;
+// The geometry a schedule belongs to (which renderer, which pixels, how many bounces, which env).
+struct SchedKey {
+    int32_t kind = 0;   // 0: the diffuse kernels; 1 + env mode: v4
     int32_t width = 0, height = 0, col0 = 0, ncols = 0, row_start = 0, row_stride = 0, nrows = 0, bounces = 0;
     const float* env = nullptr;
     uint32_t ntiles = 0;
+    bool operator==(const SchedKey& o) const
+    {
+        return kind == o.kind && width == o.width && height == o.height && col0 == o.col0 && ncols == o.ncols &&
+               row_start == o.row_start && row_stride == o.row_stride && nrows == o.nrows && bounces == o.bounces &&
+               env == o.env && ntiles == o.ntiles;
+    }
+};
+struct Sched {
+    bool used = false;
+    hipStream_t stream = nullptr;
+    SchedKey key;
     uint32_t* cost = nullptr;
     uint32_t* order = nullptr;
     uint32_t* units = nullptr;    // ntiles + 2 words: run starts, then the run count
@@ -212,15 +223,47 @@ void free_sched(Sched& s)
     s = Sched{};
 }
 
-Sched* find_sched(const PtJob& j, hipStream_t st)
+SchedKey sched_key(const PtJob& j)
 {
-    const uint32_t n = pt_job_tiles(j);
+    SchedKey k;
+    k.kind = 0;
+    k.width = j.width;
+    k.height = j.height;
+    k.col0 = j.col0;
+    k.ncols = j.ncols;
+    k.row_start = j.row_start;
+    k.row_stride = j.row_stride;
+    k.nrows = j.nrows;
+    k.bounces = j.num_bounces;
+    k.env = j.env;
+    k.ntiles = pt_job_tiles(j);
+    return k;
+}
+
+SchedKey sched_key(const PtV4Job& j)
+{
+    SchedKey k;
+    k.kind = 1 + j.env_mode;
+    k.width = j.width;
+    k.height = j.height;
+    k.col0 = j.col0;
+    k.ncols = j.ncols;
+    k.row_start = j.row_start;
+    k.row_stride = j.row_stride;
+    k.nrows = j.nrows;
+    k.bounces = j.num_bounces;
+    k.env = j.env;
+    k.ntiles = (uint32_t)((j.ncols + 7) / 8) * (uint32_t)((j.nrows + 7) / 8);
+    return k;
+}
+
+Sched* find_sched(const SchedKey& key, hipStream_t st)
+{
+    const uint32_t n = key.ntiles;
     if (n < kSchedMinTiles) return nullptr;
     Sched* lru = &g.sched[0];
     for (Sched& s : g.sched) {
-        if (s.used && s.stream == st && s.width == j.width && s.height == j.height && s.col0 == j.col0 &&
-            s.ncols == j.ncols && s.row_start == j.row_start && s.row_stride == j.row_stride && s.nrows == j.nrows &&
-            s.bounces == j.num_bounces && s.env == j.env) {
+        if (s.used && s.stream == st && s.key == key) {
             s.last_use = ++g.sched_clock;
             return &s;
         }
@@ -238,42 +281,55 @@ Sched* find_sched(const PtJob& j, hipStream_t st)
     }
     s.used = true;
     s.stream = st;
-    s.width = j.width;
-    s.height = j.height;
-    s.col0 = j.col0;
-    s.ncols = j.ncols;
-    s.row_start = j.row_start;
-    s.row_stride = j.row_stride;
-    s.nrows = j.nrows;
-    s.bounces = j.num_bounces;
-    s.env = j.env;
-    s.ntiles = n;
+    s.key = key;
     s.last_use = ++g.sched_clock;
     *lru = s;
     return lru;
 }
 
-int launch(PtJob j, hipStream_t st, bool count)
+// The schedule and queue fields of a launch of geometry `key` on stream `st`.
+struct LaunchSched {
+    unsigned int* queue = nullptr;
+    const uint32_t* order = nullptr;
+    const uint32_t* units = nullptr;
+    const uint32_t* nunits = nullptr;
+    uint32_t* cost = nullptr;
+};
+int use_sched(const SchedKey& key, hipStream_t st, LaunchSched* ls)
 {
-    if (Sched* s = find_sched(j, st)) {
+    *ls = LaunchSched{};
+    if (Sched* s = find_sched(key, st)) {
         // (re)build the schedule from the last launch's costs on the 2nd launch of a geometry and
         // then every kSchedRebuild launches (the costs of a fixed view barely change; the builder
         // is a one-workgroup kernel of ~80 us)
         if (s->have_cost && (!s->built || s->launches % kSchedRebuild == 0)) {
-            hipError_t e = pt_launch_schedule(s->cost, s->order, s->units, s->units + s->ntiles + 1, s->ntiles, st);
+            hipError_t e = pt_launch_schedule(s->cost, s->order, s->units, s->units + s->key.ntiles + 1, s->key.ntiles, st);
             if (e != hipSuccess) return fail(PT_EHIP, "schedule launch failed: %s", hipGetErrorString(e));
             s->built = true;
         }
         if (s->built) {
-            j.order = s->order;
-            j.units = s->units;
-            j.nunits = s->units + s->ntiles + 1;
+            ls->order = s->order;
+            ls->units = s->units;
+            ls->nunits = s->units + s->key.ntiles + 1;
         }
-        j.cost = s->cost;
+        ls->cost = s->cost;
         s->have_cost = true;
         ++s->launches;
     }
-    j.queue = g.dqueue + (size_t)(g.queue_next++ % kQueueSlots) * PT_QUEUE_WORDS;
+    ls->queue = g.dqueue + (size_t)(g.queue_next++ % kQueueSlots) * PT_QUEUE_WORDS;
+    return PT_OK;
+}
+
+int launch(PtJob j, hipStream_t st, bool count)
+{
+    LaunchSched ls;
+    int rc;
+    if ((rc = use_sched(sched_key(j), st, &ls))) return rc;
+    j.queue = ls.queue;
+    j.order = ls.order;
+    j.units = ls.units;
+    j.nunits = ls.nunits;
+    j.cost = ls.cost;
     hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
     return PT_OK;
@@ -546,8 +602,16 @@ int v4_use_env(PtV4Job& j)
     return PT_OK;
 }
 
-int v4_launch(const PtV4Job& j, hipStream_t st, bool count)
+int v4_launch(PtV4Job j, hipStream_t st, bool count)
 {
+    LaunchSched ls;
+    int rc;
+    if ((rc = use_sched(sched_key(j), st, &ls))) return rc;
+    j.queue = ls.queue;
+    j.order = ls.order;
+    j.units = ls.units;
+    j.nunits = ls.nunits;
+    j.cost = ls.cost;
     hipError_t e = pt_launch_v4(j, g.v4scene, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "v4 render launch failed: %s", hipGetErrorString(e));
     return PT_OK;

@@ -40,6 +40,7 @@
 #define PT_IT_DIV(a, b) pt::div_guarded((a), (b))
 #define PT_IT_SQRT(x) pt::sqrt_guarded(x)
 #include "pt_invtrig.h"
+#include "pt_tile_queue.h"
 #include <math.h>
 #include <algorithm>
 
@@ -475,86 +476,11 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     unsigned long long n_tiles_diag = 0;
 #endif
 
-    // (built with the atomic optimizer off: a single-lane atomic needs no wave reduction, and its
-    // return value is then only waited for where it is used, at the next tile)
-    // Tile schedule.  The launch's work is a list of UNITS -- runs of tiles in schedule order
-    // (job.order: the previous launch's tiles sorted by descending cost, so the long tiles start
-    // first and the tail is made of short ones; job.units: run boundaries, each run worth about
-    // kUnitCost trace iterations, so a run of cheap sky tiles costs one dequeue, not dozens).
-    // Without a schedule every tile is a unit, in raster order.
-    // Units are dealt to PT_NQUEUES groups of blocks (block b -> group b % 8, the XCD it is
-    // dispatched to): group x owns unit slots x, x+8, ...  Each wave's first unit is static (its
-    // index in the group), later ones come from the group's own counter (one returning atomic per
-    // unit, issued when the last tile of the current unit has finished its pool); a group whose
-    // units are used up takes the others'.  One counter for the whole chip saturated (~90
-    // dequeues/us, MI355X_MICROARCH.md "dequeue").
-    constexpr uint32_t kNone = 0xffffffffu;
-    const uint32_t nunits = job.units ? *job.nunits : total_tiles;
-    const uint32_t ngroups = gridDim.x < PT_NQUEUES ? gridDim.x : PT_NQUEUES;   // small grids: fewer
-    const uint32_t qg = blockIdx.x % ngroups;
-    auto group_waves = [&](uint32_t g) { return ((gridDim.x - g + ngroups - 1) / ngroups) * kWavesPerBlock; };
-    auto slot_of = [&](uint32_t g, uint32_t c) {   // unit slot of dynamic position c of group g
-        const uint32_t slot = g + ngroups * (group_waves(g) + c);
-        return slot < nunits ? slot : kNone;
-    };
-    // Stealing happens only at the end of the launch, when thousands of waves run out at once and
-    // atomics on the counters queue up: a group found exhausted is remembered per wave, and a
-    // plain load of a counter screens it first (a counter only grows, so a load that shows it used
-    // up is right; without the screening the tail's atomics tripled the launch time).
-    uint32_t dead = 0;   // lane 0: groups known to be exhausted
-#ifndef PT_STEAL_SPREAD
-#define PT_STEAL_SPREAD 1
-#endif
-    // victims in a per-wave rotation, so the waves of a group that runs dry do not all queue on
-    // the same neighbour's counter
-    const uint32_t steal0 = PT_STEAL_SPREAD ? (blockIdx.x / ngroups) * kWavesPerBlock + (uint32_t)wv : 0u;
-    auto steal = [&]() {
-        for (uint32_t k = 1; k < ngroups; ++k) {
-            const uint32_t g = ngroups > 1 ? (qg + 1 + (steal0 + k - 1) % (ngroups - 1)) % ngroups : qg;
-            if ((dead >> g) & 1u) continue;
-            unsigned int* const c = job.queue + g * 32u;
-            if (slot_of(g, __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == kNone) {
-                dead |= 1u << g;
-                continue;
-            }
-            const uint32_t slot = slot_of(g, atomicAdd(c, 1u));
-            if (slot != kNone) return slot;
-            dead |= 1u << g;
-        }
-        return kNone;
-    };
-    auto unit_lo = [&](uint32_t u) { return job.units ? job.units[u] : u; };
-    auto unit_hi = [&](uint32_t u) { return job.units ? job.units[u + 1] : u + 1; };
-    auto tile_at = [&](uint32_t i) { return job.order ? job.order[i] : i; };
-    unsigned int* const q = job.queue + qg * 32u;
-    // lane 0: the current unit's remaining schedule positions [c_pos, c_end).  The next unit is
-    // claimed only when the current one is used up, after the pool of its last tile has drained
-    // (its returning atomic and schedule loads overlap that tile's phase C): a claim made earlier
-    // reserves a long tile for a wave that is still busy, and the longest-first order comes apart
-    // at the end of the launch.
-    uint32_t c_pos = kNone, c_end = kNone;
-    auto take_next = [&]() -> uint32_t {
-        if (c_pos == c_end) {
-            uint32_t u = ((dead >> qg) & 1u) ? kNone : slot_of(qg, atomicAdd(q, 1u));
-            if (u == kNone) {
-                dead |= 1u << qg;
-                u = steal();
-            }
-            if (u == kNone) return kNone;
-            c_pos = unit_lo(u);
-            c_end = unit_hi(u);
-        }
-        return tile_at(c_pos++);
-    };
+    // tiles from the launch's queue (pt_tile_queue.h)
+    constexpr uint32_t kNone = PtTileQueue<kWavesPerBlock>::kNone;
+    PtTileQueue<kWavesPerBlock> tq(job.queue, job.order, job.units, job.nunits, total_tiles, wv);
     uint32_t tile = kNone, next_tile = kNone;
-    if (lane == 0) {
-        const uint32_t u0 = qg + ngroups * ((blockIdx.x / ngroups) * kWavesPerBlock + (uint32_t)wv);
-        if (u0 < nunits) {   // static first unit
-            c_pos = unit_lo(u0);
-            c_end = unit_hi(u0);
-            tile = take_next();
-        }
-    }
+    if (lane == 0) tile = tq.first();
     tile = __builtin_amdgcn_readfirstlane(tile);
     while (tile != kNone) {
         const int tyi = (int)(tile / (uint32_t)tiles_x), txi = (int)(tile % (uint32_t)tiles_x);
@@ -725,7 +651,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 }
             }
             if (DEFER && qn > 0) drain(0, qn);
-            if (f0 + CH >= S && lane == 0) next_tile = take_next();   // the last chunk's pool is done
+            if (f0 + CH >= S && lane == 0) next_tile = tq.next();   // the last chunk's pool is done
             // ---------------- phase C: progressive lerp in frame order ----------------
             DIAG_MARK(t_c);
             if (kind >= 0) {
@@ -750,7 +676,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             px[2 * cs] = acc.z;
         }
         if (job.cost && lane == 0) job.cost[this_tile] = tile_work;
-        if (S <= 0 && lane == 0) next_tile = take_next();   // no chunk ran (nframes 0)
+        if (S <= 0 && lane == 0) next_tile = tq.next();   // no chunk ran (nframes 0)
         tile = __builtin_amdgcn_readfirstlane(next_tile);
 #if PT_DIAG
         if (job.counters && lane == 0 && n_tiles_diag <= 32) {
@@ -825,41 +751,6 @@ constexpr auto kernel_of()
     else return pt_render_kernel<LAYOUT, COUNT>;
 }
 
-// Persistent grid: as many blocks as the device keeps resident (every wave then pulls tiles until
-// the queue is drained), capped by the tile count.  The count must be exact: a block beyond
-// residency starts only when a resident one ends, and its waves' static first units -- the most
-// expensive tiles of the schedule -- then run last (measured: 1024 of 5120 waves born 270-460 us
-// into a 470 us launch).  hipOccupancyMaxActiveBlocksPerMultiprocessor is capped here by the LDS
-// rule measured on gfx950: 1280-B allocation granules out of the CU's 160 KiB.
-constexpr int kLdsGranule = 1280;
-template <typename K>
-int resident_blocks(K kern, int threads)
-{
-    struct Entry {
-        const void* kern;
-        int dev, blocks;
-    };
-    static Entry cache[64];   // (kernel, device) -> resident blocks; one entry per instantiation
-    static int used = 0;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 1024;
-    for (int i = 0; i < used; ++i)
-        if (cache[i].kern == (const void*)kern && cache[i].dev == dev) return cache[i].blocks;
-    int nb = 0, cus = 0, lds_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, threads, 0) != hipSuccess || nb <= 0) nb = 4;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
-        lds_cu <= 0)
-        lds_cu = 160 * 1024;
-    hipFuncAttributes fa{};
-    if (hipFuncGetAttributes(&fa, (const void*)kern) == hipSuccess && fa.sharedSizeBytes > 0) {
-        const int granules = (int)((fa.sharedSizeBytes + kLdsGranule - 1) / kLdsGranule);
-        nb = std::min(nb, std::max(1, lds_cu / (granules * kLdsGranule)));
-    }
-    if (used < 64) cache[used++] = Entry{(const void*)kern, dev, nb * cus};
-    return nb * cus;
-}
-
 template <int LAYOUT, bool ENV>
 hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 {
@@ -869,11 +760,11 @@ hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
     if (e != hipSuccess) return e;
     if (count) {
         auto k = kernel_of<LAYOUT, ENV, true>();
-        const unsigned blocks = (unsigned)std::min<long>(resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
+        const unsigned blocks = (unsigned)std::min<long>(pt_resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
         hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
     } else {
         auto k = kernel_of<LAYOUT, ENV, false>();
-        const unsigned blocks = (unsigned)std::min<long>(resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
+        const unsigned blocks = (unsigned)std::min<long>(pt_resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
         hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
     }
     return hipGetLastError();

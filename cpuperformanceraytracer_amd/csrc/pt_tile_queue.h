@@ -1,0 +1,144 @@
+// pt_tile_queue.h -- the tile queue of the persistent render kernels (pt_kernel.hip: the diffuse
+// renderers, pt_v4.hip: DemofoxRenderOptV4), and the resident-grid size they are launched with.
+//
+// The launch's work is a list of UNITS -- runs of 8x8 tiles in schedule order (order: the previous
+// launch's tiles sorted by descending cost, so the long tiles start first and the tail is made of
+// short ones; units: run boundaries, each run worth about kUnitCost pool iterations, so a run of
+// cheap sky tiles costs one dequeue, not dozens; pt_kernel.hip's pt_schedule_kernel builds both).
+// Without a schedule every tile is a unit, in raster order.
+//
+// Units are dealt to PT_NQUEUES groups of blocks (block b -> group b % 8, the XCD it is dispatched
+// to): group x owns unit slots x, x+8, ...  Each wave's first unit is static (its index in the
+// group); later ones come from the group's own counter, one returning atomic per unit, claimed
+// only when the current unit is used up -- the kernels call next() once the pool of the unit's last
+// tile has drained, so the atomic and the schedule loads overlap that tile's epilogue.  A claim
+// made earlier reserves a long tile for a wave that is still busy, and the longest-first order
+// comes apart at the end of the launch (claiming one and two units ahead, tiles of 23-26
+// iterations started 500 us into a launch while other waves ran sky tiles).  One counter for the
+// whole chip saturated (~90 dequeues/us, MI355X_MICROARCH.md "dequeue").
+//
+// A group whose units are used up takes the others'.  That happens only at the end of the launch,
+// when thousands of waves run out at once and atomics on the counters queue up: a group found
+// exhausted is remembered per wave, and a plain load of a counter screens it first (a counter
+// only grows, so a load that shows it used up is right; without the screening the tail's atomics
+// tripled the launch time).  Victims are visited in a per-wave rotation.
+//
+// All state is lane 0's (the kernels broadcast the tile with readfirstlane); the kernels are built
+// with the atomic optimizer off, so a single-lane atomic needs no wave reduction.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+
+#include "pt_kernel.h"   // PT_NQUEUES
+
+template <int WAVES_PER_BLOCK>
+struct PtTileQueue {
+    static constexpr uint32_t kNone = 0xffffffffu;
+    unsigned int* base;       // PT_NQUEUES counters, 128 B apart (zeroed before the launch)
+    const uint32_t* order;    // schedule position -> tile, or nullptr (raster order)
+    const uint32_t* units;    // unit -> first schedule position (units[u + 1] its end), or nullptr
+    uint32_t nunits, ngroups, qg, wave;
+    uint32_t dead = 0;        // groups known to be exhausted
+    uint32_t c_pos = kNone, c_end = kNone;   // the current unit's remaining schedule positions
+
+    __device__ PtTileQueue(unsigned int* queue, const uint32_t* order_, const uint32_t* units_,
+                           const uint32_t* nunits_, uint32_t total_tiles, int wv)
+        : base(queue), order(order_), units(units_)
+    {
+        nunits = units ? *nunits_ : total_tiles;
+        ngroups = gridDim.x < PT_NQUEUES ? gridDim.x : PT_NQUEUES;   // small grids: fewer groups
+        qg = blockIdx.x % ngroups;
+        wave = (blockIdx.x / ngroups) * WAVES_PER_BLOCK + (uint32_t)wv;   // index inside the group
+    }
+    __device__ uint32_t group_waves(uint32_t g) const
+    {
+        return ((gridDim.x - g + ngroups - 1) / ngroups) * WAVES_PER_BLOCK;
+    }
+    __device__ uint32_t slot_of(uint32_t g, uint32_t c) const   // unit slot of dynamic position c of group g
+    {
+        const uint32_t slot = g + ngroups * (group_waves(g) + c);
+        return slot < nunits ? slot : kNone;
+    }
+    __device__ uint32_t unit_lo(uint32_t u) const { return units ? units[u] : u; }
+    __device__ uint32_t unit_hi(uint32_t u) const { return units ? units[u + 1] : u + 1; }
+    __device__ uint32_t tile_at(uint32_t i) const { return order ? order[i] : i; }
+
+    __device__ uint32_t steal()
+    {
+        for (uint32_t k = 1; k < ngroups; ++k) {
+            const uint32_t g = (qg + 1 + (wave + k - 1) % (ngroups - 1)) % ngroups;
+            if ((dead >> g) & 1u) continue;
+            unsigned int* const c = base + g * 32u;
+            if (slot_of(g, __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == kNone) {
+                dead |= 1u << g;
+                continue;
+            }
+            const uint32_t slot = slot_of(g, atomicAdd(c, 1u));
+            if (slot != kNone) return slot;
+            dead |= 1u << g;
+        }
+        return kNone;
+    }
+    // the first tile of this wave's static unit, kNone if the launch has fewer units than waves
+    __device__ uint32_t first()
+    {
+        const uint32_t u0 = qg + ngroups * wave;
+        if (u0 >= nunits) return kNone;
+        c_pos = unit_lo(u0);
+        c_end = unit_hi(u0);
+        return next();
+    }
+    // the next tile: the current unit's, or the first of a newly claimed unit; kNone when every
+    // unit of every group has been taken
+    __device__ uint32_t next()
+    {
+        if (c_pos == c_end) {
+            uint32_t u = ((dead >> qg) & 1u) ? kNone : slot_of(qg, atomicAdd(base + qg * 32u, 1u));
+            if (u == kNone) {
+                dead |= 1u << qg;
+                u = steal();
+            }
+            if (u == kNone) return kNone;
+            c_pos = unit_lo(u);
+            c_end = unit_hi(u);
+        }
+        return tile_at(c_pos++);
+    }
+};
+
+// Blocks of `threads` threads of `kern` the device keeps resident: the grid of a persistent
+// launch.  It must be exact -- a block beyond residency starts only when a resident one ends, and
+// its waves' static first units (the most expensive tiles of the schedule) then run last
+// (measured: 1024 of 5120 waves born 270-460 us into a 470 us launch).
+// hipOccupancyMaxActiveBlocksPerMultiprocessor is capped by the LDS rule measured on gfx950
+// (scripts/lds_probe.hip): LDS is allocated in 1280-B granules of the CU's 160 KiB, which the API
+// does not model (it reports 5 blocks for 32001..32768 B, where 4 fit).
+constexpr int kPtLdsGranule = 1280;
+template <typename K>
+int pt_resident_blocks(K kern, int threads)
+{
+    struct Entry {
+        const void* kern;
+        int dev, blocks;
+    };
+    static Entry cache[64];   // (kernel, device) -> resident blocks; one entry per instantiation
+    static int used = 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 1024;
+    for (int i = 0; i < used; ++i)
+        if (cache[i].kern == (const void*)kern && cache[i].dev == dev) return cache[i].blocks;
+    int nb = 0, cus = 0, lds_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, threads, 0) != hipSuccess || nb <= 0) nb = 4;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
+        lds_cu <= 0)
+        lds_cu = 160 * 1024;
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, (const void*)kern) == hipSuccess && fa.sharedSizeBytes > 0) {
+        const int granules = (int)((fa.sharedSizeBytes + kPtLdsGranule - 1) / kPtLdsGranule);
+        nb = std::min(nb, std::max(1, lds_cu / (granules * kPtLdsGranule)));
+    }
+    if (used < 64) cache[used++] = Entry{(const void*)kern, dev, nb * cus};
+    return nb * cus;
+}

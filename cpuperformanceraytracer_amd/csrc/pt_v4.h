@@ -53,6 +53,12 @@ struct PtV4Job {
     int32_t env_w, env_h;
     unsigned long long* counters;   // COUNT launches: [0] segments, [1] samples, [2] escaped, [3] lane slots
     int32_t default_scene;          // the scene is InitializeScene's: literal-geometry instantiation
+    // persistent-grid tile queue and schedule (pt_tile_queue.h; as PtJob, pt_kernel.h)
+    unsigned int* queue;            // PT_QUEUE_WORDS words, zeroed on the stream before each launch
+    const uint32_t* order;          // tile schedule (longest first) or nullptr
+    const uint32_t* units;
+    const uint32_t* nunits;
+    uint32_t* cost;                 // per-tile cost written by this launch, or nullptr
 };
 
 // Scene description in AddQuad/Sphere/MaterialToScene order (v4 :1368-1401).

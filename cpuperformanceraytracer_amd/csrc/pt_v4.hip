@@ -27,6 +27,7 @@
 #define PT_IT_SQRT(x) pt::sqrt_guarded(x)
 #include "pt_invtrig.h"
 #include "pt_v4_default_scene.h"
+#include "pt_tile_queue.h"
 #include <algorithm>
 
 namespace {
@@ -421,15 +422,30 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int tiles_x = (job.ncols + 7) >> 3;
     const int ntiles = tiles_x * ((job.nrows + 7) >> 3);
-    const int tile = (int)blockIdx.x * kWaves + wv;   // raster order (reversed / 1-2 wave blocks measured slower)
-    if (tile >= ntiles) return;
-    const int tcol = (tile % tiles_x) * 8, trow = (tile / tiles_x) * 8;
     float* const col = s_col[wv];
+    const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;
+    const Tex tex{job.env, job.env_w, job.env_h};
+    const bool random = job.random_jitter != 0, rejection = job.rejection != 0;
+    const int B = job.num_bounces;
+    const float W = (float)job.width, H = (float)job.height;
+    const float rW = rcp(W), rH = rcp(H);
+    const float cam_dist = 1.0f;   // 1 / tanf(c_FOVDegrees * 0.5f * c_pi / 180.0f) == 1.0f exactly (InitializeCamera :1500)
+    unsigned long long n_seg = 0, n_esc = 0, n_slots = 0;
+
+    // persistent waves: 8x8 tiles from the launch's queue (pt_tile_queue.h), longest first when the
+    // geometry has a schedule
+    constexpr uint32_t kNone = PtTileQueue<kWaves>::kNone;
+    PtTileQueue<kWaves> tq(job.queue, job.order, job.units, job.nunits, (uint32_t)ntiles, wv);
+    uint32_t tile = kNone, next_tile = kNone;
+    if (lane == 0) tile = tq.first();
+    tile = __builtin_amdgcn_readfirstlane(tile);
+    while (tile != kNone) {
+    const int tcol = ((int)tile % tiles_x) * 8, trow = ((int)tile / tiles_x) * 8;
+    uint32_t tile_work = 1;   // pool iterations of this tile (the schedule's cost)
 
     // this lane's pixel (phase C) and its accumulator
     const int px = job.col0 + tcol + (lane & 7), pr = trow + (lane >> 3);
     const bool pvalid = (tcol + (lane & 7)) < job.ncols && pr < job.nrows;
-    const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;
     float* acc_p = nullptr;
     V3 acc = v3(0.0f, 0.0f, 0.0f);
     if (pvalid) {
@@ -438,13 +454,6 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
         acc_p = job.buf + out_index<LAYOUT>(job, px, orow);
         acc = v3(acc_p[0], acc_p[cs], acc_p[2 * cs]);
     }
-    const Tex tex{job.env, job.env_w, job.env_h};
-    const bool random = job.random_jitter != 0, rejection = job.rejection != 0;
-    const int B = job.num_bounces;
-    const float W = (float)job.width, H = (float)job.height;
-    const float rW = rcp(W), rH = rcp(H);
-    const float cam_dist = 1.0f;   // 1 / tanf(c_FOVDegrees * 0.5f * c_pi / 180.0f) == 1.0f exactly (InitializeCamera :1500)
-    unsigned long long n_seg = 0, n_esc = 0, n_slots = 0;
 
     for (int c0 = 0; c0 < job.nframes; c0 += kChunk) {
         const int nf = std::min(kChunk, job.nframes - c0);
@@ -506,6 +515,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
             }
             next += __builtin_popcountll(m);
             if (__ballot(item >= 0) == 0ull) break;
+            ++tile_work;
             if (COUNT) n_slots += 64;
             bool queued = false;   // DEFER: this lane's item missed and goes to the queue
             int qslot = 0;
@@ -654,6 +664,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
             }
         }
         if (DEFER && qn > 0) drain(qn);
+        if (c0 + kChunk >= job.nframes && lane == 0) next_tile = tq.next();   // the last pool is done
         // all radiance of this chunk is in LDS (written by lanes of this wave)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -669,10 +680,14 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    if (job.nframes <= 0 && lane == 0) next_tile = tq.next();   // no chunk ran
     if (pvalid) {
         acc_p[0] = acc.x;
         acc_p[cs] = acc.y;
         acc_p[2 * cs] = acc.z;
+    }
+    if (job.cost && lane == 0) job.cost[tile] = tile_work;
+    tile = __builtin_amdgcn_readfirstlane(next_tile);
     }
     if (COUNT) {
         // per-lane counts summed over the wave by lane 0's atomics
@@ -692,16 +707,22 @@ template <int ENV, int LAYOUT>
 hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool count)
 {
     const int tiles = ((j.ncols + 7) / 8) * ((j.nrows + 7) / 8);
-    const dim3 grid((unsigned)((tiles + kWaves - 1) / kWaves)), block(64 * kWaves);
+    const dim3 block(64 * kWaves);
+    hipError_t e = hipMemsetAsync(j.queue, 0, PT_QUEUE_WORDS * sizeof(unsigned), st);
+    if (e != hipSuccess) return e;
+    auto go = [&](auto kern) {   // persistent grid: the resident blocks, at most one tile per wave
+        const long blocks = std::min<long>(pt_resident_blocks(kern, 64 * kWaves), (tiles + kWaves - 1) / kWaves);
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), block, 0, st, j, sc);
+    };
 #ifndef PT_V4_FORCE_GENERIC
 #define PT_V4_FORCE_GENERIC 0   // A/B builds: the scene-table path even for the default scene
 #endif
     if (j.default_scene && !PT_V4_FORCE_GENERIC) {
-        if (count) hipLaunchKernelGGL((pt_v4_kernel<ENV, LAYOUT, true, true>), grid, block, 0, st, j, sc);
-        else hipLaunchKernelGGL((pt_v4_kernel<ENV, LAYOUT, false, true>), grid, block, 0, st, j, sc);
+        if (count) go(pt_v4_kernel<ENV, LAYOUT, true, true>);
+        else go(pt_v4_kernel<ENV, LAYOUT, false, true>);
     } else {
-        if (count) hipLaunchKernelGGL((pt_v4_kernel<ENV, LAYOUT, true, false>), grid, block, 0, st, j, sc);
-        else hipLaunchKernelGGL((pt_v4_kernel<ENV, LAYOUT, false, false>), grid, block, 0, st, j, sc);
+        if (count) go(pt_v4_kernel<ENV, LAYOUT, true, false>);
+        else go(pt_v4_kernel<ENV, LAYOUT, false, false>);
     }
     return hipGetLastError();
 }
@@ -725,6 +746,7 @@ hipError_t pt_launch_v4(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, b
     if (sc.nquads < 0 || sc.nspheres < 0 || sc.nquads + sc.nspheres > PT_V4_MAX_OBJECTS) return hipErrorInvalidValue;
     if (j.env_mode != PT_V4_ENV_NONE_ && (!j.env || j.env_w <= 0 || j.env_h <= 0)) return hipErrorInvalidValue;
     if (count && !j.counters) return hipErrorInvalidValue;
+    if (!j.queue || (j.order && (!j.units || !j.nunits))) return hipErrorInvalidValue;
     switch (j.env_mode) {
         case PT_V4_ENV_NONE_: return launch_env<PT_V4_ENV_NONE_>(j, sc, st, count);
         case PT_V4_ENV_EQUIRECT_: return launch_env<PT_V4_ENV_EQUIRECT_>(j, sc, st, count);
