@@ -48,17 +48,19 @@ constexpr int kChunk = PT_V4_CHUNK;   // frames per LDS chunk
 // cube-face pick) and texel gathers.  Evaluated where the miss happens it runs in most pool
 // iterations for a fraction of the lanes.  Deferred, the miss stores ret in its colour slot and
 // queues (env dir, rng, throughput, slot) in LDS; when the queue would overflow, all lanes
-// evaluate one queued miss each (the same fma on the same operands, bit for bit).  The queue is
-// drained before phase C.  kEnvQ entries of 32 B per wave keep the block within 32 KiB of LDS
-// (5 blocks per CU, the VGPR-bound occupancy of the env kernels).
-// Off by default: v4 paths are short, about 37 of 64 lanes miss per env evaluation already, and the
-// queue's LDS traffic costs more than the fuller drains save (1920x1080 x 8 spp, 8 bounces:
-// equirect 0.635 -> 0.646 ms, cubemap 0.542 -> 0.594 ms).  The diffuse+emissive env kernel of
-// pt_kernel.hip, whose misses are sparser, gains 13 % from the same scheme (PT_ENV_DEFER).
+// evaluate one queued miss each (the same fma on the same operands, bit for bit) -- or, when the
+// new misses outnumber the queue, those are evaluated at once.  The queue is drained before
+// phase C.  kEnvQ entries of 32 B per wave keep the block at 31 536 B of LDS, 25 of the 1280-B
+// granules, so 5 blocks per CU stay resident (the VGPR-bound occupancy; at 56 entries the block
+// needed 26 granules and dropped to 4 per CU, and the queue then measured slower).  1920x1080 x
+// 8 spp, 8 bounces: equirect 0.615 -> 0.561 ms, cubemap 0.525 -> 0.510 ms.
 #ifndef PT_V4_ENV_DEFER
-#define PT_V4_ENV_DEFER 0
+#define PT_V4_ENV_DEFER 1
 #endif
-constexpr int kEnvQ = 56;
+#ifndef PT_V4_ENV_Q
+#define PT_V4_ENV_Q 48
+#endif
+constexpr int kEnvQ = PT_V4_ENV_Q;
 
 struct V3 {
     float x, y, z;
