@@ -288,3 +288,25 @@ def test_v4_planar8_device_layout():
     got = planar8_to_interleaved(got.reshape(-1), 96, 40)
     ref = _oracle(96, 40, 3, env=env)
     assert bits_equal(got, ref), mismatch_report(got, ref)
+
+
+@pytest.mark.parametrize("env_mode", [N.PT_V4_ENV_EQUIRECT, N.PT_V4_ENV_CUBEMAP])
+def test_v4_scheduled_launches_match_oracle(env_mode):
+    """Persistent v4 waves take tiles from the shared queue (pt_tile_queue.h), longest first once
+    the geometry has costs: 20 progressive 1-frame launches -- unscheduled, scheduled, rebuilt at
+    the 16th -- through the deferred-miss queue equal the oracle bit for bit."""
+    import torch
+    from cpuperformanceraytracer_amd.device import ensure_backend, render_v4_device
+    ensure_backend(0)
+    w, h, k = 320, 192, 20   # 960 tiles: scheduled (>= 512)
+    cube = env_mode == N.PT_V4_ENV_CUBEMAP
+    env = _tex(6 * 16, 16, seed=31) if cube else _tex(64, 128, seed=31)
+    pt.v4_config(env_mode=env_mode)
+    pt.set_env_map(env)
+    buf = torch.zeros(h * w * 3, dtype=torch.float32, device="cuda:0")
+    for f in range(k):
+        render_v4_device(buf, w, h, frame_first=1 + f, nframes=1, use_env=True)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy().reshape(h, w, 3)
+    ref = _oracle(w, h, k, env=env, env_mode=po.ENV_CUBEMAP if cube else po.ENV_EQUIRECT)
+    assert bits_equal(got, ref), mismatch_report(got, ref)
