@@ -371,13 +371,16 @@ constexpr int kMaxWeights = 64;    // LDS table of the lerp weights 1/(iFrame+1)
 #ifndef PT_CHUNK
 #define PT_CHUNK 8
 #endif
+#ifndef PT_OWN_LAST
+#define PT_OWN_LAST 1
+#endif
 constexpr int kChunk = PT_CHUNK;   // frames per phase-B/C chunk (LDS colour slots per pixel)
 
 // Waves (8x8 tiles in flight) per workgroup.  LDS is allocated per workgroup in 1280-B granules
 // on gfx950 (measured, scripts/lds_probe.hip; hipOccupancyMaxActiveBlocksPerMultiprocessor does not
-// model it and over-reports 5 blocks for 32001..32768 B), so the 4-wave workgroup (32 720 B -> 26
-// granules) runs 4 per CU: 4 waves per SIMD, although the ambient kernel's 96 VGPRs would allow 5.
-// 5-wave workgroups (40 656 B -> 32 granules) were placed only 3 per CU (15 waves): slower.
+// model it and over-reports 5 blocks for 32001..32768 B): the ambient kernel's 4-wave workgroup
+// fits 5 per CU only with its LDS at <= 32 000 B (OWN_LAST below).  5-wave workgroups were placed
+// only 3 per CU (15 waves), 10-wave ones 1 per CU: slower.
 #ifndef PT_AMBIENT_BLOCK_WAVES
 #define PT_AMBIENT_BLOCK_WAVES 4
 #endif
@@ -418,7 +421,13 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     __shared__ AxisRow s_axis[PT_NQUADS * 3];
     __shared__ float s_w[kMaxWeights];
     constexpr int CH = kChunk;
-    __shared__ float s_col[kWavesPerBlock][64 * CH * 3];   // phase-B radiance per (pixel, frame)
+    // The last frame of a chunk is traced by the pixel's own lane (OWN_LAST): its radiance stays in
+    // that lane's registers, and the LDS holds CH - 1 frames per pixel -- 3 KiB less per block,
+    // which brings the ambient kernel to 29 648 B = 24 LDS granules and 5 blocks per CU (5 waves
+    // per SIMD, what its 96 VGPRs allow).  The env kernel (4 waves per SIMD by VGPRs) keeps CH.
+    constexpr bool OWN_LAST = !ENV && PT_OWN_LAST != 0 && CH > 1;
+    constexpr int CHS = OWN_LAST ? CH - 1 : CH;   // LDS colour slots per pixel
+    __shared__ float s_col[kWavesPerBlock][64 * CHS * 3];   // phase-B radiance per (pixel, frame)
     // per item pixel: P1.xyz + (id | lane << 8) and n1 (planar), 28 B
     __shared__ float4 s_rec[kWavesPerBlock][64];
     __shared__ float s_nrm[kWavesPerBlock][3][64];
@@ -541,13 +550,28 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             const int nf = S - f0 < CH ? S - f0 : CH;
             DIAG_ADD(0, t_tile);
             // ---------------- phase B: the pool of (pixel, frame) items ----------------
-            const int nitems = nh * nf;
+            const bool own = OWN_LAST && nf > 1;   // last frame traced by the pixel's lane
+            const int nitems = nh * (own ? nf - 1 : nf);   // pooled items: frame-major
             int next_item = 0;
             bool has_item = false, needs_dir = false;
             int it_lane = 0, it_f = 0;
             V3 P = zero, D = zero, T = zero, ret = zero, n = zero;
+            V3 c_last = zero;   // own: the radiance of this pixel's last frame
             uint32_t rng = 0;
             int bounce = 0;
+            if (own && kind == 2) {   // start with this pixel's own last-frame sample (bounce 0 done)
+                const PtLdsPrim pr = s_prim[id1];
+                rng = seed_of(fx, fy, (float)(job.frame_first + (uint32_t)(f0 + nf - 1)));   // :332
+                P = P1;
+                n = N1;
+                ret = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one));             // :319
+                T = mulv(one, v3(pr.ar, pr.ag, pr.ab));                          // :322
+                bounce = 1;
+                it_lane = lane;
+                it_f = nf - 1;
+                has_item = true;
+                needs_dir = true;
+            }
             int qn = 0;   // queued misses (DEFER), wave-uniform
             float4* const envq = s_envq[DEFER ? wv : 0];
             // evaluate the queued misses [q0, q0 + m) (m <= 64), one per lane, into their slots
@@ -628,10 +652,14 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                         needs_dir = !done;       // the direction after the last bounce is never used
                     }
                     if (done) {
-                        float* c = col_base + (it_lane * CH + it_f) * 3;
-                        c[0] = ret.x;
-                        c[1] = ret.y;
-                        c[2] = ret.z;
+                        if (own && it_f == nf - 1) {   // own item: it_lane == lane
+                            c_last = ret;
+                        } else {
+                            float* c = col_base + (it_lane * CHS + it_f) * 3;
+                            c[0] = ret.x;
+                            c[1] = ret.y;
+                            c[2] = ret.z;
+                        }
                         has_item = false;
                     }
                     DIAG_ADD(4, t_sh);
@@ -641,7 +669,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                     if (queued) {
                         const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
-                        envq[qn + r] = make_float4(D.x, D.y, D.z, __builtin_bit_cast(float, (it_lane * CH + it_f) * 3));
+                        envq[qn + r] = make_float4(D.x, D.y, D.z, __builtin_bit_cast(float, (it_lane * CHS + it_f) * 3));
                     }
                     qn += __popcll(qm);
                     if (qn >= 64) {   // a full wave of misses: evaluate the last 64
@@ -658,8 +686,12 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 for (int fi = 0; fi < nf; ++fi) {
                     V3 c = c_const;
                     if (kind == 2) {
-                        const float* cp = col_base + (lane * CH + fi) * 3;
-                        c = v3(cp[0], cp[1], cp[2]);
+                        if (own && fi == nf - 1) {
+                            c = c_last;
+                        } else {
+                            const float* cp = col_base + (lane * CHS + fi) * 3;
+                            c = v3(cp[0], cp[1], cp[2]);
+                        }
                     }
                     // color = 0 + c * (1/1) (:355-356); lerp(last, color, 1/(iFrame+1)) (:812)
                     const V3 colr = v3(0.0f + c.x * 1.0f, 0.0f + c.y * 1.0f, 0.0f + c.z * 1.0f);
@@ -725,9 +757,8 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 #endif
 }
 
-// Kernel entry points.  The ambient kernel is held to 96 VGPRs (the 5-waves-per-SIMD budget, 3
-// spilled); its LDS keeps it at 4 waves per SIMD anyway, where the 128-VGPR build (no spills)
-// measures the same (PT_AMBIENT_WAVES=4).  The env-map kernel needs ~117 and runs at 4.
+// Kernel entry points.  The ambient kernel is held to 96 VGPRs (the 5-waves-per-SIMD budget; 10
+// spilled); the env-map kernel needs ~117 and runs at 4.
 #ifndef PT_AMBIENT_WAVES
 #define PT_AMBIENT_WAVES 5
 #endif
