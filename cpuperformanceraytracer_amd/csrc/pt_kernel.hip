@@ -879,10 +879,21 @@ __global__ __launch_bounds__(1024) void pt_schedule_kernel(const uint32_t* __res
     ucnt[t] = (count + per - 1) / per;
     __syncthreads();
     const uint32_t total_units = block_exclusive_scan_1024(ucnt, wave_tot);
-    {
-        const uint32_t u0 = ucnt[t];
-        for (uint32_t j = 0, p = first_pos; p < first_pos + count; ++j, p += per) units[u0 + j] = p;
+    // unit u of bin b starts at schedule position hist[b] + (u - ucnt[b]) * per(b): every thread
+    // writes every 1024th unit, its bin found by binary search over the bins' first units (one
+    // thread per bin would write a whole large bin serially)
+    for (uint32_t u = t; u < total_units; u += nt) {
+        uint32_t lo = 0, hi = kCostBins - 1;   // the last bin whose first unit is <= u
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (ucnt[mid] <= u) lo = mid;
+            else hi = mid - 1;
+        }
+        const uint32_t cb = (uint32_t)(kCostBins - 1) - lo;
+        const uint32_t pb = cb >= kUnitCost || cb == 0 ? 1u : kUnitCost / cb;
+        units[u] = hist[lo] + (u - ucnt[lo]) * pb;
     }
+    __syncthreads();   // hist is advanced by the scatter below
     if (t == 0) {
         *nunits = total_units;
         units[total_units] = n;

@@ -38,7 +38,7 @@ struct PtTileQueue {
     unsigned int* base;       // PT_NQUEUES counters, 128 B apart (zeroed before the launch)
     const uint32_t* order;    // schedule position -> tile, or nullptr (raster order)
     const uint32_t* units;    // unit -> first schedule position (units[u + 1] its end), or nullptr
-    uint32_t nunits, ngroups, qg, wave;
+    uint32_t nunits, ntiles, ngroups, qg, wave;
     uint32_t dead = 0;        // groups known to be exhausted
     uint32_t c_pos = kNone, c_end = kNone;   // the current unit's remaining schedule positions
 
@@ -47,6 +47,7 @@ struct PtTileQueue {
         : base(queue), order(order_), units(units_)
     {
         nunits = units ? *nunits_ : total_tiles;
+        ntiles = total_tiles;
         ngroups = gridDim.x < PT_NQUEUES ? gridDim.x : PT_NQUEUES;   // small grids: fewer groups
         qg = blockIdx.x % ngroups;
         wave = (blockIdx.x / ngroups) * WAVES_PER_BLOCK + (uint32_t)wv;   // index inside the group
@@ -62,7 +63,12 @@ struct PtTileQueue {
     }
     __device__ uint32_t unit_lo(uint32_t u) const { return units ? units[u] : u; }
     __device__ uint32_t unit_hi(uint32_t u) const { return units ? units[u + 1] : u + 1; }
-    __device__ uint32_t tile_at(uint32_t i) const { return order ? order[i] : i; }
+    // (defensive: a schedule entry outside the launch's tiles ends the wave instead of faulting)
+    __device__ uint32_t tile_at(uint32_t i) const
+    {
+        const uint32_t tile = order ? order[i] : i;
+        return tile < ntiles ? tile : kNone;
+    }
 
     __device__ uint32_t steal()
     {
@@ -93,7 +99,7 @@ struct PtTileQueue {
     // unit of every group has been taken
     __device__ uint32_t next()
     {
-        if (c_pos == c_end) {
+        if (c_pos >= c_end) {
             uint32_t u = ((dead >> qg) & 1u) ? kNone : slot_of(qg, atomicAdd(base + qg * 32u, 1u));
             if (u == kNone) {
                 dead |= 1u << qg;
