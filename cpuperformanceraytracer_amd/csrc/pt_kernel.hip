@@ -355,6 +355,9 @@ __device__ __forceinline__ V3 miss_radiance(const PtJob& job, V3 amb, V3 d)
     return amb;
 }
 
+#ifndef PT_DIAG_WAVES_ONLY
+#define PT_DIAG_WAVES_ONLY 0   // diagnostic build: per-wave birth/death only (no per-tile timeline)
+#endif
 #ifndef PT_DIAG
 #define PT_DIAG 0   // diagnostic build: per-phase shader-clock cycles in counters[5..] (COUNT launches)
 #endif
@@ -494,9 +497,11 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     while (tile != kNone) {
         const int tyi = (int)(tile / (uint32_t)tiles_x), txi = (int)(tile % (uint32_t)tiles_x);
         DIAG_MARK(t_tile);
-#if PT_DIAG
+#if PT_DIAG && !PT_DIAG_WAVES_ONLY
         const unsigned long long r_tile0 = __builtin_amdgcn_s_memrealtime();
         const uint32_t diag_tile_id = tile;
+#endif
+#if PT_DIAG
         ++n_tiles_diag;
 #endif
         // ---------------- phase A: camera ray, once per pixel ----------------
@@ -710,7 +715,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         if (job.cost && lane == 0) job.cost[this_tile] = tile_work;
         if (S <= 0 && lane == 0) next_tile = tq.next();   // no chunk ran (nframes 0)
         tile = __builtin_amdgcn_readfirstlane(next_tile);
-#if PT_DIAG
+#if PT_DIAG && !PT_DIAG_WAVES_ONLY
         if (job.counters && lane == 0 && n_tiles_diag <= 32) {
             unsigned long long* tl = job.counters + 32 + 4 * 65536 + 96 * (size_t)(blockIdx.x * kWavesPerBlock + wv);
             tl[3 * (n_tiles_diag - 1) + 0] = r_tile0;
