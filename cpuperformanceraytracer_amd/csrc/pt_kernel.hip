@@ -876,8 +876,7 @@ __global__ __launch_bounds__(1024) void pt_schedule_kernel(const uint32_t* __res
     }
     __syncthreads();
     const uint32_t count = hist[t];   // bin t
-    block_exclusive_scan_1024(hist, wave_tot);
-    const uint32_t first_pos = hist[t];
+    block_exclusive_scan_1024(hist, wave_tot);   // hist[b]: the bin's first schedule position
     // units of bin t: cost c = kCostBins - 1 - t, k = max(1, U / c) tiles each
     const uint32_t c = (uint32_t)(kCostBins - 1) - t;
     const uint32_t per = c >= kUnitCost || c == 0 ? 1u : kUnitCost / c;
