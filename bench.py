@@ -10,9 +10,11 @@ diffuse+emissive.  One STEP = one launch that accumulates 8 more frames (8 spp) 
 HBM-resident f32 accumulator of every pixel -- bit-identical to 8 calls of the reference's
 DemofoxRenderScalar.  Frames advance step to step like the reference's progressive render.
 
-N > 1 (weak scaling): every rank renders its own 1920x1080 worth of rows of a 1920 x (1080*N)
-image (rows interleaved, shard.py); after the K steps the sub-images are gathered to rank 0 over
-RCCL (the job's only exchange, inside the timed region, also reported separately).
+N > 1 (weak scaling): the image grows to ~N x 1920x1080 pixels at the same aspect ratio (so the
+same view: sqrt(N) x 1920 by sqrt(N) x 1080, e.g. 3840x2160 for N = 4) and every rank renders
+its interleaved 1/N of the rows, ~1920x1080 pixels (shard.py); after the K steps the sub-images
+are gathered to rank 0 over RCCL (the job's only exchange, inside the timed region, also reported
+separately).
 
 Printed (rank 0, one JSON line): the BASELINE metric (ray-samples/s = pixels x spp x bounces / s),
 ms per step, a roofline object for the render kernel (algorithmic FP32 FLOP/s against the 157.3
@@ -23,6 +25,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -161,6 +164,19 @@ def load_traffic(workload: str):
     return d.get("hbm_bytes_per_launch"), d.get("source")
 
 
+def weak_image(W: int, H: int, world: int) -> tuple[int, int]:
+    """The global image of an N-rank weak-scaling run: W x H scaled by sqrt(N) in both directions
+    (width a multiple of 8), so it shows the same view at N times the pixels and every rank's
+    interleaved rows hold ~W x H pixels.  (Growing only the height would change the camera's aspect
+    ratio and with it what the rows see -- mostly sky for a tall image.)"""
+    if world == 1:
+        return W, H
+    s = math.sqrt(world)
+    Wg = max(8, int(round(W * s / 8.0)) * 8)
+    Hg = max(world, int(round(Wg * H / W)))
+    return Wg, Hg
+
+
 def measure_output_stage(buf, W: int, H: int, stream) -> dict:
     """the output stage (ACES + sRGB + 8-bit pack, v4 :1260-1331) on this
     rank's accumulator -- an HBM-bound pass: 12 B read + 4 B written per pixel."""
@@ -212,7 +228,7 @@ def main() -> None:
     torch.cuda.set_device(dev)
     wl = CONFIGS[args.workload]
     W, H, S, B = wl.width, wl.height, wl.spp, wl.num_bounces
-    Hg = H * world                                   # weak scaling: H rows per rank
+    Wg, Hg = weak_image(W, H, world)                 # weak scaling: ~W*H pixels per rank, same view
     row_start, row_stride, nrows = rows_of(rank, world, Hg)
     mr = max_rows(world, Hg)
     ensure_backend(dev.index, B)
@@ -225,12 +241,12 @@ def main() -> None:
         v4_config(num_bounces=B)   # the reference's default flags (equirect, random jitter, rejection)
     render_fn, count_fn = (render_v4_device, count_v4_device) if v4 else (render_device, count_device)
 
-    buf = torch.zeros(mr * W * 3, dtype=torch.float32, device=dev)
+    buf = torch.zeros(mr * Wg * 3, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     frame = 1
 
     def step(f):
-        render_fn(buf, W, Hg, frame_first=f, nframes=S, num_bounces=B, row_start=row_start,
+        render_fn(buf, Wg, Hg, frame_first=f, nframes=S, num_bounces=B, row_start=row_start,
                   row_stride=row_stride, nrows=nrows, use_env=wl.env, stream=stream)
 
     for _ in range(args.warmup):
@@ -254,7 +270,7 @@ def main() -> None:
         g0 = torch.cuda.Event(enable_timing=True)
         g1 = torch.cuda.Event(enable_timing=True)
         g0.record(stream)
-        full = gather_rows(buf, W, Hg, rank, world)
+        full = gather_rows(buf, Wg, Hg, rank, world)
         g1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -268,13 +284,13 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, gather_ms = float(t[0]), float(t[1])
         if rank == 0:
-            assert full is not None and full.shape == (Hg, W, 3)
+            assert full is not None and full.shape == (Hg, Wg, 3)
 
     # Exact work of the timed launches (deterministic: same frames, counted on a scratch buffer).
     scratch = torch.zeros_like(buf)
     segs = samples = slots = prim = escaped = 0
     for k in range(K):
-        c = count_fn(scratch, W, Hg, frame_first=timed_first + k * S, nframes=S, num_bounces=B,
+        c = count_fn(scratch, Wg, Hg, frame_first=timed_first + k * S, nframes=S, num_bounces=B,
                      row_start=row_start, row_stride=row_stride, nrows=nrows, use_env=wl.env, stream=stream)
         escaped += c["escaped"]
         segs += c["segments"]
@@ -283,14 +299,20 @@ def main() -> None:
         prim += c.get("primary", c["samples"])
     del scratch
 
-    output_stage = measure_output_stage(buf, W, H, stream) if rank == 0 else None
+    output_stage = None
+    if rank == 0:   # the presented 1080p frame of configs[1]: a W x H accumulator
+        acc = buf if world == 1 else torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
+        if world > 1:
+            n = min(acc.numel(), buf.numel())
+            acc[:n].copy_(buf[:n])
+        output_stage = measure_output_stage(acc, W, H, stream)
 
     if rank != 0:
         dist.destroy_process_group()
         return
 
     ms_step = elapsed * 1e3 / K
-    total_ray_samples = W * H * S * B * K * world
+    total_ray_samples = Wg * Hg * S * B * K
     value = total_ray_samples / elapsed
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
     if v4:   # every frame traces its own jittered camera ray: executed == reference work
@@ -325,9 +347,9 @@ def main() -> None:
             "; env map: 2048x1024 log-normal f32, seed 0xC0FFEE, standing in for the missing chinese_garden_2k.hdr"
             if wl.env else ""),
         "config": {"workload": wl.name, "width": W, "height": H, "spp": S, "bounces": B,
-                   "image_rows_total": Hg, "parallelism": f"rows interleaved x{world}" if world > 1 else "single GPU",
+                   "image": [Wg, Hg], "parallelism": f"rows interleaved x{world}" if world > 1 else "single GPU",
                    "step": f"one launch accumulating {S} frames (spp) of every pixel in HBM"},
-        "primary_samples_per_s": W * H * S * K * world / elapsed,
+        "primary_samples_per_s": Wg * Hg * S * K / elapsed,
         "ms_per_frame_1spp": ms_step / S,
         "traced_segments_per_s": segs * world / (avg_kernel_s * K),
         "segments_per_sample": segs / samples,
@@ -347,8 +369,8 @@ def main() -> None:
             "flop_model": flop_model,
             "flops_per_launch_ref_equivalent": flops_launch_ref,
             "achieved_ref_equivalent": flops_launch_ref / avg_kernel_s / 1e12,
-            "algorithmic_bytes_per_launch": RL.BYTES_PER_PIXEL_PER_LAUNCH * W * H + env_bytes,
-            "hbm_achieved_gbps": (RL.BYTES_PER_PIXEL_PER_LAUNCH * W * H + env_bytes) / avg_kernel_s / 1e9,
+            "algorithmic_bytes_per_launch": RL.BYTES_PER_PIXEL_PER_LAUNCH * Wg * nrows + env_bytes,
+            "hbm_achieved_gbps": (RL.BYTES_PER_PIXEL_PER_LAUNCH * Wg * nrows + env_bytes) / avg_kernel_s / 1e9,
             "hbm_peak_gbps": RL.PEAK_HBM_GBPS,
             "traffic_source": traffic_src,
         },
