@@ -221,10 +221,17 @@ def main() -> None:
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             sys.exit("run N>1 under torch.distributed.run (one process per GPU)")
+    # PT_BENCH_REHEARSE=1: rehearsal of the N-rank path on one GPU -- every rank on cuda:0, gloo
+    # instead of RCCL, the gather through host memory (correctness of the multi-rank code only;
+    # the numbers are not scaling numbers)
+    rehearse = world > 1 and os.environ.get("PT_BENCH_REHEARSE") == "1"
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 and not rehearse else 0)
     torch.cuda.set_device(dev)
     wl = CONFIGS[args.workload]
     W, H, S, B = wl.width, wl.height, wl.spp, wl.num_bounces
@@ -270,7 +277,7 @@ def main() -> None:
         g0 = torch.cuda.Event(enable_timing=True)
         g1 = torch.cuda.Event(enable_timing=True)
         g0.record(stream)
-        full = gather_rows(buf, Wg, Hg, rank, world)
+        full = gather_rows(buf.cpu() if rehearse else buf, Wg, Hg, rank, world)
         g1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -280,7 +287,7 @@ def main() -> None:
     kernel_ms = [a.elapsed_time(b) for a, b in ev]
     if world > 1:
         gather_ms = g0.elapsed_time(g1)
-        t = torch.tensor([elapsed, gather_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, gather_ms], dtype=torch.float64, device="cpu" if rehearse else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, gather_ms = float(t[0]), float(t[1])
         if rank == 0:
