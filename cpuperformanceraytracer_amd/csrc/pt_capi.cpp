@@ -53,7 +53,7 @@ constexpr int kSchedSlots = 16;
 constexpr int kBands = 4;   // PT_FLAG_PIN_HOST: row bands of a pipelined frame
 constexpr uint32_t kSchedMinTiles = 512;   // smaller jobs (e.g. one RenderTile) are not scheduled
 #ifndef PT_SCHED_REBUILD
-#define PT_SCHED_REBUILD 16
+#define PT_SCHED_REBUILD 64
 #endif
 constexpr unsigned long long kSchedRebuild = PT_SCHED_REBUILD;
 
@@ -301,7 +301,7 @@ int use_sched(const SchedKey& key, hipStream_t st, LaunchSched* ls)
     if (Sched* s = find_sched(key, st)) {
         // (re)build the schedule from the last launch's costs on the 2nd launch of a geometry and
         // then every kSchedRebuild launches (the costs of a fixed view barely change; the builder
-        // is a one-workgroup kernel of ~80 us)
+        // is a one-workgroup kernel of ~57 us at 1080p)
         if (s->have_cost && (!s->built || s->launches % kSchedRebuild == 0)) {
             hipError_t e = pt_launch_schedule(s->cost, s->order, s->units, s->units + s->key.ntiles + 1, s->key.ntiles, st);
             if (e != hipSuccess) return fail(PT_EHIP, "schedule launch failed: %s", hipGetErrorString(e));

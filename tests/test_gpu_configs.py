@@ -80,10 +80,10 @@ def test_config5_rank_shard_8k_256spp():
 
 def test_scheduled_launches_match_oracle():
     """The tile schedule (longest tiles first, built from the previous launches' costs and rebuilt
-    every 16 launches) changes only the order tiles are processed in: 20 progressive 1-frame
+    every 64 launches) changes only the order tiles are processed in: 66 progressive 1-frame
     launches of one geometry -- unscheduled, scheduled, rebuilt -- equal the oracle bit for bit."""
     import torch
-    W, H, B, K = 1280, 720, 8, 20
+    W, H, B, K = 1280, 720, 8, 66
     buf = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda:0")
     for k in range(K):
         _render(W, H, 1 + k, 1, B, buf=buf)

@@ -293,12 +293,12 @@ def test_v4_planar8_device_layout():
 @pytest.mark.parametrize("env_mode", [N.PT_V4_ENV_EQUIRECT, N.PT_V4_ENV_CUBEMAP])
 def test_v4_scheduled_launches_match_oracle(env_mode):
     """Persistent v4 waves take tiles from the shared queue (pt_tile_queue.h), longest first once
-    the geometry has costs: 20 progressive 1-frame launches -- unscheduled, scheduled, rebuilt at
-    the 16th -- through the deferred-miss queue equal the oracle bit for bit."""
+    the geometry has costs: 66 progressive 1-frame launches -- unscheduled, scheduled, rebuilt at
+    the 64th -- through the deferred-miss queue equal the oracle bit for bit."""
     import torch
     from cpuperformanceraytracer_amd.device import ensure_backend, render_v4_device
     ensure_backend(0)
-    w, h, k = 320, 192, 20   # 960 tiles: scheduled (>= 512)
+    w, h, k = 320, 192, 66   # 960 tiles: scheduled (>= 512)
     cube = env_mode == N.PT_V4_ENV_CUBEMAP
     env = _tex(6 * 16, 16, seed=31) if cube else _tex(64, 128, seed=31)
     pt.v4_config(env_mode=env_mode)
