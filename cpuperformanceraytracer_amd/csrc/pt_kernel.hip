@@ -377,6 +377,9 @@ constexpr int kMaxWeights = 64;    // LDS table of the lerp weights 1/(iFrame+1)
 #ifndef PT_OWN_LAST
 #define PT_OWN_LAST 1
 #endif
+#ifndef PT_PIXEL_MAJOR   // pool items in pixel-major order: a pixel's frames are taken by
+#define PT_PIXEL_MAJOR 1    // neighbouring lanes (same ray origin); 1-1.3 % faster than frame-major
+#endif
 constexpr int kChunk = PT_CHUNK;   // frames per phase-B/C chunk (LDS colour slots per pixel)
 
 // Waves (8x8 tiles in flight) per workgroup.  LDS is allocated per workgroup in 1280-B granules
@@ -598,9 +601,19 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                     const int k = next_item + rank;
                     const bool take = !has_item && k < nitems;
+#if PT_PIXEL_MAJOR   // A/B: consecutive items = the frames of one pixel (shared ray origin)
+                    const int npf = own ? nf - 1 : nf;   // pooled frames per pixel
+                    const int slot_pm = take ? k / npf : 0;
+                    const int fi = take ? k - slot_pm * npf : 0;
+#else
                     const int fi = take ? k / nh : 0;
+#endif
                     if (take) {
+#if PT_PIXEL_MAJOR
+                        const int slot = slot_pm;
+#else
                         const int slot = k - fi * nh;                 // the item's pixel record
+#endif
                         const float4 a0 = s_rec[wv][slot];
                         const int packed = __builtin_bit_cast(int, a0.w);
                         const int sId = packed & 0xff;
