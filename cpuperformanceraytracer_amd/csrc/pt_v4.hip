@@ -57,6 +57,9 @@ constexpr int kChunk = PT_V4_CHUNK;   // frames per LDS chunk
 #ifndef PT_V4_ENV_DEFER
 #define PT_V4_ENV_DEFER 1
 #endif
+#ifndef PT_V4_PIXEL_MAJOR   // A/B: pixel-major item order (1-2.5 % slower here, unlike the
+#define PT_V4_PIXEL_MAJOR 0    // diffuse kernel, where a pixel's frames share their bounce-0 origin)
+#endif
 #ifndef PT_V4_ENV_Q
 #define PT_V4_ENV_Q 48
 #endif
@@ -493,10 +496,14 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                 const int it = next + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                 if (it < total) {
+#if PT_V4_PIXEL_MAJOR   // a pixel's frames go to neighbouring lanes (close jittered camera rays)
+                    const int p = it / nf, f = it - p * nf;
+#else
                     const int p = it & 63, f = it >> 6;
+#endif
                     const int X = job.col0 + tcol + (p & 7), rb = trow + (p >> 3);
                     if ((tcol + (p & 7)) < job.ncols && rb < job.nrows) {
-                        item = it;
+                        item = f * 64 + p;   // colour slot order (phase C)
                         // mainImage :1092-1130
                         const int Y = job.row_start + rb * job.row_stride;
                         const uint32_t frame = job.frame_first + (uint32_t)(c0 + f);
