@@ -381,6 +381,7 @@ constexpr int kMaxWeights = 64;    // LDS table of the lerp weights 1/(iFrame+1)
 #define PT_PIXEL_MAJOR 1    // neighbouring lanes (same ray origin); 1-1.3 % faster than frame-major
 #endif
 constexpr int kChunk = PT_CHUNK;   // frames per phase-B/C chunk (LDS colour slots per pixel)
+static_assert(kChunk >= 1 && kChunk < 32, "the pool's k / npf multiply is exact for npf < 32");
 
 // Waves (8x8 tiles in flight) per workgroup.  LDS is allocated per workgroup in 1280-B granules
 // on gfx950 (measured, scripts/lds_probe.hip; hipOccupancyMaxActiveBlocksPerMultiprocessor does not
@@ -559,7 +560,9 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             DIAG_ADD(0, t_tile);
             // ---------------- phase B: the pool of (pixel, frame) items ----------------
             const bool own = OWN_LAST && nf > 1;   // last frame traced by the pixel's lane
-            const int nitems = nh * (own ? nf - 1 : nf);   // pooled items: frame-major
+            const int npf = own ? nf - 1 : nf;            // pooled frames per pixel
+            const int nitems = nh * npf;                  // pooled items
+            const uint32_t div_m = (65536u + (uint32_t)npf - 1u) / (uint32_t)npf;   // see the take
             int next_item = 0;
             bool has_item = false, needs_dir = false;
             int it_lane = 0, it_f = 0;
@@ -601,9 +604,10 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                     const int k = next_item + rank;
                     const bool take = !has_item && k < nitems;
-#if PT_PIXEL_MAJOR   // A/B: consecutive items = the frames of one pixel (shared ray origin)
-                    const int npf = own ? nf - 1 : nf;   // pooled frames per pixel
-                    const int slot_pm = take ? k / npf : 0;
+#if PT_PIXEL_MAJOR   // consecutive items = the frames of one pixel (shared ray origin)
+                    // k / npf as (k * ceil(2^16 / npf)) >> 16: exact for k < 64 npf, npf < 32 (the
+                    // error k (M - 2^16 / npf) / 2^16 < npf / 1024 stays below the 1/npf gap)
+                    const int slot_pm = take ? (int)(((uint32_t)k * div_m) >> 16) : 0;
                     const int fi = take ? k - slot_pm * npf : 0;
 #else
                     const int fi = take ? k / nh : 0;
