@@ -14,6 +14,11 @@ if ENV:
     set_env_map(synthetic_env(), 0, B)
 buf = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
 count_device(buf, W, H, frame_first=1, nframes=S, num_bounces=B, use_env=ENV)   # warm
+import os
+_t0 = time.perf_counter()   # device warm-up (clock ramp), as bench.py --device-warmup-ms
+while time.perf_counter() - _t0 < float(os.environ.get("PT_QP_WARM_S", "0.08")):
+    render_device(buf, W, H, frame_first=1, nframes=S, num_bounces=B, use_env=ENV)
+    torch.cuda.synchronize()
 c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 c0.record()
 cnt = count_device(buf, W, H, frame_first=1, nframes=S, num_bounces=B, use_env=ENV)
