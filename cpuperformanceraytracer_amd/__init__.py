@@ -39,6 +39,7 @@ from .renderer import (  # noqa: F401
     RenderTileInfo,
     get_frame,
     init,
+    initialized_device,
     make_tiles,
     readback,
     set_env_map,
@@ -46,6 +47,7 @@ from .renderer import (  # noqa: F401
     shutdown,
     texture,
     tonemap,
+    unpin_host,
     WriteImage,
 )
 
@@ -56,5 +58,5 @@ __all__ = [
     "DemofoxRenderOptV4", "InitializeGlobalRenderResources", "ReinitializeRenderTileData", "InitializeScene",
     "ClearScene", "AddMaterialToScene", "AddQuadObjectToScene", "AddSphereObjectToScene", "LoadCubemapTexture",
     "v4_config", "v4_begin_frame", "v4_get_frame", "v4_set_frame", "MakeWorkQueue", "AddWorkQueueEntry",
-    "CompleteAllWork", "WorkQueue",
+    "CompleteAllWork", "WorkQueue", "initialized_device", "unpin_host",
 ]

@@ -32,7 +32,7 @@ PT_PIXEL_XRGB8 = 1
 EXPORTED_SYMBOLS = (
     "pt_init", "pt_shutdown", "pt_last_error", "pt_default_config", "pt_set_frame", "pt_get_frame",
     "pt_render_scalar", "pt_render_simd", "pt_render_simd_tiled", "pt_render_tile", "pt_begin_frame",
-    "pt_readback", "pt_render_device", "pt_count_device",
+    "pt_readback", "pt_unpin_host", "pt_initialized_device", "pt_render_device", "pt_count_device",
     "pt_load_texture", "pt_decode_hdr", "pt_free_texture", "pt_set_env_map", "pt_render_simt_textured",
     "pt_tonemap", "pt_tonemap_device", "pt_write_bmp", "pt_load_cubemap_texture",
     "pt_v4_default_config", "pt_v4_set_config", "pt_v4_initialize_global_render_resources",
@@ -144,6 +144,8 @@ def load() -> ctypes.CDLL:
         "pt_render_tile": (i32, [ctypes.POINTER(PtBufferInfo), ctypes.POINTER(PtTileInfo)]),
         "pt_begin_frame": (i32, []),
         "pt_readback": (i32, [vp]),
+        "pt_unpin_host": (i32, [vp]),
+        "pt_initialized_device": (i32, []),
         "pt_render_device": (i32, [ctypes.POINTER(PtDeviceJob), vp]),
         "pt_count_device": (i32, [ctypes.POINTER(PtDeviceJob), vp, ctypes.POINTER(PtWorkCounts)]),
         "pt_load_texture": (i32, [ctypes.c_char_p, ctypes.POINTER(PtTexture)]),

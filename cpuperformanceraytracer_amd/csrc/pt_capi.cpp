@@ -52,6 +52,7 @@ struct Sched {
 constexpr int kSchedSlots = 16;
 constexpr int kBands = 4;   // PT_FLAG_PIN_HOST: row bands of a pipelined frame
 constexpr uint32_t kSchedMinTiles = 512;   // smaller jobs (e.g. one RenderTile) are not scheduled
+constexpr unsigned kQueueRing = 256;       // tile-queue ring slots (reuse across streams is event-ordered)
 #ifndef PT_SCHED_REBUILD
 #define PT_SCHED_REBUILD 64
 #endif
@@ -71,8 +72,12 @@ struct State {
     size_t mirror_bytes = 0;
     bool mirror_valid = false;          // deferred mode: device copy is authoritative
     unsigned long long* dcounters = nullptr;
-    unsigned int* dqueue = nullptr;     // ring of kQueueSlots tile-queue blocks (PT_QUEUE_WORDS each)
+    unsigned int* dqueue = nullptr;     // ring of kQueueRing tile-queue blocks (PT_QUEUE_WORDS each)
     unsigned queue_next = 0;
+    // per ring slot: the stream of the last launch that used it and an event recorded after that
+    // launch; a launch on another stream waits for it before re-zeroing the slot
+    hipStream_t queue_stream[kQueueRing] = {};
+    hipEvent_t queue_event[kQueueRing] = {};
     // env map in HBM (pt_set_env_map / pt_render_simt_textured)
     float* denv = nullptr;
     int32_t env_w = 0, env_h = 0;
@@ -122,7 +127,6 @@ int fail(int code, const char* fmt, ...)
     } while (0)
 
 constexpr uint32_t kMaxFrame = 1u << 24;   // iFrame is an f32 counter: exact below 2^24
-constexpr unsigned kQueueSlots = 256;      // launches in flight that may share the ring
 #if PT_DIAG
 constexpr int kCounterSlots = 32 + 4 * 65536 + 96 * 65536;   // + per-wave records, per-tile log
 #else
@@ -153,13 +157,30 @@ int ensure_dbuf(size_t bytes)
     return PT_OK;
 }
 
+// Deferred mode: a valid mirror is the only up-to-date copy of its host buffer's accumulation.
+// Before the mirror is given to another buffer it is written back to its own host buffer (as if
+// pt_readback had been called), so alternating buffers loses nothing.
+int flush_mirror()
+{
+    if (!g.mirror_valid || !g.dbuf || !g.mirror_host) {
+        g.mirror_valid = false;
+        return PT_OK;
+    }
+    HIP_TRY(hipMemcpyAsync((void*)g.mirror_host, g.dbuf, g.mirror_bytes, hipMemcpyDeviceToHost, g.stream));
+    HIP_TRY(hipStreamSynchronize(g.stream));
+    g.mirror_valid = false;
+    return PT_OK;
+}
+
 // Make the device mirror hold the host buffer [0, bytes).  In deferred mode an already valid
 // mirror of the same buffer is authoritative and nothing is copied.
 int stage_in(const float* host, size_t bytes, size_t off, size_t len)
 {
     const bool deferred = (g.cfg.flags & PT_FLAG_DEFER_READBACK) != 0;
-    if (g.mirror_host != host || g.mirror_bytes != bytes) g.mirror_valid = false;
-    int rc = ensure_dbuf(bytes);
+    int rc;
+    if (g.mirror_host != host || g.mirror_bytes != bytes)
+        if ((rc = flush_mirror())) return rc;
+    rc = ensure_dbuf(bytes);
     if (rc) return rc;
     if (deferred && g.mirror_valid) return PT_OK;
     if (deferred) {   // first deferred touch: the whole buffer becomes device-resident
@@ -289,6 +310,7 @@ Sched* find_sched(const SchedKey& key, hipStream_t st)
 
 // The schedule and queue fields of a launch of geometry `key` on stream `st`.
 struct LaunchSched {
+    unsigned slot = 0;   // tile-queue ring slot (queue_done after the launch)
     unsigned int* queue = nullptr;
     const uint32_t* order = nullptr;
     const uint32_t* units = nullptr;
@@ -316,7 +338,21 @@ int use_sched(const SchedKey& key, hipStream_t st, LaunchSched* ls)
         s->have_cost = true;
         ++s->launches;
     }
-    ls->queue = g.dqueue + (size_t)(g.queue_next++ % kQueueSlots) * PT_QUEUE_WORDS;
+    // The slot is re-zeroed by this launch (a memset on `st`).  Launches on one stream are
+    // ordered; when the slot's previous user ran on another stream, wait for its event first.
+    ls->slot = g.queue_next++ % kQueueRing;
+    if (g.queue_event[ls->slot] && g.queue_stream[ls->slot] != st)
+        HIP_TRY(hipStreamWaitEvent(st, g.queue_event[ls->slot], 0));
+    ls->queue = g.dqueue + (size_t)ls->slot * PT_QUEUE_WORDS;
+    return PT_OK;
+}
+
+// After the launch that used ring slot `slot` was enqueued on `st`.
+int queue_done(unsigned slot, hipStream_t st)
+{
+    if (!g.queue_event[slot]) HIP_TRY(hipEventCreateWithFlags(&g.queue_event[slot], hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(g.queue_event[slot], st));
+    g.queue_stream[slot] = st;
     return PT_OK;
 }
 
@@ -332,7 +368,7 @@ int launch(PtJob j, hipStream_t st, bool count)
     j.cost = ls.cost;
     hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
-    return PT_OK;
+    return queue_done(ls.slot, st);
 }
 
 void unpin()
@@ -345,9 +381,28 @@ void unpin()
     g.pinned_bytes = 0;
 }
 
+// Is the cached registration of `p` still the live one?  A buffer freed and reallocated at the
+// same address (common with numpy) is no longer page-locked by our registration: the runtime then
+// no longer reports `p` as registered host memory, and the buffer is registered afresh.
+bool pin_is_live(const float* p)
+{
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost && a.hostPointer == (void*)p;
+}
+
 bool pin(const float* p, size_t bytes)
 {
-    if (g.pinned == p && g.pinned_bytes == bytes) return true;
+    if (g.pinned == p && g.pinned_bytes == bytes && pin_is_live(p)) return true;
+    if (g.pinned == p) {   // stale registration of a freed buffer: forget it without unregistering
+        (void)hipHostUnregister((void*)p);
+        (void)hipGetLastError();
+        g.pinned = nullptr;
+        g.pinned_bytes = 0;
+    }
     unpin();
     if (hipHostRegister((void*)p, bytes, hipHostRegisterDefault) != hipSuccess) {
         (void)hipGetLastError();
@@ -614,7 +669,7 @@ int v4_launch(PtV4Job j, hipStream_t st, bool count)
     j.cost = ls.cost;
     hipError_t e = pt_launch_v4(j, g.v4scene, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "v4 render launch failed: %s", hipGetErrorString(e));
-    return PT_OK;
+    return queue_done(ls.slot, st);
 }
 
 }  // namespace
@@ -663,7 +718,7 @@ int pt_init(const pt_config* cfg)
     }
     if (hipMalloc(&g.dcounters, kCounterSlots * sizeof(unsigned long long)) != hipSuccess)
         return fail(PT_ENOMEM, "hipMalloc(counters) failed");
-    if (hipMalloc(&g.dqueue, (size_t)kQueueSlots * PT_QUEUE_WORDS * sizeof(unsigned)) != hipSuccess)
+    if (hipMalloc(&g.dqueue, (size_t)kQueueRing * PT_QUEUE_WORDS * sizeof(unsigned)) != hipSuccess)
         return fail(PT_ENOMEM, "hipMalloc(queue) failed");
     g.cfg = c;
     pt_build_demofox_scene(&g.scene, c.ambient);
@@ -688,6 +743,8 @@ void pt_shutdown(void)
     if (g.dtone_out) (void)hipFree(g.dtone_out);
     for (Sched& sc : g.sched)
         if (sc.used) free_sched(sc);
+    for (hipEvent_t& e : g.queue_event)
+        if (e) (void)hipEventDestroy(e);
     unpin();
     for (int k = 0; k < kBands; ++k) {
         if (g.ev_in[k]) (void)hipEventDestroy(g.ev_in[k]);
@@ -973,7 +1030,23 @@ int pt_v4_initialize_global_render_resources(void)
     return v4_ensure_scene();
 }
 
-int pt_v4_reinitialize_render_tile_data(void) { return PT_OK; }
+int pt_v4_reinitialize_render_tile_data(void)
+{
+    // Resize reallocated the render target (Application.cpp:142-154): the old buffer's page-lock
+    // must not outlive it
+    if (g.inited) unpin();
+    return PT_OK;
+}
+
+int32_t pt_initialized_device(void) { return g.inited ? g.cfg.device : -1; }
+
+int pt_unpin_host(const void* buf)
+{
+    if (!g.inited || !g.pinned) return PT_OK;
+    if (buf && buf != (const void*)g.pinned) return PT_OK;
+    unpin();
+    return PT_OK;
+}
 
 int pt_v4_initialize_scene(void)
 {

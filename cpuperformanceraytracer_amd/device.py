@@ -9,17 +9,27 @@ import ctypes
 
 from . import _native as N
 
-_backend_device = None
-
 
 def ensure_backend(device_index: int, num_bounces: int = 4) -> None:
-    """Initialise libpt_mi355 on `device_index` (the torch device of this rank)."""
-    global _backend_device
-    if _backend_device == device_index:
+    """Initialise libpt_mi355 on `device_index` (the torch device of this rank) if it is not
+    initialised yet.  The library state (env map, schedules, pinned buffer, frame counters) is per
+    process and lives on one device: a job on another device raises PtError(PT_ESTATE) instead of
+    silently re-initialising (one process per GPU, as bench.py and shard.py run).  The caller's
+    current HIP device is restored after an initialisation."""
+    from . import renderer
+    cur = renderer.initialized_device()
+    if cur == device_index:
         return
-    from .renderer import init
-    init(num_bounces=num_bounces, device=device_index)
-    _backend_device = device_index
+    if cur is not None:
+        raise N.PtError(N.PT_ESTATE, "ensure_backend",
+                        f"libpt_mi355 is initialised on device {cur}; a job on device {device_index} needs "
+                        "its own process (or renderer.shutdown() first)")
+    import torch
+    prev = torch.cuda.current_device()
+    try:
+        renderer.init(num_bounces=num_bounces, device=device_index)
+    finally:
+        torch.cuda.set_device(prev)
 
 
 def set_env_map(env, device_index: int = 0, num_bounces: int = 4) -> None:

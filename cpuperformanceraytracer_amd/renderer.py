@@ -22,11 +22,42 @@ settings raise PtError (the reference __debugbreak()s, Application.cpp:36-94).
 from __future__ import annotations
 
 import ctypes
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
 
 from . import _native as N
+
+_pin_host = False      # the library was initialised with PT_FLAG_PIN_HOST
+_pin_watch = {}        # (id(owner), ptr) -> weakref.finalize dropping the page-lock of ptr
+
+
+def _unpin_ptr(ptr: int) -> None:
+    try:
+        N.load().pt_unpin_host(ctypes.c_void_p(ptr))
+    except Exception:   # interpreter shutdown
+        pass
+
+
+def _watch_pinned(a: np.ndarray) -> None:
+    """PT_FLAG_PIN_HOST: the library page-locks the frame buffer and keeps it locked across calls.
+    When the array that owns the memory is released (a Resize reallocating the render target,
+    Application.cpp:142-151), drop that page-lock before numpy can hand the address out again."""
+    owner = a
+    while isinstance(owner.base, np.ndarray):
+        owner = owner.base
+    ptr = a.ctypes.data
+    key = (id(owner), ptr)
+    f = _pin_watch.get(key)
+    if f is not None and f.alive:
+        return
+    for k in [k for k, v in _pin_watch.items() if not v.alive]:
+        del _pin_watch[k]
+    try:
+        _pin_watch[key] = weakref.finalize(owner, _unpin_ptr, ptr)
+    except TypeError:   # memory owned by an object without weakref support: unpinned at shutdown
+        pass
 
 
 def _buf(a: np.ndarray, width: int, height: int, num_channels: int) -> int:
@@ -36,6 +67,8 @@ def _buf(a: np.ndarray, width: int, height: int, num_channels: int) -> int:
         raise N.PtError(N.PT_EINVAL, "buffer", "BufferOut must be writeable")
     if width > 0 and height > 0 and num_channels > 0 and a.size < width * height * num_channels:
         raise N.PtError(N.PT_EINVAL, "buffer", f"BufferOut holds {a.size} floats < {width}x{height}x{num_channels}")
+    if _pin_host:
+        _watch_pinned(a)
     return a.ctypes.data
 
 
@@ -54,11 +87,28 @@ def init(num_bounces: int = 4, samples_per_frame: int = 1, ambient=(0.1, 0.1, 0.
     c.flags = (N.PT_FLAG_DEFER_READBACK if defer_readback else 0) | (N.PT_FLAG_PIN_HOST if pin_host else 0)
     for i in range(3):
         c.ambient[i] = float(ambient[i])
+    global _pin_host
+    _pin_host = False
     N.check(L.pt_init(ctypes.byref(c)), "pt_init")
+    _pin_host = bool(pin_host)
 
 
 def shutdown() -> None:
+    global _pin_host
     N.load().pt_shutdown()
+    _pin_host = False
+
+
+def initialized_device() -> int | None:
+    """The HIP device the library state lives on (None before init)."""
+    d = int(N.load().pt_initialized_device())
+    return None if d < 0 else d
+
+
+def unpin_host(BufferOut: np.ndarray | None = None) -> None:
+    """pin_host mode: drop the page-lock of BufferOut (None: of any pinned buffer) before freeing it."""
+    ptr = None if BufferOut is None else ctypes.c_void_p(BufferOut.ctypes.data)
+    N.check(N.load().pt_unpin_host(ptr), "pt_unpin_host")
 
 
 def set_frame(frame: int) -> None:
@@ -330,7 +380,8 @@ def InitializeGlobalRenderResources() -> None:
 
 
 def ReinitializeRenderTileData() -> None:
-    """v4 :1723-1726 (accepted; every call uses its own arguments)."""
+    """v4 :1723-1726, called by the host's Resize (Application.cpp:154) after reallocating the render
+    target: drops the pin_host page-lock of the old buffer (every call uses its own arguments)."""
     N.check(N.load().pt_v4_reinitialize_render_tile_data(), "ReinitializeRenderTileData")
 
 

@@ -36,10 +36,14 @@ extern "C" {
 #define PT_LAYOUT_TILED_PLANAR8 2  /* RenderTile (simd_tiled.cpp:499-531): tile-major, planar8 rows   */
 
 #define PT_FLAG_DEFER_READBACK 1u  /* keep the accumulator in HBM between frame calls: no H2D/D2H;    */
-                                   /* the host buffer is refreshed only by pt_readback().            */
+                                   /* the host buffer is refreshed by pt_readback(), or written back */
+                                   /* automatically when a call names a different buffer (the device */
+                                   /* mirror holds one buffer at a time).  pt_shutdown discards it.  */
 #define PT_FLAG_PIN_HOST 2u        /* page-lock the caller's frame buffer (hipHostRegister; kept until */
-                                   /* pt_shutdown or another buffer is passed) and overlap its PCIe  */
-                                   /* transfers with rendering, in row bands (same results).         */
+                                   /* pt_unpin_host, pt_shutdown, ReinitializeRenderTileData or      */
+                                   /* another buffer is passed) and overlap its PCIe transfers with  */
+                                   /* rendering, in row bands (same results).  Free a pinned buffer  */
+                                   /* only after pt_unpin_host(buf) (a Resize that reallocates it).  */
 
 /* Runtime form of the reference's compile-time configuration (global_preprocessor_flags.h and the
  * file-scope constants of demofox_path_tracing_scalar.cpp:6-25). */
@@ -119,6 +123,12 @@ int pt_render_tile(const pt_buffer_info* buffer, const pt_tile_info* tile);
 int pt_begin_frame(void);
 /* PT_FLAG_DEFER_READBACK: copy the device accumulator of `buf` back into it */
 int pt_readback(float* buf);
+/* PT_FLAG_PIN_HOST: drop the page-lock of `buf` (NULL: of whichever buffer is pinned) before the
+ * caller frees or reallocates it (Application.cpp:142-151 Resize).  No-op if it is not pinned. */
+int pt_unpin_host(const void* buf);
+/* the HIP device the library state lives on, or -1 before pt_init (library state is per process
+ * and per device: a job on another device is an error, not a re-initialisation) */
+int32_t pt_initialized_device(void);
 
 /* --- env map (config 4: miss radiance = EquirectangularTextureSample, texture.cpp:101-139) ----- */
 /* replaces LoadTexture, asset_loading.cpp:9-16 (Radiance RGBE .hdr, flipped vertically) */
@@ -184,8 +194,9 @@ void pt_v4_default_config(pt_v4_config* cfg);
 int pt_v4_set_config(const pt_v4_config* cfg);
 /* InitializeGlobalRenderResources (v4 :1640-1661): camera + InitializeScene on first use */
 int pt_v4_initialize_global_render_resources(void);
-/* ReinitializeRenderTileData (v4 :1723-1726); accepted for the call surface -- every
- * pt_render_opt_v4 call uses its own arguments */
+/* ReinitializeRenderTileData (v4 :1723-1726), called by the host's Resize (Application.cpp:154)
+ * after it reallocated the render target: drops the PT_FLAG_PIN_HOST page-lock of the old buffer
+ * (every pt_render_opt_v4 call uses its own arguments) */
 int pt_v4_reinitialize_render_tile_data(void);
 /* scene editing: the reference's InitializeScene / AddMaterialToScene / AddQuadObjectToScene /
  * AddSphereObjectToScene (v4 :1403, :1368, :1390, :1397) plus an explicit clear.  Material i shades

@@ -1,0 +1,132 @@
+"""GPU tests of the boundary's buffer and stream state (round-1 review findings):
+
+* PT_FLAG_DEFER_READBACK with two alternating host buffers: the device mirror holds one buffer at a
+  time, and handing it to the other buffer first writes the old accumulation back (nothing lost);
+* PT_FLAG_PIN_HOST with the render target freed and reallocated between calls (numpy reuses the
+  address): the stale page-lock is dropped, every call still equals the oracle;
+* device jobs alternating between two HIP streams for more launches than the tile-queue ring has
+  slots: a slot reused across streams waits for its previous launch (event-ordered);
+* a device job on a device other than the initialised one is an error, not a silent re-init.
+All results bit-exact against the CPU oracle (oracle/pt_oracle.c).
+"""
+from __future__ import annotations
+
+import gc
+
+import numpy as np
+import pytest
+
+from conftest import bits_equal, mismatch_report
+from layouts import tiled_to_interleaved
+from oracle import pyoracle
+
+pytestmark = pytest.mark.gpu
+
+import cpuperformanceraytracer_amd as pt  # noqa: E402
+from cpuperformanceraytracer_amd import _native as N  # noqa: E402
+
+
+def test_deferred_alternating_buffers():
+    w, h, b = 200, 120, 8
+    pt.init(num_bounces=b, defer_readback=True)
+    a = np.zeros((h, w, 3), np.float32)
+    c = np.zeros((h, w, 3), np.float32)
+    ra = np.zeros_like(a)
+    rc = np.zeros_like(c)
+    rc_prev = None
+    for k in range(3):   # frames 1, 3, 5 -> a; 2, 4, 6 -> c (one global iFrame)
+        pt.DemofoxRenderScalar(a, w, h, 3)
+        pyoracle.render(w, h, frame_first=2 * k + 1, nframes=1, num_bounces=b, buf=ra)
+        pt.DemofoxRenderScalar(c, w, h, 3)
+        rc_prev = rc.copy()
+        pyoracle.render(w, h, frame_first=2 * k + 2, nframes=1, num_bounces=b, buf=rc)
+    # `a` was written back when `c` took the mirror; `c` holds what was written back when `a` took
+    # it for frame 5 (frames 2, 4); its frame 6 is still device-resident
+    assert bits_equal(a, ra), mismatch_report(a, ra)
+    assert bits_equal(c, rc_prev), mismatch_report(c, rc_prev)
+    with pytest.raises(N.PtError):
+        pt.readback(a)   # no longer the deferred buffer
+    pt.readback(c)
+    assert bits_equal(c, rc), mismatch_report(c, rc)
+    pt.shutdown()
+
+
+def test_deferred_work_queue_two_buffers():
+    """One work queue holding every tile of two buffers (the mirror switches inside run_queue)."""
+    w, h, tw, th = 160, 96, 32, 24
+    pt.init(num_bounces=4, defer_readback=True)
+    bufs = [np.zeros(w * h * 3, np.float32), np.zeros(w * h * 3, np.float32)]
+    q = pt.MakeWorkQueue(N.PT_RENDERER_SIMD_TILED)
+    pt.BeginFrame()
+    for buf in bufs:
+        info = pt.RenderBufferInfo(buf, w, h, 3)
+        for t in pt.make_tiles(w, h, w // tw, h // th):
+            pt.AddWorkQueueEntry(q, info, t)
+    pt.CompleteAllWork(q)
+    q.close()
+    ref = pyoracle.render(w, h, nframes=1, num_bounces=4)
+    assert bits_equal(tiled_to_interleaved(bufs[0], w, h, tw, th), ref)   # written back at the switch
+    pt.readback(bufs[1])
+    assert bits_equal(tiled_to_interleaved(bufs[1], w, h, tw, th), ref)
+    pt.shutdown()
+
+
+def test_pinned_buffer_reallocated_between_calls():
+    w, h, b = 640, 384, 8
+    pt.init(num_bounces=b, pin_host=True)
+    addrs = set()
+    for k in range(4):
+        a = np.zeros((h, w, 3), np.float32)   # a fresh zeroed render target (Resize)
+        addrs.add(a.ctypes.data)
+        pt.DemofoxRenderScalar(a, w, h, 3)    # frame k + 1 blended into zeros
+        ref = pyoracle.render(w, h, frame_first=k + 1, nframes=1, num_bounces=b)
+        assert bits_equal(a, ref), (k, mismatch_report(a, ref))
+        del a
+        gc.collect()
+    # explicit unpin before a free (the C++ host's Resize calls ReinitializeRenderTileData)
+    a = np.zeros((h, w, 3), np.float32)
+    pt.DemofoxRenderScalar(a, w, h, 3)
+    pt.unpin_host(a)
+    pt.ReinitializeRenderTileData()
+    pt.unpin_host(None)
+    pt.DemofoxRenderScalar(a, w, h, 3)        # re-pinned on use
+    ref = pyoracle.render(w, h, frame_first=5, nframes=2, num_bounces=b)
+    assert bits_equal(a, ref), mismatch_report(a, ref)
+    pt.shutdown()
+
+
+torch = pytest.importorskip("torch")
+
+
+def test_queue_ring_reuse_across_streams():
+    """600 launches alternating between two streams (> the 256-slot tile-queue ring)."""
+    from cpuperformanceraytracer_amd.device import render_device
+    pt.shutdown()
+    w, h, b, n = 96, 64, 4, 300
+    bufs = [torch.zeros(h * w * 3, dtype=torch.float32, device="cuda") for _ in range(2)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    for f in range(n):
+        for s, buf in zip(streams, bufs):
+            render_device(buf, w, h, frame_first=f + 1, nframes=1, num_bounces=b, stream=s)
+    torch.cuda.synchronize()
+    ref = pyoracle.render(w, h, nframes=n, num_bounces=b)
+    for buf in bufs:
+        got = buf.cpu().numpy().reshape(h, w, 3)
+        assert bits_equal(got, ref), mismatch_report(got, ref)
+
+
+def test_job_on_other_device_is_an_error():
+    from cpuperformanceraytracer_amd.device import ensure_backend
+    pt.shutdown()
+    ensure_backend(0)
+    assert pt.initialized_device() == 0
+    ensure_backend(0)   # no re-init: the frame counter survives
+    pt.set_frame(7)
+    ensure_backend(0)
+    assert pt.get_frame() == 7
+    with pytest.raises(N.PtError):
+        ensure_backend(1)
+    assert pt.initialized_device() == 0 and pt.get_frame() == 7
+    pt.shutdown()
+    assert pt.initialized_device() is None
