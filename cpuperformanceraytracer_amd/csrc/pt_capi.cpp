@@ -954,12 +954,16 @@ int pt_render_device(const pt_device_job* dj, void* stream)
     int rc;
     PtJob j;
     if ((rc = ensure_init()) || (rc = device_job(dj, &j))) return rc;
-#if PT_DIAG   // diagnostic build: every device launch records and dumps its timeline (synchronous)
+#if PT_DIAG   // diagnostic build: with PT_DIAG_OUT set, a device launch records and dumps its
+              // timeline (synchronous); without it launches run as usual (warm-up at full clocks)
+    if (!getenv("PT_DIAG_OUT")) return launch(j, (hipStream_t)stream, false);
     hipStream_t st = (hipStream_t)stream;
-    HIP_TRY(hipMemsetAsync(g.dcounters, 0, kCounterSlots * sizeof(unsigned long long), st));
+    const char* mode = getenv("PT_DIAG_MODE");   // experiment switches: "nomemset", "nocounters"
+    const bool nomemset = mode && !strcmp(mode, "nomemset"), nocounters = mode && !strcmp(mode, "nocounters");
+    HIP_TRY(hipMemsetAsync(g.dcounters, 0, (nomemset ? 32 + 4 * 65536 : kCounterSlots) * sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(g.dcounters + PT_CNT_N + 9, 0xff, sizeof(unsigned long long), st));
     HIP_TRY(hipMemsetAsync(g.dcounters + PT_CNT_N + 12, 0xff, sizeof(unsigned long long), st));
-    j.counters = g.dcounters;
+    j.counters = nocounters ? nullptr : g.dcounters;
     if ((rc = launch(j, st, false))) return rc;
     static unsigned long long h[kCounterSlots];
     HIP_TRY(hipMemcpyAsync(h, g.dcounters, sizeof(h), hipMemcpyDeviceToHost, st));

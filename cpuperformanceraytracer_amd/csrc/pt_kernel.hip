@@ -355,6 +355,21 @@ __device__ __forceinline__ V3 miss_radiance(const PtJob& job, V3 amb, V3 d)
     return amb;
 }
 
+#ifndef PT_PRIO
+#define PT_PRIO 0          // s_setprio by the tile's previous cost (PT_PRIO_T1..T3 thresholds)
+#endif
+#ifndef PT_PRIO_T1
+#define PT_PRIO_T1 24
+#endif
+#ifndef PT_PRIO_T2
+#define PT_PRIO_T2 36
+#endif
+#ifndef PT_PRIO_T3
+#define PT_PRIO_T3 46
+#endif
+#ifndef PT_DIAG_NOATOMIC
+#define PT_DIAG_NOATOMIC 0
+#endif
 #ifndef PT_DIAG_WAVES_ONLY
 #define PT_DIAG_WAVES_ONLY 0   // diagnostic build: per-wave birth/death only (no per-tile timeline)
 #endif
@@ -500,6 +515,18 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     tile = __builtin_amdgcn_readfirstlane(tile);
     while (tile != kNone) {
         const int tyi = (int)(tile / (uint32_t)tiles_x), txi = (int)(tile % (uint32_t)tiles_x);
+#if PT_PRIO
+        // issue priority by the tile's cost in the previous launch (the schedule's input): the
+        // longest tiles are the launch's critical path, and on their SIMD they take the issue
+        // slots first while the cheaper tiles' waves fill the gaps
+        if (job.order) {
+            const uint32_t c = job.cost[tile];
+            if (c >= (uint32_t)PT_PRIO_T3) __builtin_amdgcn_s_setprio(3);
+            else if (c >= (uint32_t)PT_PRIO_T2) __builtin_amdgcn_s_setprio(2);
+            else if (c >= (uint32_t)PT_PRIO_T1) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
         DIAG_MARK(t_tile);
 #if PT_DIAG && !PT_DIAG_WAVES_ONLY
         const unsigned long long r_tile0 = __builtin_amdgcn_s_memrealtime();
@@ -762,14 +789,16 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 #if PT_DIAG >= 2
             for (int k = 0; k < 7; ++k) atomicAdd(&job.counters[PT_CNT_N + k], dg[k]);
 #endif
+            const unsigned long long r_death = __builtin_amdgcn_s_memrealtime();
+#if !PT_DIAG_NOATOMIC   // (same-address atomics from every wave; the per-wave records suffice)
             const unsigned long long t_death = __builtin_amdgcn_s_memtime();
             atomicAdd(&job.counters[PT_CNT_N + 7], t_death - t_birth);      // wave lifetimes
-            const unsigned long long r_death = __builtin_amdgcn_s_memrealtime();
             atomicAdd(&job.counters[PT_CNT_N + 10], r_death - r_birth);      // 100 MHz ticks
             atomicMax(&job.counters[PT_CNT_N + 8], r_birth);                 // last wave start
             atomicMin(&job.counters[PT_CNT_N + 9], r_death);                 // first wave end
             atomicMax(&job.counters[PT_CNT_N + 11], r_death);                // last wave end
             atomicMin(&job.counters[PT_CNT_N + 12], r_birth);                // first wave start
+#endif
             unsigned long long* rec = job.counters + 32 + 4 * (size_t)(blockIdx.x * kWavesPerBlock + wv);
             rec[0] = r_birth;
             rec[1] = r_death;
@@ -830,10 +859,15 @@ hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 //       tiles -- expensive tiles are units of their own, cheap ones are dequeued in runs.  Built
 //       from the histogram alone (no per-tile prefix pass).
 constexpr int kCostBins = 1024;
+// The unit size adapts to the launch: the cheapest tiles (camera rays that miss: cost 1, ~4-6 us
+// each) come last, and at the end of a 1080p launch units of 12 of them left ~3600 of the 5120
+// waves idle while ~1500 ran 60-us units (per-tile timeline, scripts/diag_timeline.py).  Units
+// of ~tiles / (1.5 x waves) iterations, clamped to [2, 12]: 1080p 4 (c2 360 -> 353 us), 4K 12
+// (its 4x more cheap tiles keep every wave busy; 4 measured 1-2 % slower there).
 #ifndef PT_UNIT_COST
-#define PT_UNIT_COST 12
+#define PT_UNIT_COST 0   // 0: adaptive (above); else a fixed unit cost
 #endif
-constexpr uint32_t kUnitCost = PT_UNIT_COST;
+constexpr uint32_t kUnitCostMax = 12, kUnitCostMin = 2;
 static_assert(kCostBins == 1024, "the schedule kernel scans one histogram bin per thread");
 
 // In-place exclusive scan of a[0..1023] by a 1024-thread workgroup (one entry per thread);
@@ -868,7 +902,7 @@ __device__ uint32_t block_exclusive_scan_1024(uint32_t* a, uint32_t* wave_tot)
 
 __global__ __launch_bounds__(1024) void pt_schedule_kernel(const uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
                                                            uint32_t* __restrict__ units, uint32_t* __restrict__ nunits,
-                                                           uint32_t n)
+                                                           uint32_t n, uint32_t kUnitCost)
 {
     __shared__ uint32_t hist[kCostBins];    // tiles per bin, then the bin's first schedule position
     __shared__ uint32_t ucnt[kCostBins];    // units per bin, then the bin's first unit index
@@ -937,7 +971,17 @@ hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* u
 {
     if (ntiles == 0) return hipSuccess;
     if (!cost || !order || !units || !nunits) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(pt_schedule_kernel, dim3(1), dim3(1024), 0, st, cost, order, units, nunits, ntiles);
+    uint32_t unit_cost = PT_UNIT_COST;
+    if (unit_cost == 0) {   // adaptive: ~tiles / (1.5 x resident waves), 20 waves per CU
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        const uint32_t waves = (uint32_t)cus * 20u;
+        unit_cost = (uint32_t)((2ull * ntiles) / (3ull * waves));
+        unit_cost = std::min(kUnitCostMax, std::max(kUnitCostMin, unit_cost));
+    }
+    hipLaunchKernelGGL(pt_schedule_kernel, dim3(1), dim3(1024), 0, st, cost, order, units, nunits, ntiles, unit_cost);
     return hipGetLastError();
 }
 

@@ -3,7 +3,7 @@
 //
 // The launch's work is a list of UNITS -- runs of 8x8 tiles in schedule order (order: the previous
 // launch's tiles sorted by descending cost, so the long tiles start first and the tail is made of
-// short ones; units: run boundaries, each run worth about kUnitCost pool iterations, so a run of
+// short ones; units: run boundaries, each run worth about a unit cost of pool iterations (2-12, adaptive), so a run of
 // cheap sky tiles costs one dequeue, not dozens; pt_kernel.hip's pt_schedule_kernel builds both).
 // Without a schedule every tile is a unit, in raster order.
 //
