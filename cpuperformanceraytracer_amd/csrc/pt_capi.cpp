@@ -1000,6 +1000,7 @@ int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
     out->samples = h[PT_CNT_SAMPLES];
     out->escaped = h[PT_CNT_ESCAPED];
     out->primary = h[PT_CNT_PRIMARY];
+    out->quad_fallbacks = h[PT_CNT_FALLBACK];
     return PT_OK;
 }
 
@@ -1239,6 +1240,7 @@ int pt_v4_count_device(const pt_device_job* dj, void* stream, pt_work_counts* ou
     out->samples = (uint64_t)dj->width * (uint64_t)dj->nrows * (uint64_t)dj->nframes;
     out->escaped = h[2];
     out->primary = out->samples;   // one camera ray per sample (jittered)
+    out->quad_fallbacks = 0;
     return PT_OK;
 }
 

@@ -18,7 +18,8 @@ enum PtCounter : int {
     PT_CNT_SAMPLES = 2,      // primary samples finished
     PT_CNT_ESCAPED = 3,      // paths that ended on a miss
     PT_CNT_PRIMARY = 4,      // camera-ray segments traced (one per pixel)
-    PT_CNT_N = 5,
+    PT_CNT_FALLBACK = 5,     // segments whose culled quad stage ran the six exact tests
+    PT_CNT_N = 6,
 };
 
 struct PtJob {

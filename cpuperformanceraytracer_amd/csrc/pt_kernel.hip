@@ -84,6 +84,21 @@ __device__ __forceinline__ float rcp_x(float x)
 // comparisons (see quad_test) or cannot occur (camera: 0 <= a <= 2^24).
 __device__ __forceinline__ float div_x(float a, float b, float y) { return pt::div_rn(a, b, y); }
 
+#ifndef PT_QUAD_CULL
+#define PT_QUAD_CULL 1   // one exact quad test per ray (pt_quadcull.h), the six exact tests as fallback
+#endif
+#ifndef PT_CULL_SPHERES_FIRST
+#define PT_CULL_SPHERES_FIRST 0   // 1: sphere distances computed while the culled quad's LDS record
+#endif                            // loads (straight-line, all lanes): measured slower (0.334 vs 0.318 ms)
+}  // namespace
+#define PTQC_HD __device__ __forceinline__
+#define PTQC_RCP_APPROX(x) pt::rcp_approx(x)
+#define PTQC_RCP_EXACT(x) rcp_x(x)
+#define PTQC_DIV_EXACT(a, b, y) div_x((a), (b), (y))
+#define PTQC_FMA(a, b, c) __builtin_fmaf((a), (b), (c))
+#include "pt_quadcull.h"
+namespace {
+
 // mathlib.h:750   normalize = v * (1 / sqrt(dot(v, v)))
 __device__ __forceinline__ V3 normalize(V3 v) { return mul(v, rcp_x(sqrt_x(dot(v, v)))); }
 
@@ -233,6 +248,29 @@ __device__ __forceinline__ void sphere_test(int s, V3 P, V3 D, float& best, int&
     }
 }
 
+// TestSphereTrace (scalar.cpp:145-184) up to its distance, straight-line: hit = the reference
+// reaches the distance test (:157, :164), dist/inside as it computes them.  The acceptance
+// (0.01 < dist < best, :176) is applied by the caller.
+struct SphereHit {
+    float dist;
+    bool hit, inside;
+};
+template <class SC>
+__device__ __forceinline__ SphereHit sphere_dist(int s, V3 P, V3 D)
+{
+    const V3 m = sub(P, v3(SC::sph[s][0], SC::sph[s][1], SC::sph[s][2]));
+    const float b = dot(m, D);
+    const float c = dot(m, m) - SC::sph_r2[s];
+    const float discr = b * b - c;
+    SphereHit r;
+    r.hit = !(c > 0.0f && b > 0.0f) && !(discr < 0.0f);
+    const float sq = sqrt_x(r.hit ? discr : 1.0f);
+    const float d1 = -b - sq;                                 // :169
+    r.inside = d1 < 0.0f;                                     // :170-174
+    r.dist = r.inside ? -b + sq : d1;
+    return r;
+}
+
 template <int LAYOUT>
 __device__ __forceinline__ size_t out_index(const PtJob& j, int lc, int lr)
 {
@@ -277,18 +315,14 @@ struct Hit {
     float best;   // c_superFar (10000) on a miss
     int id;       // primitive 0..8 (quads then spheres)
     int flag;     // quad: normal flipped; sphere: hit from inside
+    int fb;       // the culled quad stage fell back to the six exact tests (counted by COUNT builds)
 };
 
+// The six exact quad tests in the reference's order (TestSceneTrace :192-261) into h.
 template <class SC>
-__device__ __forceinline__ Hit trace(const AxisRow* s_axis, V3 P, V3 D)
+__device__ __forceinline__ void quads_exact(const AxisRow* s_axis, V3 P, V3 D, V3 pq, int axis, float dP, float dD,
+                                            float yD, Hit& h)
 {
-    const V3 pq = sub(add(P, D), P);
-    // :122-133 axis used for the hit distance (ray-constant)
-    const int axis = fabsf(D.x) > 0.1f ? 0 : (fabsf(D.y) > 0.1f ? 1 : 2);
-    const float dP = axis == 0 ? P.x : (axis == 1 ? P.y : P.z);
-    const float dD = axis == 0 ? D.x : (axis == 1 ? D.y : D.z);
-    const float yD = rcp_x(dD);
-    Hit h{PT_SUPER_FAR, -1, 0};
 #if PT_AXIS_ASM
     // software pipeline of the per-quad LDS rows: row q+1 is read while quad q is tested, so the
     // LDS latency hides under a quad test instead of stalling inside its divergent tail
@@ -309,6 +343,78 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, V3 P, V3 D)
 #pragma unroll PT_TRACE_UNROLL
     for (int q = 0; q < PT_NQUADS; ++q) quad_test<SC>(s_axis, q, P, D, pq, axis, dP, dD, yD, h.best, h.id, h.flag);
 #endif
+}
+
+// Per (quad, flip): the vertices in the reference's order after its facing flip (a, b, c, d or
+// d, c, b, a), 12 floats in 3 float4 -- the exact test of the culling's chosen quad reads them.
+constexpr int kQuadVecs = PT_NQUADS * 2 * 3;
+
+// TestSceneTrace (scalar.cpp:186-287).  CAMERA: P is the camera origin (0, 0, 0).  CULL: the
+// culled quad stage (else the six exact tests).
+template <class SC, bool CAMERA, bool CULL>
+__device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, V3 P, V3 D)
+{
+    const V3 pq = sub(add(P, D), P);
+    // :122-133 axis used for the hit distance (ray-constant)
+    const int axis = fabsf(D.x) > 0.1f ? 0 : (fabsf(D.y) > 0.1f ? 1 : 2);
+    const float dP = axis == 0 ? P.x : (axis == 1 ? P.y : P.z);
+    const float dD = axis == 0 ? D.x : (axis == 1 ? D.y : D.z);
+    const float yD = rcp_x(dD);
+    Hit h{PT_SUPER_FAR, -1, 0, 0};
+    if (CULL) {
+        // classify the six quads cheaply, test the one candidate W exactly (pt_quadcull.h); a ray
+        // whose result is not certified runs the six exact tests (wave-uniform branch, rare).
+        // Straight-line order: W's vertex record is read from LDS, the spheres' distances are
+        // computed while the read is in flight, then W's exact test, then the spheres' updates in
+        // the reference's order (a sphere's distance does not depend on the running best).
+        const ptqc::F3 Pf{P.x, P.y, P.z}, pqf{pq.x, pq.y, pq.z};
+        const ptqc::Cull cl = ptqc::cull<CAMERA>(Pf, pqf, dP, yD);
+        const int W = cl.W < 0 ? 0 : cl.W;
+        const uint32_t jW = (ptqc::kAxisBits >> (2u * (uint32_t)W)) & 3u;
+        const float DjW = jW == 0 ? D.x : (jW == 1 ? D.y : D.z);
+        const bool fl = DjW > 0.0f;                                          // :69 (unit normal +e_j)
+        const float4* rec = s_qv + (W * 2 + (fl ? 1 : 0)) * 3;
+        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
+        const AxisRow ar = s_axis[W * 3 + axis];
+#if PT_CULL_SPHERES_FIRST
+        SphereHit sh[PT_NSPHERES];
+#pragma unroll
+        for (int k = 0; k < PT_NSPHERES; ++k) sh[k] = sphere_dist<SC>(k, P, D);
+#endif
+        const float ak = fl ? ar.d : ar.a, bk = fl ? ar.c : ar.b, ck = fl ? ar.b : ar.c, dk = fl ? ar.a : ar.d;
+        float dist;
+        const int code = ptqc::quad_exact(Pf, pqf, ptqc::F3{r0.x, r0.y, r0.z}, ptqc::F3{r0.w, r1.x, r1.y},
+                                          ptqc::F3{r1.z, r1.w, r2.x}, ptqc::F3{r2.y, r2.z, r2.w}, ak, bk, ck, dk, dP, dD,
+                                          yD, PT_SUPER_FAR, dist);
+        const bool ok = code == ptqc::kAccepted && cl.lb2 > dist;
+        bool unc = cl.unc || (cl.W >= 0 && !ok);
+        if (cl.W >= 0 && ok) {
+            h.best = dist;
+            h.id = W;
+            h.flag = fl ? 1 : 0;
+        }
+        if (__any(unc)) {
+            if (unc) {
+                h = Hit{PT_SUPER_FAR, -1, 0, 1};
+                quads_exact<SC>(s_axis, P, D, pq, axis, dP, dD, yD, h);
+            }
+        }
+#if PT_CULL_SPHERES_FIRST
+#pragma unroll
+        for (int k = 0; k < PT_NSPHERES; ++k)                               // :176-181
+            if (sh[k].hit && sh[k].dist > PT_MIN_HIT && sh[k].dist < h.best) {
+                h.best = sh[k].dist;
+                h.id = PT_NQUADS + k;
+                h.flag = sh[k].inside ? 1 : 0;
+            }
+#else
+#pragma unroll
+        for (int k = 0; k < PT_NSPHERES; ++k) sphere_test<SC>(k, P, D, h.best, h.id, h.flag);
+#endif
+        return h;
+    }
+    (void)s_qv;
+    quads_exact<SC>(s_axis, P, D, pq, axis, dP, dD, yD, h);
 #pragma unroll PT_TRACE_UNROLL
     for (int k = 0; k < PT_NSPHERES; ++k) sphere_test<SC>(k, P, D, h.best, h.id, h.flag);
     return h;
@@ -441,6 +547,10 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     constexpr int kWavesPerBlock = waves_per_block<ENV>();
     __shared__ PtLdsPrim s_prim[PT_NPRIMS];
     __shared__ AxisRow s_axis[PT_NQUADS * 3];
+    // the culled quad stage (pt_quadcull.h): the env kernel keeps the six exact tests (its 40 912 B
+    // of LDS leave no room for the 576-B vertex table at 4 blocks per CU)
+    constexpr bool CULL = PT_QUAD_CULL && !ENV;
+    __shared__ float4 s_qv[CULL ? kQuadVecs : 1];
     __shared__ float s_w[kMaxWeights];
     constexpr int CH = kChunk;
     // The last frame of a chunk is traced by the pixel's own lane (OWN_LAST): its radiance stays in
@@ -473,14 +583,26 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         } else if (t >= 64 && t < 64 + PT_NQUADS * 3) {
             const int q = (t - 64) / 3, k = (t - 64) % 3;
             s_axis[t - 64] = AxisRow{sc->qv[q][0][k], sc->qv[q][1][k], sc->qv[q][2][k], sc->qv[q][3][k]};
+        } else if (CULL && t >= 128 && t < 128 + kQuadVecs) {
+            const int r = (t - 128) / 3, part = (t - 128) % 3, q = r >> 1, fl = r & 1;
+            float e[4];
+            for (int i = 0; i < 4; ++i) {
+                const int f = part * 4 + i, v = f / 3, k = f % 3;   // vertex v of the flipped order
+                e[i] = sc->qv[q][fl ? 3 - v : v][k];
+            }
+            s_qv[t - 128] = make_float4(e[0], e[1], e[2], e[3]);
         }
         if (t < kMaxWeights && t < job.nframes)   // :812 1/(iFrame + 1), iFrame exact below 2^24
             s_w[t] = rcp_x((float)(job.frame_first + (uint32_t)t) + 1.0f);
     }
     __syncthreads();
 
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    float* const col_base = s_col[wv];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: scalar addressing
+    // this wave's colour slots through a 32-bit LDS pointer (a generic one is 64-bit: its base was
+    // hoisted out of the pool loop and spilled)
+    typedef __attribute__((address_space(3))) float lds_f32;
+    lds_f32* const col_lds = (lds_f32*)&s_col[0][0] + wv * (64 * CHS * 3);
     const int tiles_x = (job.ncols + 7) >> 3;
     const uint32_t total_tiles = (uint32_t)tiles_x * (uint32_t)((job.nrows + 7) >> 3);
     const int S = job.nframes, B = job.num_bounces;
@@ -497,7 +619,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     const V3 amb = v3(sc->ambient[0], sc->ambient[1], sc->ambient[2]);
     const V3 zero = v3(0.0f, 0.0f, 0.0f), one = v3(1.0f, 1.0f, 1.0f);
 
-    unsigned long long n_seg = 0, n_iter = 0, n_samp = 0, n_esc = 0, n_prim = 0;
+    unsigned long long n_seg = 0, n_iter = 0, n_samp = 0, n_esc = 0, n_prim = 0, n_fb = 0;
 #if PT_DIAG
 #if PT_DIAG >= 2
     unsigned long long dg[7] = {0, 0, 0, 0, 0, 0, 0};   // A, take, dir, trace, shade, C, tile-total
@@ -550,8 +672,8 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             px = job.buf + out_index<LAYOUT>(job, lc, lr);
             acc = v3(px[0], px[cs], px[2 * cs]);
             const V3 D0 = camera_dir(cam, fx, fy);
-            const Hit h = trace<DemofoxScene>(s_axis, zero, D0);                    // :335 rayPos = origin
-            if (COUNT) ++n_seg, ++n_prim;
+            const Hit h = trace<DemofoxScene, true, CULL>(s_axis, s_qv, zero, D0);                    // :335 rayPos = origin
+            if (COUNT) ++n_seg, ++n_prim, n_fb += (unsigned long long)h.fb;
             if (h.best == PT_SUPER_FAR) {                                 // :305-310
                 kind = 0;
                 c_const = add(zero, miss_radiance<ENV>(job, amb, D0));
@@ -617,7 +739,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 if (lane < m) {
                     const float4 e = envq[q0 + lane];
                     const V3 c = env_sample(job.env, job.env_w, job.env_h, v3(e.x, e.y, e.z));
-                    float* cp = col_base + __builtin_bit_cast(int, e.w);
+                    lds_f32* cp = col_lds + __builtin_bit_cast(int, e.w);
                     cp[0] = cp[0] + c.x;
                     cp[1] = cp[1] + c.y;
                     cp[2] = cp[2] + c.z;
@@ -680,10 +802,10 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                     }
                     DIAG_ADD(2, t_dir);
                     DIAG_MARK(t_tr);
-                    const Hit h = trace<DemofoxScene>(s_axis, P, D);
+                    const Hit h = trace<DemofoxScene, false, CULL>(s_axis, s_qv, P, D);
                     DIAG_ADD(3, t_tr);
                     DIAG_MARK(t_sh);
-                    if (COUNT) ++n_seg;
+                    if (COUNT) ++n_seg, n_fb += (unsigned long long)h.fb;
                     bool done;
                     if (h.best == PT_SUPER_FAR) {                                     // :305-310
                         if (DEFER) queued = true;                                     // env added at the drain
@@ -704,7 +826,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                         if (own && it_f == nf - 1) {   // own item: it_lane == lane
                             c_last = ret;
                         } else {
-                            float* c = col_base + (it_lane * CHS + it_f) * 3;
+                            lds_f32* c = col_lds + (it_lane * CHS + it_f) * 3;
                             c[0] = ret.x;
                             c[1] = ret.y;
                             c[2] = ret.z;
@@ -738,7 +860,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                         if (own && fi == nf - 1) {
                             c = c_last;
                         } else {
-                            const float* cp = col_base + (lane * CHS + fi) * 3;
+                            const lds_f32* cp = col_lds + (lane * CHS + fi) * 3;
                             c = v3(cp[0], cp[1], cp[2]);
                         }
                     }
@@ -775,6 +897,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             n_samp += __shfl_xor(n_samp, off, 64);
             n_esc += __shfl_xor(n_esc, off, 64);
             n_prim += __shfl_xor(n_prim, off, 64);
+            n_fb += __shfl_xor(n_fb, off, 64);
         }
         if (lane == 0) {
             atomicAdd(&job.counters[PT_CNT_SEGMENTS], n_seg);
@@ -782,6 +905,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             atomicAdd(&job.counters[PT_CNT_SAMPLES], n_samp);
             atomicAdd(&job.counters[PT_CNT_ESCAPED], n_esc);
             atomicAdd(&job.counters[PT_CNT_PRIMARY], n_prim);
+            atomicAdd(&job.counters[PT_CNT_FALLBACK], n_fb);
         }
     }
 #if PT_DIAG

@@ -66,18 +66,32 @@ PT_HD void sincosf_glibc(float y, float* s_out, float* c_out)
         n = ((int32_t)r + 0x800000) >> 24;
         x = __builtin_fma(-(double)n, kHpi, x);
     }
+    // The two polynomial constants that end up as fma addends must sit in VGPRs; writing them with
+    // inline v_mov makes the device code materialise them here (two v_mov each) instead of
+    // hoisting them out of the caller's loop, where the register allocator spilled them to scratch.
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t s2lo, s2hi, c3lo, c3hi;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(s2lo) : "n"((uint32_t)(__builtin_bit_cast(uint64_t, kS2) & 0xffffffffu)));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(s2hi) : "n"((uint32_t)(__builtin_bit_cast(uint64_t, kS2) >> 32)));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(c3lo) : "n"((uint32_t)(__builtin_bit_cast(uint64_t, kC3) & 0xffffffffu)));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(c3hi) : "n"((uint32_t)(__builtin_bit_cast(uint64_t, kC3) >> 32)));
+    const double s2 = __builtin_bit_cast(double, (uint64_t)s2hi << 32 | s2lo);
+    const double c3 = __builtin_bit_cast(double, (uint64_t)c3hi << 32 | c3lo);
+#else
+    const double s2 = kS2, c3 = kC3;
+#endif
     const double sg = ((n + 1) & 2) ? -1.0 : 1.0;        // sign[n & 3] = {1,-1,-1,1}
     const double xs = x * sg;
     const double x2 = x * x;
     // sine polynomial (sinf_poly, even n)
     const double x3 = xs * x2;
-    const double s1 = __builtin_fma(x2, kS3, kS2);
+    const double s1 = __builtin_fma(x2, kS3, s2);
     const double x7 = x3 * x2;
     const double ss = __builtin_fma(x3, kS1, xs);
     const float sp = (float)__builtin_fma(x7, s1, ss);
     // cosine polynomial (sinf_poly, odd n), table selected by n & 2
     const double x4 = x2 * x2;
-    const double c2 = __builtin_fma(x2, kC4, kC3);
+    const double c2 = __builtin_fma(x2, kC4, c3);
     const double c1 = __builtin_fma(x2, kC1, kC0);
     const double x6 = x4 * x2;
     const double cc = __builtin_fma(x4, kC2, c1);

@@ -81,7 +81,7 @@ def count_device(buf, width: int, height: int, *, frame_first: int, nframes: int
     out = N.PtWorkCounts()
     N.check(N.load().pt_count_device(ctypes.byref(job), _stream(stream), ctypes.byref(out)), "pt_count_device")
     return {"segments": out.segments, "lane_slots": out.lane_slots, "samples": out.samples, "escaped": out.escaped,
-            "primary": out.primary}
+            "primary": out.primary, "quad_fallbacks": out.quad_fallbacks}
 
 
 def render_v4_device(buf, width: int, height: int, *, frame_first: int, nframes: int, num_bounces: int = 8,

@@ -97,6 +97,8 @@ typedef struct pt_work_counts {
     uint64_t samples;            /* primary samples (pixels x frames)                              */
     uint64_t escaped;            /* paths that ended on a miss                                     */
     uint64_t primary;            /* camera-ray segments traced (= pixels rendered)                 */
+    uint64_t quad_fallbacks;     /* segments whose culled quad stage was not certified, so the six */
+                                 /* exact quad tests ran (diffuse kernel; pt_quadcull.h)           */
 } pt_work_counts;
 
 /* --- lifecycle -------------------------------------------------------------------------------- */

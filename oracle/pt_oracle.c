@@ -158,6 +158,39 @@ void pto_random_unit_vector(uint32_t* s, float o[3])
     ruv_plain(s, o);
 }
 
+/* The quad stage of TestSceneTrace alone (scalar.cpp:192-261): the six TestQuadTrace calls in
+ * order from info.dist = c_superFar.  *id = the last quad that updated (-1 none), *flipped = its
+ * normal was flipped (:69-80).  Returns the resulting info.dist. */
+float pto_trace_quads(const float P[3], const float D[3], int* id, int* flipped)
+{
+    pthread_once(&g_once, pto_init_scene);
+    hit_t_plain h;
+    h.dist = PTO_SUPER_FAR;
+    *id = -1;
+    *flipped = 0;
+    for (int i = 0; i < PTO_NQUADS; ++i)
+        if (quad_plain(P, D, &h, &g_quads[i])) {
+            *id = i;
+            *flipped = h.n[0] != g_quads[i].n[0] || h.n[1] != g_quads[i].n[1] || h.n[2] != g_quads[i].n[2];
+        }
+    return h.dist;
+}
+
+/* The whole TestSceneTrace (scalar.cpp:186-287): dist, hit normal, material id (-1 on a miss). */
+float pto_trace_scene(const float P[3], const float D[3], float n_out[3], int* id)
+{
+    pthread_once(&g_once, pto_init_scene);
+    hit_t_plain h;
+    h.dist = PTO_SUPER_FAR;
+    *id = -1;
+    for (int i = 0; i < PTO_NQUADS; ++i)
+        if (quad_plain(P, D, &h, &g_quads[i])) *id = i;
+    for (int i = 0; i < PTO_NSPHERES; ++i)
+        if (sphere_plain(P, D, &h, g_spheres[i])) *id = PTO_NQUADS + i;
+    n_out[0] = h.n[0]; n_out[1] = h.n[1]; n_out[2] = h.n[2];
+    return h.dist;
+}
+
 static int pto_check(const float* buf, const pto_params* p)
 {
     (void)ruv_unused_guard;

@@ -72,6 +72,9 @@ uint32_t pto_wang_hash(uint32_t* state);                  /* scalar.cpp:27-35  *
 float pto_randomf(uint32_t* state);                        /* scalar.cpp:37-40  */
 void pto_random_unit_vector(uint32_t* state, float out3[3]);/* scalar.cpp:42-50 */
 uint32_t pto_seed(uint32_t x, uint32_t y, uint32_t frame); /* scalar.cpp:332    */
+/* TestSceneTrace pieces (scalar.cpp:186-287) for the product's quad-culling check. */
+float pto_trace_quads(const float P[3], const float D[3], int* id, int* flipped);
+float pto_trace_scene(const float P[3], const float D[3], float n_out[3], int* id);
 void pto_env_sample(const pto_env* env, const float dir[3], float out3[3]); /* texture.cpp:101-139 */
 
 /* Output stage (pt_oracle_output.c): ACES + fast sRGB + 8-bit pack, v4 :144-187, :1260-1331. */
