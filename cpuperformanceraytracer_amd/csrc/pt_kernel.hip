@@ -87,6 +87,9 @@ __device__ __forceinline__ float div_x(float a, float b, float y) { return pt::d
 #ifndef PT_QUAD_CULL
 #define PT_QUAD_CULL 1   // one exact quad test per ray (pt_quadcull.h), the six exact tests as fallback
 #endif
+#ifndef PT_ENV_CULL
+#define PT_ENV_CULL 1    // the env kernel too (vertices from the per-axis rows, no extra LDS)
+#endif
 #ifndef PT_CULL_SPHERES_FIRST
 #define PT_CULL_SPHERES_FIRST 0   // 1: sphere distances computed while the culled quad's LDS record
 #endif                            // loads (straight-line, all lanes): measured slower (0.334 vs 0.318 ms)
@@ -350,8 +353,10 @@ __device__ __forceinline__ void quads_exact(const AxisRow* s_axis, V3 P, V3 D, V
 constexpr int kQuadVecs = PT_NQUADS * 2 * 3;
 
 // TestSceneTrace (scalar.cpp:186-287).  CAMERA: P is the camera origin (0, 0, 0).  CULL: the
-// culled quad stage (else the six exact tests).
-template <class SC, bool CAMERA, bool CULL>
+// culled quad stage (else the six exact tests).  QV: the culled quad's vertices come from the
+// flip-ordered table s_qv (else from its three per-axis rows of s_axis, flipped by selects -- the
+// env kernel, whose LDS has no room for the 576-B table at 4 blocks per CU).
+template <class SC, bool CAMERA, bool CULL, bool QV = true>
 __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, V3 P, V3 D)
 {
     const V3 pq = sub(add(P, D), P);
@@ -373,9 +378,24 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, 
         const uint32_t jW = (ptqc::kAxisBits >> (2u * (uint32_t)W)) & 3u;
         const float DjW = jW == 0 ? D.x : (jW == 1 ? D.y : D.z);
         const bool fl = DjW > 0.0f;                                          // :69 (unit normal +e_j)
-        const float4* rec = s_qv + (W * 2 + (fl ? 1 : 0)) * 3;
-        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2];
-        const AxisRow ar = s_axis[W * 3 + axis];
+        float4 r0, r1, r2;
+        AxisRow ar;
+        if (QV) {
+            const float4* rec = s_qv + (W * 2 + (fl ? 1 : 0)) * 3;
+            r0 = rec[0], r1 = rec[1], r2 = rec[2];
+            ar = s_axis[W * 3 + axis];
+        } else {
+            // rows x, y, z of quad W: (a_k, b_k, c_k, d_k); flipped order d, c, b, a
+            const AxisRow rx = s_axis[W * 3 + 0], ry = s_axis[W * 3 + 1], rz = s_axis[W * 3 + 2];
+            ar = axis == 0 ? rx : (axis == 1 ? ry : rz);
+            const V3 va = v3(fl ? rx.d : rx.a, fl ? ry.d : ry.a, fl ? rz.d : rz.a);
+            const V3 vb = v3(fl ? rx.c : rx.b, fl ? ry.c : ry.b, fl ? rz.c : rz.b);
+            const V3 vc = v3(fl ? rx.b : rx.c, fl ? ry.b : ry.c, fl ? rz.b : rz.c);
+            const V3 vd = v3(fl ? rx.a : rx.d, fl ? ry.a : ry.d, fl ? rz.a : rz.d);
+            r0 = make_float4(va.x, va.y, va.z, vb.x);
+            r1 = make_float4(vb.y, vb.z, vc.x, vc.y);
+            r2 = make_float4(vc.z, vd.x, vd.y, vd.z);
+        }
 #if PT_CULL_SPHERES_FIRST
         SphereHit sh[PT_NSPHERES];
 #pragma unroll
@@ -547,10 +567,11 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     constexpr int kWavesPerBlock = waves_per_block<ENV>();
     __shared__ PtLdsPrim s_prim[PT_NPRIMS];
     __shared__ AxisRow s_axis[PT_NQUADS * 3];
-    // the culled quad stage (pt_quadcull.h): the env kernel keeps the six exact tests (its 40 912 B
-    // of LDS leave no room for the 576-B vertex table at 4 blocks per CU)
-    constexpr bool CULL = PT_QUAD_CULL && !ENV;
-    __shared__ float4 s_qv[CULL ? kQuadVecs : 1];
+    // the culled quad stage (pt_quadcull.h); the env kernel's 40 912 B of LDS leave no room for the
+    // 576-B flip-ordered vertex table at 4 blocks per CU, so it reads the per-axis rows (QV false)
+    constexpr bool CULL = PT_QUAD_CULL && (!ENV || PT_ENV_CULL);
+    constexpr bool QV = CULL && !ENV;
+    __shared__ float4 s_qv[QV ? kQuadVecs : 1];
     __shared__ float s_w[kMaxWeights];
     constexpr int CH = kChunk;
     // The last frame of a chunk is traced by the pixel's own lane (OWN_LAST): its radiance stays in
@@ -583,7 +604,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         } else if (t >= 64 && t < 64 + PT_NQUADS * 3) {
             const int q = (t - 64) / 3, k = (t - 64) % 3;
             s_axis[t - 64] = AxisRow{sc->qv[q][0][k], sc->qv[q][1][k], sc->qv[q][2][k], sc->qv[q][3][k]};
-        } else if (CULL && t >= 128 && t < 128 + kQuadVecs) {
+        } else if (QV && t >= 128 && t < 128 + kQuadVecs) {
             const int r = (t - 128) / 3, part = (t - 128) % 3, q = r >> 1, fl = r & 1;
             float e[4];
             for (int i = 0; i < 4; ++i) {
@@ -672,7 +693,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             px = job.buf + out_index<LAYOUT>(job, lc, lr);
             acc = v3(px[0], px[cs], px[2 * cs]);
             const V3 D0 = camera_dir(cam, fx, fy);
-            const Hit h = trace<DemofoxScene, true, CULL>(s_axis, s_qv, zero, D0);                    // :335 rayPos = origin
+            const Hit h = trace<DemofoxScene, true, CULL, QV>(s_axis, s_qv, zero, D0);                    // :335 rayPos = origin
             if (COUNT) ++n_seg, ++n_prim, n_fb += (unsigned long long)h.fb;
             if (h.best == PT_SUPER_FAR) {                                 // :305-310
                 kind = 0;
@@ -802,7 +823,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                     }
                     DIAG_ADD(2, t_dir);
                     DIAG_MARK(t_tr);
-                    const Hit h = trace<DemofoxScene, false, CULL>(s_axis, s_qv, P, D);
+                    const Hit h = trace<DemofoxScene, false, CULL, QV>(s_axis, s_qv, P, D);
                     DIAG_ADD(3, t_tr);
                     DIAG_MARK(t_sh);
                     if (COUNT) ++n_seg, n_fb += (unsigned long long)h.fb;
