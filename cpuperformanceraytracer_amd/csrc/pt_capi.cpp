@@ -1001,6 +1001,7 @@ int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
     out->escaped = h[PT_CNT_ESCAPED];
     out->primary = h[PT_CNT_PRIMARY];
     out->quad_fallbacks = h[PT_CNT_FALLBACK];
+    out->sphere_fallbacks = 0;
     return PT_OK;
 }
 
@@ -1232,7 +1233,7 @@ int pt_v4_count_device(const pt_device_job* dj, void* stream, pt_work_counts* ou
     HIP_TRY(hipMemsetAsync(g.dcounters, 0, kCounterSlots * sizeof(unsigned long long), st));
     j.counters = g.dcounters;
     if ((rc = v4_launch(j, st, true))) return rc;
-    unsigned long long h[4];
+    unsigned long long h[5];
     HIP_TRY(hipMemcpyAsync(h, g.dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     out->segments = h[0];
@@ -1241,6 +1242,7 @@ int pt_v4_count_device(const pt_device_job* dj, void* stream, pt_work_counts* ou
     out->escaped = h[2];
     out->primary = out->samples;   // one camera ray per sample (jittered)
     out->quad_fallbacks = 0;
+    out->sphere_fallbacks = h[4];
     return PT_OK;
 }
 

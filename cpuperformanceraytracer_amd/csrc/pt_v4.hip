@@ -362,12 +362,44 @@ __device__ __forceinline__ float dot_k(V3 v, float cx, float cy, float cz)
     return cx != 0.0f ? v.x * cx : 0.0f;
 }
 
+// Closest sphere only (default scene).  TestSphereTrace's result for the whole sphere list is the
+// accepted sphere with the smallest distance.  The default scene's spheres are pairwise disjoint
+// balls, at least kSphereGap apart (static_assert below), so along any ray the chords of two balls
+// the ray meets are disjoint and kSphereGap apart, and they come in the order of the centres'
+// projections -b.  (Both balls within r of the line => their projections differ by
+// sqrt(|c_i - c_j|^2 - (r_i + r_j)^2) > 0; a ball holding the origin has the chord around t = 0, and
+// every ball behind the origin is rejected by the reference's own early test.)  So of the spheres
+// the reference does not reject early -- computed with its exact operations -- the one with the
+// largest b is the only one whose distance can be the smallest: its root, distance and normal are
+// evaluated once, exactly as TestSphereTrace does.  When its distance fails c_minimumRayHitTime
+// (the origin within 0.01 of its surface) a later sphere could still be accepted, so that ray runs
+// the reference's sequential tests (`fallback`, rare).  Rounding moves a distance by ~1e-5, far
+// inside the gap (0.4 in the default scene; asserted >= kSphereGap).
+constexpr float kSphereGap = 0.1f;
+constexpr bool default_spheres_disjoint()
+{
+    namespace D = pt_v4_default;
+    for (int i = 0; i < D::kSpheres; ++i)
+        for (int j = i + 1; j < D::kSpheres; ++j) {
+            const float dx = D::kSphere[i][0] - D::kSphere[j][0], dy = D::kSphere[i][1] - D::kSphere[j][1],
+                        dz = D::kSphere[i][2] - D::kSphere[j][2];
+            const float rr = D::kSphere[i][3] + D::kSphere[j][3] + kSphereGap;
+            if (!(dx * dx + dy * dy + dz * dz > rr * rr)) return false;
+        }
+    return true;
+}
+static_assert(default_spheres_disjoint(), "the closest-sphere trace needs pairwise disjoint spheres");
+#ifndef PT_V4_SPHERE_CLOSEST
+#define PT_V4_SPHERE_CLOSEST 1
+#endif
+
 // TestSceneTrace :700-718: quads in order, then spheres (object index = material index).
 // DEF: the reference's InitializeScene, geometry as instruction literals (pt_v4_default_scene.h,
 // generated from pt_v4_build_scene and checked by tests/test_oracle_v4.py); otherwise the scene
-// table of the kernel arguments (scalar loads per primitive).
+// table of the kernel arguments (scalar loads per primitive).  s_sc: the default scene's sphere
+// centres in LDS (DEF); fb: set when the closest-sphere stage fell back to the sequential tests.
 template <bool DEF>
-__device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir)
+__device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir, const float4* s_sc, int& fb)
 {
     Hit h{kSuperFar, v3(0.0f, 0.0f, 0.0f), false, 0};
     if constexpr (DEF) {
@@ -379,10 +411,56 @@ __device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir)
         for (int i = 0; i < D::kQuads; ++i)
             quad_test(pos, dir, h, i, v3(D::kQuad[i][0], D::kQuad[i][1], D::kQuad[i][2]),
                       v3(D::kQuad[i][3], D::kQuad[i][4], D::kQuad[i][5]), dk, i);
+        if (PT_V4_SPHERE_CLOSEST) {
+            float bmax = -__builtin_huge_valf(), dsel = 0.0f;
+            int ksel = -1;
 #pragma unroll
-        for (int i = 0; i < D::kSpheres; ++i)
-            sphere_test(pos, dir, h, D::kQuads + i, v3(D::kSphere[i][0], D::kSphere[i][1], D::kSphere[i][2]),
-                        D::kSphere[i][3]);
+            for (int i = 0; i < D::kSpheres; ++i) {   // :645-657, the early test exactly
+                const V3 m = pos - v3(D::kSphere[i][0], D::kSphere[i][1], D::kSphere[i][2]);
+                const float b = dot(m, dir);
+                const float cc = fma_(-D::kSphere[i][3], D::kSphere[i][3], dot(m, m));
+                const float discr = fma_(b, b, -cc);
+                const bool early = discr < 0.0f || (cc > 0.0f && b > 0.0f);
+                const bool take = !early && b > bmax;
+                bmax = take ? b : bmax;
+                dsel = take ? discr : dsel;
+                ksel = take ? i : ksel;
+            }
+            bool seq = false;
+            if (ksel >= 0) {
+                const float4 c = s_sc[ksel];
+                const V3 m = pos - v3(c.x, c.y, c.z);
+                const float s = sqrt_(dsel);
+                const bool inside = -bmax < s;
+                const float dist = (inside ? s : -s) - bmax;
+                if (dist > kMinHit) {
+                    if (dist < h.dist) {
+                        h.inside = inside;
+                        h.dist = dist;
+                        const V3 p = v3(fma_(dir.x, dist, m.x), fma_(dir.y, dist, m.y), fma_(dir.z, dist, m.z));
+                        h.n = normalize(p) * (inside ? -1.0f : 1.0f);
+                        h.mat = D::kQuads + ksel;
+                    }
+                } else {
+                    seq = true;
+                }
+            }
+            if (__builtin_expect(__any(seq), 0)) {   // wave-uniform, rare
+                if (seq) {
+                    fb = 1;
+#pragma unroll 1
+                    for (int i = 0; i < D::kSpheres; ++i) {
+                        const float4 c = s_sc[i];
+                        sphere_test(pos, dir, h, D::kQuads + i, v3(c.x, c.y, c.z), c.w);
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < D::kSpheres; ++i)
+                sphere_test(pos, dir, h, D::kQuads + i, v3(D::kSphere[i][0], D::kSphere[i][1], D::kSphere[i][2]),
+                            D::kSphere[i][3]);
+        }
     } else {
         int obj = 0;
         for (int i = 0; i < sc.nquads; ++i, ++obj) {
@@ -417,11 +495,16 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
 {
     __shared__ float s_col[kWaves][kChunk * 64 * 3];
     __shared__ PtV4Mat s_mat[PT_V4_MAX_OBJECTS];
+    __shared__ float4 s_sc[DEF ? pt_v4_default::kSpheres : 1];   // default scene: sphere centre, radius
     constexpr bool DEFER = ENV != PT_V4_ENV_NONE_ && PT_V4_ENV_DEFER != 0;
     __shared__ float4 s_qd[DEFER ? kWaves : 1][DEFER ? kEnvQ : 1];   // env dir, rng
     __shared__ float4 s_qt[DEFER ? kWaves : 1][DEFER ? kEnvQ : 1];   // throughput, colour slot
     for (int t = threadIdx.x; t < PT_V4_MAX_OBJECTS * 17; t += 64 * kWaves)
         reinterpret_cast<float*>(s_mat)[t] = reinterpret_cast<const float*>(sc.mat)[t];
+    if (DEF && threadIdx.x < pt_v4_default::kSpheres) {
+        const float* c = pt_v4_default::kSphere[threadIdx.x];
+        s_sc[threadIdx.x] = make_float4(c[0], c[1], c[2], c[3]);
+    }
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -435,7 +518,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     const float W = (float)job.width, H = (float)job.height;
     const float rW = rcp(W), rH = rcp(H);
     const float cam_dist = 1.0f;   // 1 / tanf(c_FOVDegrees * 0.5f * c_pi / 180.0f) == 1.0f exactly (InitializeCamera :1500)
-    unsigned long long n_seg = 0, n_esc = 0, n_slots = 0;
+    unsigned long long n_seg = 0, n_esc = 0, n_slots = 0, n_fb = 0;
 
     // persistent waves: 8x8 tiles from the launch's queue (pt_tile_queue.h), longest first when the
     // geometry has a schedule
@@ -530,8 +613,9 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
             int qslot = 0;
             if (item >= 0) {
                 // one iteration of GetColorForRay's bounce loop (:733-909)
-                const Hit h = trace<DEF>(sc, pos, dir);
-                if (COUNT) ++n_seg;
+                int fb = 0;
+                const Hit h = trace<DEF>(sc, pos, dir, s_sc, fb);
+                if (COUNT) ++n_seg, n_fb += (unsigned long long)fb;
                 const bool miss = h.dist == kSuperFar;
                 bool done = false;
                 if (miss) {
@@ -703,11 +787,13 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
         for (int off = 32; off > 0; off >>= 1) {
             n_seg += __shfl_down(n_seg, off);
             n_esc += __shfl_down(n_esc, off);
+            n_fb += __shfl_down(n_fb, off);
         }
         if (lane == 0) {
             atomicAdd(&job.counters[0], n_seg);
             atomicAdd(&job.counters[2], n_esc);
             atomicAdd(&job.counters[3], n_slots);
+            atomicAdd(&job.counters[4], n_fb);
         }
     }
 }

@@ -102,4 +102,5 @@ def count_v4_device(buf, width: int, height: int, *, frame_first: int, nframes: 
     job = _job(buf, width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces, layout, use_env)
     out = N.PtWorkCounts()
     N.check(N.load().pt_v4_count_device(ctypes.byref(job), _stream(stream), ctypes.byref(out)), "pt_v4_count_device")
-    return {"segments": out.segments, "lane_slots": out.lane_slots, "samples": out.samples, "escaped": out.escaped}
+    return {"segments": out.segments, "lane_slots": out.lane_slots, "samples": out.samples, "escaped": out.escaped,
+            "sphere_fallbacks": out.sphere_fallbacks}

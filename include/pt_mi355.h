@@ -99,6 +99,8 @@ typedef struct pt_work_counts {
     uint64_t primary;            /* camera-ray segments traced (= pixels rendered)                 */
     uint64_t quad_fallbacks;     /* segments whose culled quad stage was not certified, so the six */
                                  /* exact quad tests ran (diffuse kernel; pt_quadcull.h)           */
+    uint64_t sphere_fallbacks;   /* segments whose closest-sphere stage fell back to the sequential */
+                                 /* sphere tests (v4 kernel, default scene)                        */
 } pt_work_counts;
 
 /* --- lifecycle -------------------------------------------------------------------------------- */

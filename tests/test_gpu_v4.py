@@ -115,6 +115,9 @@ def test_v4_full_1080p_8spp():
     ref = po.render4(1920, 1080, nframes=8, env=env)
     assert bits_equal(got, ref), mismatch_report(got, ref)
     assert cnt["samples"] == 1920 * 1080 * 8
+    # the closest-sphere stage (pt_v4.hip) decides almost every segment; the sequential sphere
+    # tests run as a fallback only, and the image above is still bit-identical
+    assert cnt["sphere_fallbacks"] <= 1e-3 * cnt["segments"], cnt
 
 
 def test_v4_counts_match_oracle():
