@@ -274,6 +274,72 @@ __device__ __forceinline__ SphereHit sphere_dist(int s, V3 P, V3 D)
     return r;
 }
 
+// The three TestSphereTrace calls (scalar.cpp:274-285) with one root.  The spheres are pairwise
+// disjoint balls (static_assert: 3 apart), so along a ray the chords of two balls it meets are
+// disjoint, at least that far apart, and ordered like the centres' projections -b (see pt_v4.hip's
+// closest-sphere stage for the argument).  Of the spheres the reference does not reject early --
+// its exact operations -- only the one with the largest b can hold the smallest distance: its root
+// and distance are evaluated as TestSphereTrace does and accepted against the running best.  A
+// distance that fails c_minimumRayHitTime (origin within 0.01 of that surface) sends the ray to the
+// sequential tests (rare; a sphere farther along could still be accepted).
+constexpr bool scene_spheres_disjoint()
+{
+    for (int i = 0; i < PT_NSPHERES; ++i)
+        for (int j = i + 1; j < PT_NSPHERES; ++j) {
+            const float dx = DemofoxScene::sph[i][0] - DemofoxScene::sph[j][0];
+            const float dy = DemofoxScene::sph[i][1] - DemofoxScene::sph[j][1];
+            const float dz = DemofoxScene::sph[i][2] - DemofoxScene::sph[j][2];
+            const float rr = DemofoxScene::sph[i][3] + DemofoxScene::sph[j][3] + 0.1f;
+            if (!(dx * dx + dy * dy + dz * dz > rr * rr)) return false;
+        }
+    return true;
+}
+static_assert(scene_spheres_disjoint(), "the closest-sphere stage needs pairwise disjoint spheres");
+#ifndef PT_SPHERE_CLOSEST
+#define PT_SPHERE_CLOSEST 1
+#endif
+
+template <class SC>
+__device__ __forceinline__ void spheres_closest(V3 P, V3 D, float& best, int& id, int& flag)
+{
+    float bmax = -__builtin_huge_valf(), dsel = 0.0f;
+    int ksel = -1;
+#pragma unroll
+    for (int s = 0; s < PT_NSPHERES; ++s) {   // :150-164 exactly
+        const V3 m = sub(P, v3(SC::sph[s][0], SC::sph[s][1], SC::sph[s][2]));
+        const float b = dot(m, D);
+        const float c = dot(m, m) - SC::sph_r2[s];
+        const float discr = b * b - c;
+        const bool early = (c > 0.0f && b > 0.0f) || discr < 0.0f;
+        const bool take = !early && b > bmax;
+        bmax = take ? b : bmax;
+        dsel = take ? discr : dsel;
+        ksel = take ? s : ksel;
+    }
+    bool seq = false;
+    if (ksel >= 0) {
+        const float sq = sqrt_x(dsel);
+        float dist = -bmax - sq;                                  // :169
+        const bool inside = dist < 0.0f;                          // :170-174
+        dist = inside ? -bmax + sq : dist;
+        if (dist > PT_MIN_HIT) {
+            if (dist < best) {                                    // :176-181
+                best = dist;
+                id = PT_NQUADS + ksel;
+                flag = inside ? 1 : 0;
+            }
+        } else {
+            seq = true;
+        }
+    }
+    if (__builtin_expect(__any(seq), 0)) {
+        if (seq) {
+#pragma unroll
+            for (int k = 0; k < PT_NSPHERES; ++k) sphere_test<SC>(k, P, D, best, id, flag);
+        }
+    }
+}
+
 template <int LAYOUT>
 __device__ __forceinline__ size_t out_index(const PtJob& j, int lc, int lr)
 {
@@ -356,7 +422,7 @@ constexpr int kQuadVecs = PT_NQUADS * 2 * 3;
 // culled quad stage (else the six exact tests).  QV: the culled quad's vertices come from the
 // flip-ordered table s_qv (else from its three per-axis rows of s_axis, flipped by selects -- the
 // env kernel, whose LDS has no room for the 576-B table at 4 blocks per CU).
-template <class SC, bool CAMERA, bool CULL, bool QV = true>
+template <class SC, bool CAMERA, bool CULL, bool QV = true, bool SPH_CLOSEST = true>
 __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, V3 P, V3 D)
 {
     const V3 pq = sub(add(P, D), P);
@@ -427,6 +493,13 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, 
                 h.id = PT_NQUADS + k;
                 h.flag = sh[k].inside ? 1 : 0;
             }
+#elif PT_SPHERE_CLOSEST
+        if (SPH_CLOSEST) {
+            spheres_closest<SC>(P, D, h.best, h.id, h.flag);
+        } else {
+#pragma unroll
+            for (int k = 0; k < PT_NSPHERES; ++k) sphere_test<SC>(k, P, D, h.best, h.id, h.flag);
+        }
 #else
 #pragma unroll
         for (int k = 0; k < PT_NSPHERES; ++k) sphere_test<SC>(k, P, D, h.best, h.id, h.flag);
@@ -693,7 +766,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             px = job.buf + out_index<LAYOUT>(job, lc, lr);
             acc = v3(px[0], px[cs], px[2 * cs]);
             const V3 D0 = camera_dir(cam, fx, fy);
-            const Hit h = trace<DemofoxScene, true, CULL, QV>(s_axis, s_qv, zero, D0);                    // :335 rayPos = origin
+            const Hit h = trace<DemofoxScene, true, CULL, QV, !ENV>(s_axis, s_qv, zero, D0);                    // :335 rayPos = origin
             if (COUNT) ++n_seg, ++n_prim, n_fb += (unsigned long long)h.fb;
             if (h.best == PT_SUPER_FAR) {                                 // :305-310
                 kind = 0;
@@ -823,7 +896,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                     }
                     DIAG_ADD(2, t_dir);
                     DIAG_MARK(t_tr);
-                    const Hit h = trace<DemofoxScene, false, CULL, QV>(s_axis, s_qv, P, D);
+                    const Hit h = trace<DemofoxScene, false, CULL, QV, !ENV>(s_axis, s_qv, P, D);
                     DIAG_ADD(3, t_tr);
                     DIAG_MARK(t_sh);
                     if (COUNT) ++n_seg, n_fb += (unsigned long long)h.fb;

@@ -29,7 +29,7 @@ for i in range(3):
     render_device(buf, W, H, frame_first=1 + S * (i + 1), nframes=S, num_bounces=B, use_env=ENV)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-K = 10
+K = int(os.environ.get("PT_QP_K", "10"))
 e0.record()
 for i in range(K):
     render_device(buf, W, H, frame_first=1 + S * (i + 4), nframes=S, num_bounces=B, use_env=ENV)
