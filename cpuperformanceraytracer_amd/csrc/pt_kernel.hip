@@ -298,6 +298,9 @@ static_assert(scene_spheres_disjoint(), "the closest-sphere stage needs pairwise
 #ifndef PT_SPHERE_CLOSEST
 #define PT_SPHERE_CLOSEST 1
 #endif
+#ifndef PT_SPHERE_FORCE_SEQ
+#define PT_SPHERE_FORCE_SEQ 0   // test builds: every candidate ray takes the sequential fallback
+#endif
 
 template <class SC>
 __device__ __forceinline__ void spheres_closest(V3 P, V3 D, float& best, int& id, int& flag)
@@ -322,7 +325,7 @@ __device__ __forceinline__ void spheres_closest(V3 P, V3 D, float& best, int& id
         float dist = -bmax - sq;                                  // :169
         const bool inside = dist < 0.0f;                          // :170-174
         dist = inside ? -bmax + sq : dist;
-        if (dist > PT_MIN_HIT) {
+        if (dist > PT_MIN_HIT && !PT_SPHERE_FORCE_SEQ) {
             if (dist < best) {                                    // :176-181
                 best = dist;
                 id = PT_NQUADS + ksel;

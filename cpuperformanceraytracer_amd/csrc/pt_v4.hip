@@ -392,6 +392,9 @@ static_assert(default_spheres_disjoint(), "the closest-sphere trace needs pairwi
 #ifndef PT_V4_SPHERE_CLOSEST
 #define PT_V4_SPHERE_CLOSEST 1
 #endif
+#ifndef PT_V4_SPHERE_FORCE_SEQ
+#define PT_V4_SPHERE_FORCE_SEQ 0   // test builds: every candidate ray takes the sequential fallback
+#endif
 
 // TestSceneTrace :700-718: quads in order, then spheres (object index = material index).
 // DEF: the reference's InitializeScene, geometry as instruction literals (pt_v4_default_scene.h,
@@ -433,7 +436,7 @@ __device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir, const 
                 const float s = sqrt_(dsel);
                 const bool inside = -bmax < s;
                 const float dist = (inside ? s : -s) - bmax;
-                if (dist > kMinHit) {
+                if (dist > kMinHit && !PT_V4_SPHERE_FORCE_SEQ) {
                     if (dist < h.dist) {
                         h.inside = inside;
                         h.dist = dist;
