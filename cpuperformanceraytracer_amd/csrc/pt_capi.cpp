@@ -127,6 +127,7 @@ int fail(int code, const char* fmt, ...)
     } while (0)
 
 constexpr uint32_t kMaxFrame = 1u << 24;   // iFrame is an f32 counter: exact below 2^24
+constexpr int32_t kMaxDim = 1 << 24;        // pixel coordinates are f32 in mainImage: exact up to 2^24
 #if PT_DIAG
 constexpr int kCounterSlots = 32 + 4 * 65536 + 96 * 65536;   // + per-wave records, per-tile log
 #else
@@ -512,6 +513,7 @@ int check_frame_args(const float* buf, int32_t w, int32_t h, int32_t nc)
     if (w <= 0 || h <= 0) return fail(PT_EINVAL, "invalid size %dx%d", w, h);
     if (nc != 3) return fail(PT_EINVAL, "NumChannels must be 3 (RGB f32), got %d", nc);
     if ((int64_t)w * h > (int64_t)1 << 30) return fail(PT_EINVAL, "image too large");
+    if (w > kMaxDim || h > kMaxDim) return fail(PT_EINVAL, "image side > 2^24 (f32 pixel coordinates inexact)");
     return PT_OK;
 }
 
@@ -869,6 +871,8 @@ static int device_job(const pt_device_job* dj, PtJob* j)
     if (!dj || !dj->buf) return fail(PT_EINVAL, "null device job/buffer");
     if (dj->width <= 0 || dj->height <= 0 || dj->nrows < 0 || dj->row_stride <= 0 || dj->row_start < 0)
         return fail(PT_EINVAL, "invalid device job geometry");
+    if (dj->width > kMaxDim || dj->height > kMaxDim)
+        return fail(PT_EINVAL, "image side > 2^24 (f32 pixel coordinates inexact)");
     if (dj->nrows > 0 && dj->row_start + (int64_t)(dj->nrows - 1) * dj->row_stride >= dj->height)
         return fail(PT_EINVAL, "row shard exceeds the image height");
     if (dj->layout != PT_LAYOUT_INTERLEAVED && dj->layout != PT_LAYOUT_PLANAR8)

@@ -376,10 +376,14 @@ __device__ __forceinline__ V3 camera_dir(const Camera& cam, float fx, float fy)
     return normalize(v3(tx - 0.0f, ty - 0.0f, cam.cam_dist - 0.0f));                            // :351
 }
 
-// scalar.cpp:332
-__device__ __forceinline__ uint32_t seed_of(float fx, float fy, float iFrame)
+// scalar.cpp:332: (uint32_t)(float)x * 1973 + (uint32_t)(float)y * 9277 + (uint32_t)iFrame * 26699, | 1.
+// The pixel coordinates and the frame index are integers below 2^24 (the C ABI rejects larger
+// images and frame counters), so every float round trip is the identity, and each wrapping u32
+// product is the low word of the 24 x 24-bit product (v_mul_u32_u24, not the quarter-rate
+// v_mul_lo_u32).
+__device__ __forceinline__ uint32_t seed_int(uint32_t x, uint32_t y, uint32_t frame)
 {
-    return ((uint32_t)fx * 1973u + (uint32_t)fy * 9277u + (uint32_t)iFrame * 26699u) | 1u;
+    return (__umul24(x, 1973u) + __umul24(y, 9277u) + __umul24(frame, 26699u)) | 1u;
 }
 
 // Closest hit of one ray against the scene (TestSceneTrace, scalar.cpp:186-287).
@@ -818,7 +822,8 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             int bounce = 0;
             if (own && kind == 2) {   // start with this pixel's own last-frame sample (bounce 0 done)
                 const PtLdsPrim pr = s_prim[id1];
-                rng = seed_of(fx, fy, (float)(job.frame_first + (uint32_t)(f0 + nf - 1)));   // :332
+                rng = seed_int((uint32_t)(job.col0 + lc), (uint32_t)(job.height - 1 - (job.row_start + lr * job.row_stride)),
+                               job.frame_first + (uint32_t)(f0 + nf - 1));   // :332
                 P = P1;
                 n = N1;
                 ret = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one));             // :319
@@ -853,8 +858,8 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 #if PT_PIXEL_MAJOR   // consecutive items = the frames of one pixel (shared ray origin)
                     // k / npf as (k * ceil(2^16 / npf)) >> 16: exact for k < 64 npf, npf < 32 (the
                     // error k (M - 2^16 / npf) / 2^16 < npf / 1024 stays below the 1/npf gap)
-                    const int slot_pm = take ? (int)(((uint32_t)k * div_m) >> 16) : 0;
-                    const int fi = take ? k - slot_pm * npf : 0;
+                    const int slot_pm = take ? (int)(__umul24((uint32_t)k, div_m) >> 16) : 0;   // k * div_m < 2^25
+                    const int fi = take ? k - (int)__umul24((uint32_t)slot_pm, (uint32_t)npf) : 0;
 #else
                     const int fi = take ? k / nh : 0;
 #endif
@@ -869,10 +874,10 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                         const int sId = packed & 0xff;
                         const int src = packed >> 8;                  // lane owning the pixel
                         const int slc = txi * 8 + (src & 7), slr = tyi * 8 + (src >> 3);
-                        const float sfx = (float)(job.col0 + slc);
-                        const float sfy = (float)(job.height - 1 - (job.row_start + slr * job.row_stride));
                         const PtLdsPrim pr = s_prim[sId];
-                        rng = seed_of(sfx, sfy, (float)(job.frame_first + (uint32_t)(f0 + fi)));    // :332
+                        rng = seed_int((uint32_t)(job.col0 + slc),
+                                       (uint32_t)(job.height - 1 - (job.row_start + slr * job.row_stride)),
+                                       job.frame_first + (uint32_t)(f0 + fi));                    // :332
                         P = v3(a0.x, a0.y, a0.z);                                            // :313 (bounce 0)
                         n = v3(s_nrm[wv][0][slot], s_nrm[wv][1][slot], s_nrm[wv][2][slot]);
                         ret = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one));                 // :319

@@ -79,6 +79,16 @@ def test_no_gpu_fails_loudly(lib_path):
         pt.DemofoxRenderScalar(buf, 8, 4, 3)
 
 
+def test_image_side_limit(lib_path):
+    """mainImage's pixel coordinates are f32: sides above 2^24 are rejected before any GPU work."""
+    from cpuperformanceraytracer_amd import _native
+    L = _native.load()
+    buf = np.zeros(8, np.float32)   # never touched: the size check fails first
+    rc = L.pt_render_scalar(buf.ctypes.data, (1 << 24) + 8, 1, 3)
+    assert rc == _native.PT_EINVAL
+    assert b"2^24" in L.pt_last_error()
+
+
 def test_struct_layouts_match_header():
     """ctypes mirrors of the POD structs have the C sizes the header implies."""
     from cpuperformanceraytracer_amd import _native as N
@@ -86,7 +96,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(N.PtBufferInfo) == 8 + 3 * 4 + 4      # pointer + 3 ints (+ tail pad)
     assert ctypes.sizeof(N.PtTileInfo) == 8 * 4
     assert ctypes.sizeof(N.PtDeviceJob) == 8 + 9 * 4 + 4
-    assert ctypes.sizeof(N.PtWorkCounts) == 6 * 8
+    assert ctypes.sizeof(N.PtWorkCounts) == 7 * 8
 
 
 def test_reference_shaped_host_compiles_and_links(tmp_path):
