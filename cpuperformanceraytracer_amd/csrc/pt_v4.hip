@@ -253,20 +253,39 @@ __device__ __forceinline__ V3 cubemap(const Tex& t, V3 d, bool random, uint32_t&
 
 // ---- intersection and shading -------------------------------------------------------------------
 
-__device__ __forceinline__ float fresnel(float n1, float n2, V3 normal, V3 incident, float f0)   // :429-453
+// Per-material constants of fresnel() and the refraction ratio, evaluated once per block with the
+// very operations the per-hit code used (so the same bits): r0 = (n1 - n2) * rcp(n1 + n2) squared
+// is the same for (n1, n2) = (1, ior) and (ior, 1) (1 + ior == ior + 1, 1 - ior == -(ior - 1));
+// n1 * rcp(n2) is rcp(ior) outside (1 * x == x) and ior inside (rcp(1) == 1).
+struct MatX {
+    float r0sq, omr0, rior, nnout, rscc;
+};
+__device__ __forceinline__ MatX mat_consts(const PtV4Mat& M)
 {
-    float r0 = (n1 - n2) * rcp(n1 + n2);
-    r0 = r0 * r0;
+    MatX x;
+    float r0 = (1.0f - M.ior) * rcp(1.0f + M.ior);
+    x.r0sq = r0 * r0;
+    x.omr0 = 1.0f - x.r0sq;
+    x.rior = rcp(M.ior);
+    x.nnout = x.rior * x.rior;
+    x.rscc = rcp(1.0f - M.spec_chance);
+    return x;
+}
+
+// Fresnel-Schlick (v4 :429-453) for (n1, n2) = inside ? (ior, 1) : (1, ior), with the constants of MatX
+__device__ __forceinline__ float fresnel_m(bool inside, float ior, const MatX& X, V3 normal, V3 incident, float f0)
+{
+    const float r0 = X.r0sq;
     float cosX = -dot(normal, incident);
-    const bool cond = n1 > n2;
-    const float n = n1 * rcp(n2);
-    const float stc = fma_(-(n * n), fma_(-cosX, cosX, 1.0f), 1.0f);
+    const bool cond = inside ? ior > 1.0f : 1.0f > ior;
+    const float nn = inside ? ior * ior : X.nnout;
+    const float stc = fma_(-nn, fma_(-cosX, cosX, 1.0f), 1.0f);
     const float ncos = sqrt_(stc);
     const bool tir = 0.0f > stc;
     cosX = (cond && !tir) ? ncos : cosX;
     const float x = 1.0f - cosX;
     const float x2 = x * x;
-    float ret = fma_(((1.0f - r0) * x2) * x2, x, r0);
+    float ret = fma_((X.omr0 * x2) * x2, x, r0);
     ret = (cond && tir) ? 1.0f : ret;
     return fma_(ret, 1.0f - f0, f0);
 }
@@ -499,11 +518,14 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     __shared__ float s_col[kWaves][kChunk * 64 * 3];
     __shared__ PtV4Mat s_mat[PT_V4_MAX_OBJECTS];
     __shared__ float4 s_sc[DEF ? pt_v4_default::kSpheres : 1];   // default scene: sphere centre, radius
+    __shared__ MatX s_mx[PT_V4_MAX_OBJECTS];                        // per-material constants (mat_consts)
     constexpr bool DEFER = ENV != PT_V4_ENV_NONE_ && PT_V4_ENV_DEFER != 0;
     __shared__ float4 s_qd[DEFER ? kWaves : 1][DEFER ? kEnvQ : 1];   // env dir, rng
     __shared__ float4 s_qt[DEFER ? kWaves : 1][DEFER ? kEnvQ : 1];   // throughput, colour slot
     for (int t = threadIdx.x; t < PT_V4_MAX_OBJECTS * 17; t += 64 * kWaves)
         reinterpret_cast<float*>(s_mat)[t] = reinterpret_cast<const float*>(sc.mat)[t];
+    __syncthreads();
+    if (threadIdx.x < PT_V4_MAX_OBJECTS) s_mx[threadIdx.x] = mat_consts(s_mat[threadIdx.x]);
     if (DEF && threadIdx.x < pt_v4_default::kSpheres) {
         const float* c = pt_v4_default::kSphere[threadIdx.x];
         s_sc[threadIdx.x] = make_float4(c[0], c[1], c[2], c[3]);
@@ -594,7 +616,8 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                         const int Y = job.row_start + rb * job.row_stride;
                         const uint32_t frame = job.frame_first + (uint32_t)(c0 + f);
                         const int fyi = job.height - 1 - Y;
-                        rng = 1u | ((uint32_t)X * 1973u + (uint32_t)fyi * 9277u + frame * 26699u);
+                        // 24 x 24-bit products: X, fyi, frame < 2^24 (C ABI), low words = the u32 products
+                        rng = 1u | (__umul24((uint32_t)X, 1973u) + __umul24((uint32_t)fyi, 9277u) + __umul24(frame, 26699u));
                         const float jx = randf(rng) - 0.5f;
                         const float jy = randf(rng) - 0.5f;
                         const float tx = fma_(((float)X + jx) * rW, 2.0f, -1.0f);
@@ -648,9 +671,9 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                     } else {
                         float spec = M.spec_chance, refr = M.refr_chance;
                         if (spec > 0.0f) {   // :807-829 (the Fresnel result is used only with a specular chance)
-                            const float n1 = h.inside ? M.ior : 1.0f, n2 = h.inside ? 1.0f : M.ior;
-                            const float nspec = fresnel(n1, n2, h.n, dir, M.spec_chance);
-                            const float rscc = rcp(1.0f - M.spec_chance);
+                            const MatX& X = s_mx[h.mat];
+                            const float nspec = fresnel_m(h.inside, M.ior, X, h.n, dir, M.spec_chance);
+                            const float rscc = X.rscc;
                             spec = nspec;
                             refr = refr * fma_(-nspec, rscc, rscc);
                         }
@@ -692,7 +715,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                             }
                         } else {
                             uint32_t r = s_refr;
-                            const float ior = h.inside ? M.ior : rcp(M.ior);
+                            const float ior = h.inside ? M.ior : s_mx[h.mat].rior;
                             const float rrsq = M.refr_rough * M.refr_rough;
                             V3 rd = refract(dir, h.n, ior);
                             if (rejection) {

@@ -21,11 +21,14 @@ if use_env:
     set_env_map(env, 0, B)
 buf = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
 cnt = count_v4_device(buf, W, H, frame_first=1, nframes=S, num_bounces=B, use_env=use_env)
-for i in range(3):
-    render_v4_device(buf, W, H, frame_first=1 + S * (i + 1), nframes=S, num_bounces=B, use_env=use_env)
-torch.cuda.synchronize()
+import time
+_t0 = time.perf_counter()   # device warm-up (clock ramp), as bench.py --device-warmup-ms
+while time.perf_counter() - _t0 < float(os.environ.get("PT_QP_WARM_S", "0.08")):
+    for i in range(3):
+        render_v4_device(buf, W, H, frame_first=1 + S * (i + 1), nframes=S, num_bounces=B, use_env=use_env)
+    torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-K = 10
+K = int(os.environ.get("PT_QP_K", "10"))
 e0.record()
 for i in range(K):
     render_v4_device(buf, W, H, frame_first=1 + S * (i + 4), nframes=S, num_bounces=B, use_env=use_env)
