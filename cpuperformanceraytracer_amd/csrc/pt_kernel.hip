@@ -368,11 +368,20 @@ struct Camera {
 
 // mainImage, scalar.cpp:338-351: the camera ray of pixel (fx, fy).  It does not depend on the
 // frame (no jitter in the reference), so it is computed once per pixel.
+// A wave-uniform divisor copied into a VGPR here, at the use: the division's fmas read it beside
+// another scalar operand (one SGPR per VALU instruction), and a copy the compiler hoists out of
+// the tile loop stays live across the pool and is spilled.
+__device__ __forceinline__ float vgpr_here(float x)
+{
+    float v;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(v) : "s"(x));
+    return v;
+}
 __device__ __forceinline__ V3 camera_dir(const Camera& cam, float fx, float fy)
 {
-    const float tx = div_x(fx, cam.W, cam.yW) * 2.0f - 1.0f;                                   // :342
-    float ty = div_x(fy, cam.H, cam.yH) * 2.0f - 1.0f;
-    ty = div_x(ty, cam.aspect, cam.yAspect);                                                    // :347
+    const float tx = div_x(fx, vgpr_here(cam.W), cam.yW) * 2.0f - 1.0f;                       // :342
+    float ty = div_x(fy, vgpr_here(cam.H), cam.yH) * 2.0f - 1.0f;
+    ty = div_x(ty, vgpr_here(cam.aspect), cam.yAspect);                                         // :347
     return normalize(v3(tx - 0.0f, ty - 0.0f, cam.cam_dist - 0.0f));                            // :351
 }
 
@@ -709,13 +718,13 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     const int S = job.nframes, B = job.num_bounces;
     const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;   // channel stride
 
-    Camera cam;
-    cam.W = (float)job.width;
-    cam.H = (float)job.height;
-    cam.yW = rcp_x(cam.W);
-    cam.yH = rcp_x(cam.H);
-    cam.aspect = div_x(cam.W, cam.H, cam.yH);                                   // :346
-    cam.yAspect = rcp_x(cam.aspect);
+    Camera cam;   // frame constants from the kernel arguments (pt_launch_render, host)
+    cam.W = job.cam_W;
+    cam.H = job.cam_H;
+    cam.yW = job.cam_yW;
+    cam.yH = job.cam_yH;
+    cam.aspect = job.cam_aspect;                                                // :346
+    cam.yAspect = job.cam_yAspect;
     cam.cam_dist = sc->cam_dist;
     const V3 amb = v3(sc->ambient[0], sc->ambient[1], sc->ambient[2]);
     const V3 zero = v3(0.0f, 0.0f, 0.0f), one = v3(1.0f, 1.0f, 1.0f);
@@ -763,14 +772,14 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         const bool valid = lc < job.ncols && lr < job.nrows;
         const float fx = (float)(job.col0 + lc);                                            // :806
         const float fy = (float)(job.height - 1 - (job.row_start + lr * job.row_stride));   // :803
-        float* px = nullptr;
+        // (the accumulator address is recomputed for the store: held across phase B it was spilled)
         V3 acc = zero;
         int kind = -1;            // -1 no pixel, 0 camera ray missed, 1 hit and B == 0, 2 has items
         V3 c_const = zero;        // radiance of every frame for kinds 0 and 1
         V3 P1 = zero, N1 = zero;
         int id1 = 0;
         if (valid) {
-            px = job.buf + out_index<LAYOUT>(job, lc, lr);
+            const float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
             acc = v3(px[0], px[cs], px[2 * cs]);
             const V3 D0 = camera_dir(cam, fx, fy);
             const Hit h = trace<DemofoxScene, true, CULL, QV, !ENV>(s_axis, s_qv, zero, D0);                    // :335 rayPos = origin
@@ -976,6 +985,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             DIAG_ADD(5, t_c);
         }
         if (valid) {
+            float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
             px[0] = acc.x;
             px[cs] = acc.y;
             px[2 * cs] = acc.z;
@@ -1211,10 +1221,19 @@ hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* u
     return hipGetLastError();
 }
 
-hipError_t pt_launch_render(const PtJob& job, hipStream_t st, bool count)
+hipError_t pt_launch_render(const PtJob& job_in, hipStream_t st, bool count)
 {
-    if (job.ncols <= 0 || job.nrows <= 0 || job.nframes <= 0) return hipSuccess;
-    if (!job.scene || !job.buf || !job.queue) return hipErrorInvalidValue;
+    if (job_in.ncols <= 0 || job_in.nrows <= 0 || job_in.nframes <= 0) return hipSuccess;
+    if (!job_in.scene || !job_in.buf || !job_in.queue) return hipErrorInvalidValue;
+    // mainImage's frame constants (scalar.cpp:338-347): IEEE f32 '/' here (host, -ffp-contract=off)
+    // == the kernel's correctly rounded div_x / rcp_x
+    PtJob job = job_in;
+    job.cam_W = (float)job.width;
+    job.cam_H = (float)job.height;
+    job.cam_yW = 1.0f / job.cam_W;
+    job.cam_yH = 1.0f / job.cam_H;
+    job.cam_aspect = job.cam_W / job.cam_H;
+    job.cam_yAspect = 1.0f / job.cam_aspect;
     if (job.env) {
         if (job.env_w <= 0 || job.env_h <= 0) return hipErrorInvalidValue;
         switch (job.layout) {
