@@ -133,3 +133,21 @@ def test_config4_full_size_sampled_rows():
     rows = list(range(5, H, 27))
     ref = pyoracle.render(W, H, nframes=S, num_bounces=B, row_start=5, row_stride=27, nrows=len(rows), env=env)
     assert bits_equal(img[rows], ref), mismatch_report(img[rows], ref)
+
+
+def test_env_kernel_quad_cull_counts():
+    """The env kernel runs the culled quad stage too (vertices from the per-axis rows): the six
+    exact quad tests run as a fallback for a tiny fraction of the segments, and the counted work
+    equals the oracle's path statistics."""
+    import torch
+    from cpuperformanceraytracer_amd.device import count_device, set_env_map
+    W, H, S, B = 320, 180, 4, 8
+    env = synthetic_env()
+    set_env_map(env, 0, B)
+    buf = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda:0")
+    cnt = count_device(buf, W, H, frame_first=1, nframes=S, num_bounces=B, use_env=True)
+    img = buf.cpu().numpy().reshape(H, W, 3)
+    ref, oc = pyoracle.render_counted(W, H, nframes=S, num_bounces=B, env=env)
+    assert bits_equal(img, ref), mismatch_report(img, ref)
+    assert cnt["escaped"] == oc["escaped"]
+    assert cnt["quad_fallbacks"] <= 2e-3 * cnt["segments"], cnt
