@@ -411,6 +411,9 @@ static_assert(default_spheres_disjoint(), "the closest-sphere trace needs pairwi
 #ifndef PT_V4_SPHERE_CLOSEST
 #define PT_V4_SPHERE_CLOSEST 1
 #endif
+#ifndef PT_V4_UNIFIED_DIR
+#define PT_V4_UNIFIED_DIR 1   // rejection sampling: one straight-line direction for all three outcomes
+#endif
 #ifndef PT_V4_SPHERE_FORCE_SEQ
 #define PT_V4_SPHERE_FORCE_SEQ 0   // test builds: every candidate ray takes the sequential fallback
 #endif
@@ -696,7 +699,36 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                         const uint32_t s_refr = rng;
                         rng_skip(rng, rejection ? 3 : 2);
                         V3 ndir;
-                        if (!do_refr) {
+                        if (PT_V4_UNIFIED_DIR && rejection) {
+                            // The three outcomes share one shape: a unit vector u drawn from the chosen
+                            // stream, nb = (u +- n) * rcp(sqrt(|u +- n|^2)) (diffuse: n + u; refraction:
+                            // u - n == u + (-n) exactly), and -- for specular and refraction -- the
+                            // reference's fma lerp from a mirror direction R (reflect or refract) towards
+                            // nb.  Evaluated once per lane with per-lane operands instead of as two
+                            // divergent branches; every value is the branch's own, bit for bit.
+                            uint32_t r = do_refr ? s_refr : s_diff;
+                            const V3 u = ruv_rejection(r);
+                            const V3 sn = do_refr ? neg(h.n) : h.n;
+                            const V3 a = u + sn;
+                            const V3 nb = a * rcp(sqrt_(dot(a, a)));
+                            const float vdn = dot(dir, h.n);
+                            // reflect (:861-862): dir - 2 dot(dir, n) n as fma
+                            const float d2 = 2.0f * vdn;
+                            const V3 sd = v3(fma_(-d2, h.n.x, dir.x), fma_(-d2, h.n.y, dir.y), fma_(-d2, h.n.z, dir.z));
+                            // refract (rfrct, mathlib.h:781-789); k of the lanes that do not refract is
+                            // replaced by 1 so that no lane takes sqrt's slow path for a discarded value
+                            const float ior = h.inside ? M.ior : s_mx[h.mat].rior;
+                            const float k = fma_(-ior, ior * fma_(-vdn, vdn, 1.0f), 1.0f);
+                            const float sk = fma_(ior, vdn, sqrt_(do_refr ? k : 1.0f));
+                            V3 rd = v3(fma_(ior, dir.x, -(sk * h.n.x)), fma_(ior, dir.y, -(sk * h.n.y)),
+                                       fma_(ior, dir.z, -(sk * h.n.z)));
+                            rd = k < 0.0f ? v3(0.0f, 0.0f, 0.0f) : rd;
+                            const V3 R = do_refr ? rd : sd;
+                            const float rough = do_refr ? M.refr_rough : M.spec_rough;
+                            const float rsq = rough * rough;
+                            const V3 lr = v3(fma_(rsq, nb.x - R.x, R.x), fma_(rsq, nb.y - R.y, R.y), fma_(rsq, nb.z - R.z, R.z));
+                            ndir = (do_spec || do_refr) ? lr : nb;
+                        } else if (!do_refr) {
                             uint32_t r = s_diff;
                             V3 diffuse;
                             if (rejection) {
