@@ -385,6 +385,32 @@ __device__ __forceinline__ V3 camera_dir(const Camera& cam, float fx, float fy)
     return normalize(v3(tx - 0.0f, ty - 0.0f, cam.cam_dist - 0.0f));                            // :351
 }
 
+// A camera ray (origin 0, D.z > 0) with |D.x| > 0.51 D.z or |D.y| > 0.51 D.z misses every primitive
+// of TestSceneTrace (scalar.cpp:186-287, translated scene):
+//   back wall z = 35, |x|,|y| <= 12.6 needs |D.x|,|D.y| <= 0.36 D.z;
+//   side walls x = +-12.5 (z in [25, 35]) need |D.x| / D.z = 12.5 / z <= 0.5, and |y| <= 12.6 at
+//   z >= 25 then needs |D.y| / D.z <= 0.504;
+//   floor y = -12.45 and ceiling y = 12.5 (z in [25, 35], |x| <= 12.6) need |D.y| / D.z <= 0.5 and
+//   |D.x| / D.z <= 12.6 / 25 = 0.504;  the light (y = 12.4, |x| <= 5, z in [27.5, 32.5]) less;
+//   the spheres (centres (-9 | 0 | 9, -9.5, 30), r = 3) subtend slopes below 0.41 (x) and 0.43 (y).
+// The 0.51 threshold leaves >= 0.006 of slope (0.15 units at z = 25) to every boundary: the
+// reference's rounding moves its triple products / discriminants by ~1e-3 of that scale, far
+// inside it (the culled quad stage's bounds, pt_quadcull.h).  tests/native/check_sky.cpp checks it
+// against the oracle's TestSceneTrace on dense direction grids around the thresholds.
+constexpr float kSkySlope = 0.51f;
+__device__ __forceinline__ bool sky_ray(V3 D)
+{
+    return __builtin_fabsf(D.x) > kSkySlope * D.z || __builtin_fabsf(D.y) > kSkySlope * D.z;
+}
+#ifndef PT_SKY_SKIP
+#define PT_SKY_SKIP 1
+#endif
+constexpr bool SKY_SKIP = PT_SKY_SKIP != 0;
+static_assert(DemofoxScene::qv[0][0][2] == 35.0f && DemofoxScene::qv[3][0][0] == -12.5f && DemofoxScene::qv[4][0][0] == 12.5f &&
+                  DemofoxScene::qv[1][0][1] == -12.45f && DemofoxScene::qv[2][0][1] == 12.5f && DemofoxScene::qv[5][0][1] == 12.4f &&
+                  DemofoxScene::sph[0][0] == -9.0f && DemofoxScene::sph[2][0] == 9.0f && DemofoxScene::sph[0][3] == 3.0f,
+              "sky_ray's bounds are derived for the demofox scene");
+
 // scalar.cpp:332: (uint32_t)(float)x * 1973 + (uint32_t)(float)y * 9277 + (uint32_t)iFrame * 26699, | 1.
 // The pixel coordinates and the frame index are integers below 2^24 (the C ABI rejects larger
 // images and frame counters), so every float round trip is the identity, and each wrapping u32
@@ -778,11 +804,16 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         V3 c_const = zero;        // radiance of every frame for kinds 0 and 1
         V3 P1 = zero, N1 = zero;
         int id1 = 0;
+        const V3 D0 = camera_dir(cam, fx, fy);   // (lanes outside the image: unused values)
+        // A tile whose camera rays all leave the box's silhouette skips their TestSceneTrace: the
+        // result is the reference's miss (sky_ray below), and the trace is the whole cost of such
+        // a tile's phase A -- about half of all 1080p tiles are sky.
+        const bool all_sky = SKY_SKIP && __ballot(valid && !sky_ray(D0)) == 0;
         if (valid) {
             const float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
             acc = v3(px[0], px[cs], px[2 * cs]);
-            const V3 D0 = camera_dir(cam, fx, fy);
-            const Hit h = trace<DemofoxScene, true, CULL, QV, !ENV>(s_axis, s_qv, zero, D0);                    // :335 rayPos = origin
+            const Hit h = all_sky ? Hit{PT_SUPER_FAR, -1, 0, 0}
+                                  : trace<DemofoxScene, true, CULL, QV, !ENV>(s_axis, s_qv, zero, D0);   // :335 rayPos = origin
             if (COUNT) ++n_seg, ++n_prim, n_fb += (unsigned long long)h.fb;
             if (h.best == PT_SUPER_FAR) {                                 // :305-310
                 kind = 0;
