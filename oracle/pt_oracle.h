@@ -126,6 +126,7 @@ void pto4_default_scene(pto4_scene* s);   /* InitializeScene, v4 :1403-1496 */
  * the default scene; counts (optional) forces one thread.  0 on success. */
 int pto4_render(float* buf, const pto4_params* p, const pto4_scene* scene, pto4_counts* counts);
 int pto4_scene_tables(const pto4_scene* scene, float* out, int32_t n);
+float pto4_trace_scene(const pto4_scene* scene, const float P[3], const float D[3], int* mat);   /* v4 :700-718 */
 float pto4_randomf(uint32_t* state);                                          /* mathutils.h:18-26 */
 void pto4_random_unit_vector(uint32_t* state, int rejection, float out[3]);   /* v4 :109 / mathutils.h:33 */
 void pto4_env_sample(const pto_env* env, int32_t env_mode, int32_t random_jitter, const float dir[3],

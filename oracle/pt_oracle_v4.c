@@ -679,6 +679,33 @@ int pto4_render(float* buf, const pto4_params* p, const pto4_scene* scene, pto4_
     return 0;
 }
 
+/* TestSceneTrace (v4 :700-718) of one ray against `scene` (NULL: InitializeScene): the hit distance
+ * (c_superFar on a miss), *mat = the hit object (-1 none).  Checker entry point for the kernel's
+ * sky test (tests/native/check_sky.cpp). */
+static s4 g_def_scene;
+static pthread_once_t g_def_once = PTHREAD_ONCE_INIT;
+static void build_default_scene(void)
+{
+    pto4_scene def;
+    pto4_default_scene(&def);
+    (void)build_scene(&def, &g_def_scene);
+}
+float pto4_trace_scene(const pto4_scene* scene, const float P[3], const float D[3], int* mat)
+{
+    s4 own;
+    const s4* s = &own;
+    if (!scene) {
+        pthread_once(&g_def_once, build_default_scene);
+        s = &g_def_scene;
+    } else if (build_scene(scene, &own)) {
+        return -1.0f;
+    }
+    hit4 h = {0, V4_SUPER_FAR, {0.0f, 0.0f, 0.0f}, -1};
+    scene_trace(s, mk(P[0], P[1], P[2]), mk(D[0], D[1], D[2]), &h);
+    if (mat) *mat = h.dist == V4_SUPER_FAR ? -1 : h.mat;
+    return h.dist;
+}
+
 int pto4_scene_tables(const pto4_scene* scene, float* out, int32_t n)
 {
     /* precomputed quad rows (v0, n, NxV01, NxV20, NxV30, NxV02: 18 f32 per quad) then the material
