@@ -312,7 +312,7 @@ def main() -> None:
 
     # Exact work of the timed launches (deterministic: same frames, counted on a scratch buffer).
     scratch = torch.zeros_like(buf)
-    segs = samples = slots = prim = escaped = 0
+    segs = samples = slots = prim = escaped = sky = 0
     for k in range(K):
         c = count_fn(scratch, Wg, Hg, frame_first=timed_first + k * S, nframes=S, num_bounces=B,
                      row_start=row_start, row_stride=row_stride, nrows=nrows, use_env=wl.env, stream=stream)
@@ -321,6 +321,7 @@ def main() -> None:
         samples += c["samples"]
         slots += c["lane_slots"]
         prim += c.get("primary", c["samples"])
+        sky += c.get("sky_skipped", 0)
     del scratch
 
     output_stage = None
@@ -339,16 +340,18 @@ def main() -> None:
     total_ray_samples = Wg * Hg * S * B * K
     value = total_ray_samples / elapsed
     avg_kernel_s = sum(kernel_ms) / len(kernel_ms) / 1e3
-    if v4:   # every frame traces its own jittered camera ray: executed == reference work
-        flops_launch = flops_launch_ref = RL.v4_launch_flops(segs, samples) / K
-        flop_model = (f"segments x V4_F_SEGMENT + samples x V4_F_SAMPLE; F = {RL.V4_F_SEGMENT}/{RL.V4_F_SAMPLE} "
-                      "(roofline.py, counted by oracle/pt_oracle_v4.c)")
+    if v4:   # every frame traces its own jittered camera ray; all-sky iterations skip the trace
+        flops_launch = RL.v4_launch_flops(segs, samples, sky) / K
+        flops_launch_ref = RL.v4_launch_flops(segs, samples) / K
+        flop_model = (f"segments x V4_F_SEGMENT - sky_skipped x V4_F_SKY_TRACE + samples x V4_F_SAMPLE; F = "
+                      f"{RL.V4_F_SEGMENT}/{RL.V4_F_SKY_TRACE}/{RL.V4_F_SAMPLE} (roofline.py, counted by oracle/pt_oracle_v4.c)")
         kernel_name = "pt_v4_kernel<EQUIRECT, INTERLEAVED>"
     else:
-        flops_launch = RL.launch_flops_exec(segs, prim, samples) / K
+        flops_launch = RL.launch_flops_exec(segs, prim, samples, sky) / K
         flops_launch_ref = RL.launch_flops_ref(segs, prim, samples) / K
         flop_model = ("executed = (segments_ref x F_SEGMENT + samples x F_SAMPLE) - (samples - pixels) x "
-                      f"F_SHARED; F = {RL.F_SEGMENT}/{RL.F_SAMPLE}/{RL.F_SHARED} (roofline.py)")
+                      f"F_SHARED - sky_skipped x F_SKY_TRACE; F = {RL.F_SEGMENT}/{RL.F_SAMPLE}/{RL.F_SHARED}/"
+                      f"{RL.F_SKY_TRACE} (roofline.py)")
         kernel_name = "pt_render_env_kernel<INTERLEAVED>" if wl.env else "pt_render_kernel<INTERLEAVED>"
     achieved_tf = flops_launch / avg_kernel_s / 1e12
     hbm_launch, traffic_src = load_traffic(wl.name)
@@ -380,6 +383,7 @@ def main() -> None:
         "segments_per_sample": segs / samples,
         "ref_segments_per_sample": (segs if v4 else RL.ref_segments(segs, prim, samples)) / samples,
         "simd_lane_efficiency": segs / slots if slots else None,
+        "sky_skipped_traces_per_launch": sky / K,
         "kernel_ms_avg": avg_kernel_s * 1e3,
         "kernel_ms_min": min(kernel_ms),
         "roofline": {

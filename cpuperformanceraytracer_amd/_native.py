@@ -86,7 +86,8 @@ class PtTexture(ctypes.Structure):
 class PtWorkCounts(ctypes.Structure):
     _fields_ = [("segments", ctypes.c_uint64), ("lane_slots", ctypes.c_uint64),
                 ("samples", ctypes.c_uint64), ("escaped", ctypes.c_uint64), ("primary", ctypes.c_uint64),
-                ("quad_fallbacks", ctypes.c_uint64), ("sphere_fallbacks", ctypes.c_uint64)]
+                ("quad_fallbacks", ctypes.c_uint64), ("sphere_fallbacks", ctypes.c_uint64),
+                ("sky_skipped", ctypes.c_uint64)]
 
 
 class PtV4Config(ctypes.Structure):

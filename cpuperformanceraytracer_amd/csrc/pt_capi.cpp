@@ -1006,6 +1006,7 @@ int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
     out->primary = h[PT_CNT_PRIMARY];
     out->quad_fallbacks = h[PT_CNT_FALLBACK];
     out->sphere_fallbacks = 0;
+    out->sky_skipped = h[PT_CNT_SKY];
     return PT_OK;
 }
 
@@ -1237,7 +1238,7 @@ int pt_v4_count_device(const pt_device_job* dj, void* stream, pt_work_counts* ou
     HIP_TRY(hipMemsetAsync(g.dcounters, 0, kCounterSlots * sizeof(unsigned long long), st));
     j.counters = g.dcounters;
     if ((rc = v4_launch(j, st, true))) return rc;
-    unsigned long long h[5];
+    unsigned long long h[6];
     HIP_TRY(hipMemcpyAsync(h, g.dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     out->segments = h[0];
@@ -1247,6 +1248,7 @@ int pt_v4_count_device(const pt_device_job* dj, void* stream, pt_work_counts* ou
     out->primary = out->samples;   // one camera ray per sample (jittered)
     out->quad_fallbacks = 0;
     out->sphere_fallbacks = h[4];
+    out->sky_skipped = h[5];
     return PT_OK;
 }
 

@@ -19,7 +19,8 @@ enum PtCounter : int {
     PT_CNT_ESCAPED = 3,      // paths that ended on a miss
     PT_CNT_PRIMARY = 4,      // camera-ray segments traced (one per pixel)
     PT_CNT_FALLBACK = 5,     // segments whose culled quad stage ran the six exact tests
-    PT_CNT_N = 6,
+    PT_CNT_SKY = 6,          // camera rays whose TestSceneTrace a sky tile skipped (counted in SEGMENTS)
+    PT_CNT_N = 7,
 };
 
 struct PtJob {

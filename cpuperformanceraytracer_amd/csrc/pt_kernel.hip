@@ -755,7 +755,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     const V3 amb = v3(sc->ambient[0], sc->ambient[1], sc->ambient[2]);
     const V3 zero = v3(0.0f, 0.0f, 0.0f), one = v3(1.0f, 1.0f, 1.0f);
 
-    unsigned long long n_seg = 0, n_iter = 0, n_samp = 0, n_esc = 0, n_prim = 0, n_fb = 0;
+    unsigned long long n_seg = 0, n_iter = 0, n_samp = 0, n_esc = 0, n_prim = 0, n_fb = 0, n_sky = 0;
 #if PT_DIAG
 #if PT_DIAG >= 2
     unsigned long long dg[7] = {0, 0, 0, 0, 0, 0, 0};   // A, take, dir, trace, shade, C, tile-total
@@ -814,7 +814,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             acc = v3(px[0], px[cs], px[2 * cs]);
             const Hit h = all_sky ? Hit{PT_SUPER_FAR, -1, 0, 0}
                                   : trace<DemofoxScene, true, CULL, QV, !ENV>(s_axis, s_qv, zero, D0);   // :335 rayPos = origin
-            if (COUNT) ++n_seg, ++n_prim, n_fb += (unsigned long long)h.fb;
+            if (COUNT) ++n_seg, ++n_prim, n_fb += (unsigned long long)h.fb, n_sky += all_sky ? 1ull : 0ull;
             if (h.best == PT_SUPER_FAR) {                                 // :305-310
                 kind = 0;
                 c_const = add(zero, miss_radiance<ENV>(job, amb, D0));
@@ -1041,6 +1041,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             n_esc += __shfl_xor(n_esc, off, 64);
             n_prim += __shfl_xor(n_prim, off, 64);
             n_fb += __shfl_xor(n_fb, off, 64);
+            n_sky += __shfl_xor(n_sky, off, 64);
         }
         if (lane == 0) {
             atomicAdd(&job.counters[PT_CNT_SEGMENTS], n_seg);
@@ -1049,6 +1050,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             atomicAdd(&job.counters[PT_CNT_ESCAPED], n_esc);
             atomicAdd(&job.counters[PT_CNT_PRIMARY], n_prim);
             atomicAdd(&job.counters[PT_CNT_FALLBACK], n_fb);
+            atomicAdd(&job.counters[PT_CNT_SKY], n_sky);
         }
     }
 #if PT_DIAG

@@ -566,7 +566,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     const float W = (float)job.width, H = (float)job.height;
     const float rW = rcp(W), rH = rcp(H);
     const float cam_dist = 1.0f;   // 1 / tanf(c_FOVDegrees * 0.5f * c_pi / 180.0f) == 1.0f exactly (InitializeCamera :1500)
-    unsigned long long n_seg = 0, n_esc = 0, n_slots = 0, n_fb = 0;
+    unsigned long long n_seg = 0, n_esc = 0, n_slots = 0, n_fb = 0, n_sky = 0;
 
     // persistent waves: 8x8 tiles from the launch's queue (pt_tile_queue.h), longest first when the
     // geometry has a schedule
@@ -667,7 +667,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                 // one iteration of GetColorForRay's bounce loop (:733-909)
                 int fb = 0;
                 const Hit h = all_sky ? Hit{kSuperFar, v3(0.0f, 0.0f, 0.0f), false, 0} : trace<DEF>(sc, pos, dir, s_sc, fb);
-                if (COUNT) ++n_seg, n_fb += (unsigned long long)fb;
+                if (COUNT) ++n_seg, n_fb += (unsigned long long)fb, n_sky += all_sky ? 1ull : 0ull;
                 const bool miss = h.dist == kSuperFar;
                 bool done = false;
                 if (miss) {
@@ -869,12 +869,14 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
             n_seg += __shfl_down(n_seg, off);
             n_esc += __shfl_down(n_esc, off);
             n_fb += __shfl_down(n_fb, off);
+            n_sky += __shfl_down(n_sky, off);
         }
         if (lane == 0) {
             atomicAdd(&job.counters[0], n_seg);
             atomicAdd(&job.counters[2], n_esc);
             atomicAdd(&job.counters[3], n_slots);
             atomicAdd(&job.counters[4], n_fb);
+            atomicAdd(&job.counters[5], n_sky);
         }
     }
 }

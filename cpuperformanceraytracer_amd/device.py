@@ -81,7 +81,7 @@ def count_device(buf, width: int, height: int, *, frame_first: int, nframes: int
     out = N.PtWorkCounts()
     N.check(N.load().pt_count_device(ctypes.byref(job), _stream(stream), ctypes.byref(out)), "pt_count_device")
     return {"segments": out.segments, "lane_slots": out.lane_slots, "samples": out.samples, "escaped": out.escaped,
-            "primary": out.primary, "quad_fallbacks": out.quad_fallbacks}
+            "primary": out.primary, "quad_fallbacks": out.quad_fallbacks, "sky_skipped": out.sky_skipped}
 
 
 def render_v4_device(buf, width: int, height: int, *, frame_first: int, nframes: int, num_bounces: int = 8,
@@ -103,4 +103,4 @@ def count_v4_device(buf, width: int, height: int, *, frame_first: int, nframes: 
     out = N.PtWorkCounts()
     N.check(N.load().pt_v4_count_device(ctypes.byref(job), _stream(stream), ctypes.byref(out)), "pt_v4_count_device")
     return {"segments": out.segments, "lane_slots": out.lane_slots, "samples": out.samples, "escaped": out.escaped,
-            "sphere_fallbacks": out.sphere_fallbacks}
+            "sphere_fallbacks": out.sphere_fallbacks, "sky_skipped": out.sky_skipped}

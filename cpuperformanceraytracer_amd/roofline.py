@@ -18,6 +18,9 @@ Two figures per launch:
                         bounce-0 shading except the new direction are identical for every frame
                         of a pixel and evaluated once, so
                         FLOP_exec = FLOP_ref - (samples - pixels) * F_SHARED.
+  sky tiles             a tile whose camera rays all miss the scene skips their TestSceneTrace
+                        (pt_kernel.hip sky_ray, counted on the device as sky_skipped); FLOP_exec
+                        subtracts F_SKY_TRACE per skipped trace.
 The roofline fraction is reported on FLOP_exec (work the hardware did), never on FLOP_ref.
 """
 
@@ -33,6 +36,11 @@ T_SEGMENT = 1.14
 # trace + bounce-0 shading without RUV/normalize), 1920x1080 8 bounces rows 0::8 / 3::8 (402.47 /
 # 402.52), 3840x2160 rows 5::16 (402.37).
 F_SHARED = 402.45
+
+# Mean reference FLOP of the TestSceneTrace of a camera ray in a sky tile (the work a skipped trace
+# would have been), the oracle's accounting (pto_sky_skipped) over the bench geometries: 1920x1080
+# 347.09, 3840x2160 347.09, the weak-scaling shards 346.96-347.11 (tests/test_flops.py).
+F_SKY_TRACE = 347.1
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters").
 PEAK_FP32_TFLOPS = 157.3   # FP32 vector (= FP32 MFMA) peak, FMA counted as 2
@@ -54,8 +62,8 @@ def launch_flops_ref(traced: int, camera_rays: int, samples: int) -> float:
     return ref_segments(traced, camera_rays, samples) * F_SEGMENT + samples * F_SAMPLE
 
 
-def launch_flops_exec(traced: int, camera_rays: int, samples: int) -> float:
-    return launch_flops_ref(traced, camera_rays, samples) - (samples - camera_rays) * F_SHARED
+def launch_flops_exec(traced: int, camera_rays: int, samples: int, sky_skipped: int = 0) -> float:
+    return launch_flops_ref(traced, camera_rays, samples) - (samples - camera_rays) * F_SHARED - sky_skipped * F_SKY_TRACE
 
 
 # ---- v4 renderer (demofox_path_tracing_optimization_v4.cpp) ------------------------------------
@@ -67,7 +75,13 @@ def launch_flops_exec(traced: int, camera_rays: int, samples: int) -> float:
 V4_F_SEGMENT = 495.9
 # Per sample: camera ray 23 + c_numRendersPerFrame scale 6 + fused accumulate 9 (exact).
 V4_F_SAMPLE = 38.0
+# A camera ray that misses everything costs the reference 4 x 53 (quads) + 7 x 25 (spheres) FLOP in
+# TestSceneTrace (the v4 oracle's accounting, tests/test_flops.py): the work of a skipped trace
+# (pt_v4.hip sky_ray_v4).  Its shading (the env term) is still executed.
+V4_F_SKY_TRACE = 387.0
 
 
-def v4_launch_flops(segments: int, samples: int) -> float:
-    return segments * V4_F_SEGMENT + samples * V4_F_SAMPLE
+def v4_launch_flops(segments: int, samples: int, sky_skipped: int = 0) -> float:
+    """Reference work; with sky_skipped (camera rays of all-sky iterations whose TestSceneTrace the
+    kernel skipped, pt_v4.hip sky_ray_v4) a lower bound of the executed work."""
+    return segments * V4_F_SEGMENT - sky_skipped * V4_F_SKY_TRACE + samples * V4_F_SAMPLE

@@ -101,6 +101,8 @@ typedef struct pt_work_counts {
                                  /* exact quad tests ran (diffuse kernel; pt_quadcull.h)           */
     uint64_t sphere_fallbacks;   /* segments whose closest-sphere stage fell back to the sequential */
                                  /* sphere tests (v4 kernel, default scene)                        */
+    uint64_t sky_skipped;        /* camera-ray segments (counted in `segments`) whose TestSceneTrace */
+                                 /* was skipped because the whole tile/iteration was sky           */
 } pt_work_counts;
 
 /* --- lifecycle -------------------------------------------------------------------------------- */

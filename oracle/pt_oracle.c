@@ -191,6 +191,49 @@ float pto_trace_scene(const float P[3], const float D[3], float n_out[3], int* i
     return h.dist;
 }
 
+/* The sky tiles of the diffuse kernel (csrc/pt_kernel.hip sky_ray): 8x8 tiles of the p->nrows x
+ * p->width buffer (rows p->row_start + r * p->row_stride) whose camera rays all have |D.x| or |D.y|
+ * > slope * D.z skip those rays' TestSceneTrace.  Returns how many camera rays that is and, in
+ * *flops, what their TestSceneTrace costs the reference (the counted instantiation's accounting) --
+ * the work the kernel does not execute, for the bench's roofline (roofline.py). */
+uint64_t pto_sky_skipped(const pto_params* p, float slope, uint64_t* flops)
+{
+    pthread_once(&g_once, pto_init_scene);
+    const float W = (float)p->width, H = (float)p->height, aspect = W / H;
+    uint64_t n = 0, fl = 0;
+    pto_counts c;
+    pto_counts* const saved = g_cnt;
+    for (int32_t ty = 0; ty < (p->nrows + 7) / 8; ++ty)
+        for (int32_t tx = 0; tx < (p->width + 7) / 8; ++tx) {
+            float D[64][3];
+            int m = 0, sky = 1;
+            for (int k = 0; k < 64 && sky; ++k) {
+                const int32_t x = tx * 8 + (k & 7), r = ty * 8 + (k >> 3);
+                if (x >= p->width || r >= p->nrows) continue;
+                const float fx = (float)x, fy = (float)(p->height - 1 - (p->row_start + r * p->row_stride));
+                float t[3] = {(fx / W) * 2.0f - 1.0f, ((fy / H) * 2.0f - 1.0f) / aspect, g_cam_dist - 0.0f};
+                const float inv = 1.0f / sqrtf((t[0] * t[0] + t[1] * t[1]) + t[2] * t[2]);
+                D[m][0] = t[0] * inv; D[m][1] = t[1] * inv; D[m][2] = t[2] * inv;
+                sky = fabsf(D[m][0]) > slope * D[m][2] || fabsf(D[m][1]) > slope * D[m][2];
+                ++m;
+            }
+            if (!sky || m == 0) continue;
+            for (int k = 0; k < m; ++k) {
+                memset(&c, 0, sizeof c);
+                g_cnt = &c;
+                hit_t_counted h;
+                h.dist = PTO_SUPER_FAR;
+                const float P[3] = {0.0f, 0.0f, 0.0f};
+                scene_counted(P, D[k], &h);
+                fl += c.flops_segment;
+            }
+            n += (uint64_t)m;
+        }
+    g_cnt = saved;
+    if (flops) *flops = fl;
+    return n;
+}
+
 static int pto_check(const float* buf, const pto_params* p)
 {
     (void)ruv_unused_guard;

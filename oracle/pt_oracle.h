@@ -75,6 +75,7 @@ uint32_t pto_seed(uint32_t x, uint32_t y, uint32_t frame); /* scalar.cpp:332    
 /* TestSceneTrace pieces (scalar.cpp:186-287) for the product's quad-culling check. */
 float pto_trace_quads(const float P[3], const float D[3], int* id, int* flipped);
 float pto_trace_scene(const float P[3], const float D[3], float n_out[3], int* id);
+uint64_t pto_sky_skipped(const pto_params* p, float slope, uint64_t* flops);   /* sky tiles (pt_kernel.hip) */
 void pto_env_sample(const pto_env* env, const float dir[3], float out3[3]); /* texture.cpp:101-139 */
 
 /* Output stage (pt_oracle_output.c): ACES + fast sRGB + 8-bit pack, v4 :144-187, :1260-1331. */
@@ -127,6 +128,7 @@ void pto4_default_scene(pto4_scene* s);   /* InitializeScene, v4 :1403-1496 */
 int pto4_render(float* buf, const pto4_params* p, const pto4_scene* scene, pto4_counts* counts);
 int pto4_scene_tables(const pto4_scene* scene, float* out, int32_t n);
 float pto4_trace_scene(const pto4_scene* scene, const float P[3], const float D[3], int* mat);   /* v4 :700-718 */
+float pto4_trace_scene_flops(const pto4_scene* scene, const float P[3], const float D[3], int* mat, uint64_t* flops);
 float pto4_randomf(uint32_t* state);                                          /* mathutils.h:18-26 */
 void pto4_random_unit_vector(uint32_t* state, int rejection, float out[3]);   /* v4 :109 / mathutils.h:33 */
 void pto4_env_sample(const pto_env* env, int32_t env_mode, int32_t random_jitter, const float dir[3],

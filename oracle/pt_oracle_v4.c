@@ -690,7 +690,13 @@ static void build_default_scene(void)
     pto4_default_scene(&def);
     (void)build_scene(&def, &g_def_scene);
 }
+float pto4_trace_scene_flops(const pto4_scene* scene, const float P[3], const float D[3], int* mat, uint64_t* flops);
 float pto4_trace_scene(const pto4_scene* scene, const float P[3], const float D[3], int* mat)
+{
+    return pto4_trace_scene_flops(scene, P, D, mat, NULL);
+}
+/* ... and the reference's f32 FLOP count of that TestSceneTrace (the instrumented accounting) */
+float pto4_trace_scene_flops(const pto4_scene* scene, const float P[3], const float D[3], int* mat, uint64_t* flops)
 {
     s4 own;
     const s4* s = &own;
@@ -701,7 +707,8 @@ float pto4_trace_scene(const pto4_scene* scene, const float P[3], const float D[
         return -1.0f;
     }
     hit4 h = {0, V4_SUPER_FAR, {0.0f, 0.0f, 0.0f}, -1};
-    scene_trace(s, mk(P[0], P[1], P[2]), mk(D[0], D[1], D[2]), &h);
+    const uint64_t fl = scene_trace(s, mk(P[0], P[1], P[2]), mk(D[0], D[1], D[2]), &h);
+    if (flops) *flops = fl;
     if (mat) *mat = h.dist == V4_SUPER_FAR ? -1 : h.mat;
     return h.dist;
 }

@@ -312,3 +312,30 @@ def render_simd_tiled(width: int, height: int, num_tiles_x: int, num_tiles_y: in
     if rc:
         raise ValueError(f"ptc_render_simd_tiled failed ({rc})")
     return buf
+
+
+def sky_skipped(width: int, height: int, *, row_start: int = 0, row_stride: int = 1, nrows: int | None = None,
+                slope: float = 0.51) -> tuple[int, int]:
+    """(camera rays, their TestSceneTrace flops) that the diffuse kernel's sky tiles skip (pto_sky_skipped)."""
+    nrows = height if nrows is None else nrows
+    p, keep = _params(width, height, row_start, row_stride, nrows, 1, 1, 8, (0.1, 0.1, 0.1), None, 1)
+    fl = ctypes.c_uint64(0)
+    L = load()
+    L.pto_sky_skipped.restype = ctypes.c_uint64
+    L.pto_sky_skipped.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.POINTER(ctypes.c_uint64)]
+    n = L.pto_sky_skipped(ctypes.byref(p), slope, ctypes.byref(fl))
+    del keep
+    return int(n), int(fl.value)
+
+
+def trace4(P, D) -> tuple[float, int, int]:
+    """v4 TestSceneTrace of one ray in the default scene: (distance, material, reference flops)
+    (pto4_trace_scene_flops)."""
+    L = load()
+    f3 = ctypes.c_float * 3
+    L.pto4_trace_scene_flops.restype = ctypes.c_float
+    L.pto4_trace_scene_flops.argtypes = [ctypes.c_void_p, f3, f3, ctypes.POINTER(ctypes.c_int),
+                                         ctypes.POINTER(ctypes.c_uint64)]
+    mat, fl = ctypes.c_int(-1), ctypes.c_uint64(0)
+    d = L.pto4_trace_scene_flops(None, f3(*P), f3(*D), ctypes.byref(mat), ctypes.byref(fl))
+    return float(d), int(mat.value), int(fl.value)

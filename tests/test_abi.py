@@ -96,7 +96,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(N.PtBufferInfo) == 8 + 3 * 4 + 4      # pointer + 3 ints (+ tail pad)
     assert ctypes.sizeof(N.PtTileInfo) == 8 * 4
     assert ctypes.sizeof(N.PtDeviceJob) == 8 + 9 * 4 + 4
-    assert ctypes.sizeof(N.PtWorkCounts) == 7 * 8
+    assert ctypes.sizeof(N.PtWorkCounts) == 8 * 8
 
 
 def test_reference_shaped_host_compiles_and_links(tmp_path):

@@ -44,3 +44,24 @@ def test_v4_flop_constants(rs):
     f_seg = (c["flops"] - RL.V4_F_SAMPLE * c["samples"]) / c["segments"]
     assert abs(f_seg - RL.V4_F_SEGMENT) / RL.V4_F_SEGMENT < 0.005, f_seg
     assert RL.v4_launch_flops(c["segments"], c["samples"]) == pytest.approx(c["flops"], rel=0.005)
+
+
+@pytest.mark.parametrize("w,h,rs,st", [(1920, 1080, 0, 1), (3840, 2160, 0, 1), (2712, 1526, 0, 2), (5432, 3056, 7, 8)])
+def test_sky_trace_constant(w, h, rs, st):
+    """F_SKY_TRACE: the mean reference FLOP of the camera-ray traces the diffuse kernel's sky tiles skip
+    (bench workloads and weak-scaling shards), within 0.2 %."""
+    n, fl = pyoracle.sky_skipped(w, h, row_start=rs, row_stride=st, nrows=(h - rs + st - 1) // st)
+    assert n > 0
+    assert abs(fl / n - RL.F_SKY_TRACE) / RL.F_SKY_TRACE < 0.002, fl / n
+    # the executed-work model subtracts exactly that
+    assert RL.launch_flops_exec(100, 10, 10, sky_skipped=3) == pytest.approx(
+        RL.launch_flops_exec(100, 10, 10) - 3 * RL.F_SKY_TRACE)
+
+
+def test_v4_sky_trace_constant():
+    """V4_F_SKY_TRACE: a v4 camera ray that misses the scene costs the reference exactly that much."""
+    for D in [(0.0, -0.9, -0.4359), (0.8, 0.1, -0.5916), (-0.3, 0.2, -0.9327), (0.0, 0.0, -1.0)]:
+        d, mat, fl = pyoracle.trace4((0.0, 0.0, 40.0), D)
+        assert d == 10000.0 and mat == -1 and fl == RL.V4_F_SKY_TRACE
+    assert RL.v4_launch_flops(10, 4, sky_skipped=2) == pytest.approx(
+        10 * RL.V4_F_SEGMENT - 2 * RL.V4_F_SKY_TRACE + 4 * RL.V4_F_SAMPLE)

@@ -194,6 +194,11 @@ def test_quad_cull_fallback_rate_full_hd():
     buf = torch.zeros(h * w * 3, dtype=torch.float32, device="cuda")
     cnt = count_device(buf, w, h, frame_first=1, nframes=2, num_bounces=8)
     assert 0 < cnt["quad_fallbacks"] <= 1e-3 * cnt["segments"], cnt
+    # sky tiles (pt_kernel.hip sky_ray) skip their camera rays' TestSceneTrace: about half the
+    # pixels of this view, never more than the camera rays -- exactly the 8x8 tiles the oracle's
+    # restatement of the test classifies as sky (pto_sky_skipped, the roofline's F_SKY_TRACE count)
+    assert 0.3 * w * h < cnt["sky_skipped"] <= cnt["primary"], cnt
+    assert cnt["sky_skipped"] == pyoracle.sky_skipped(w, h)[0]
 
 
 @pytest.mark.parametrize("b", [0, 1])

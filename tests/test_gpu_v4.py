@@ -118,6 +118,8 @@ def test_v4_full_1080p_8spp():
     # the closest-sphere stage (pt_v4.hip) decides almost every segment; the sequential sphere
     # tests run as a fallback only, and the image above is still bit-identical
     assert cnt["sphere_fallbacks"] <= 1e-3 * cnt["segments"], cnt
+    # all-sky iterations (pt_v4.hip sky_ray_v4) skip TestSceneTrace for their camera rays
+    assert 0 < cnt["sky_skipped"] < cnt["samples"], cnt
 
 
 def test_v4_counts_match_oracle():
