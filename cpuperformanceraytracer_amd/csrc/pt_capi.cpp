@@ -74,6 +74,7 @@ struct State {
     unsigned long long* dcounters = nullptr;
     unsigned int* dqueue = nullptr;     // ring of kQueueRing tile-queue blocks (PT_QUEUE_WORDS each)
     unsigned queue_next = 0;
+    bool queue_pre_zeroed = false;      // the last launch's kernel zeroed ring slot queue_next % kQueueRing
     // per ring slot: the stream of the last launch that used it and an event recorded after that
     // launch; a launch on another stream waits for it before re-zeroing the slot
     hipStream_t queue_stream[kQueueRing] = {};
@@ -313,6 +314,7 @@ Sched* find_sched(const SchedKey& key, hipStream_t st)
 struct LaunchSched {
     unsigned slot = 0;   // tile-queue ring slot (queue_done after the launch)
     unsigned int* queue = nullptr;
+    unsigned int* queue_next = nullptr;   // the next ring slot, zeroed by this launch's kernel
     const uint32_t* order = nullptr;
     const uint32_t* units = nullptr;
     const uint32_t* nunits = nullptr;
@@ -339,21 +341,34 @@ int use_sched(const SchedKey& key, hipStream_t st, LaunchSched* ls)
         s->have_cost = true;
         ++s->launches;
     }
-    // The slot is re-zeroed by this launch (a memset on `st`).  Launches on one stream are
-    // ordered; when the slot's previous user ran on another stream, wait for its event first.
+    // Ring slots are used in order.  Each render kernel zeroes the NEXT slot's counters at its start,
+    // so a launch after a launched kernel finds its slot zero -- ordered after that kernel, on the
+    // same stream or by its event -- and otherwise zeroes it with a memset on `st`.  When a slot's
+    // previous user ran on another stream, wait for its event before the slot is used or zeroed.
     ls->slot = g.queue_next++ % kQueueRing;
+    const unsigned prev = (ls->slot + kQueueRing - 1) % kQueueRing, next = (ls->slot + 1) % kQueueRing;
     if (g.queue_event[ls->slot] && g.queue_stream[ls->slot] != st)
         HIP_TRY(hipStreamWaitEvent(st, g.queue_event[ls->slot], 0));
     ls->queue = g.dqueue + (size_t)ls->slot * PT_QUEUE_WORDS;
+    if (g.queue_pre_zeroed) {
+        if (g.queue_stream[prev] != st) HIP_TRY(hipStreamWaitEvent(st, g.queue_event[prev], 0));
+    } else {
+        HIP_TRY(hipMemsetAsync(ls->queue, 0, PT_QUEUE_WORDS * sizeof(unsigned), st));
+    }
+    g.queue_pre_zeroed = false;   // (set by queue_done once this launch's kernel is enqueued)
+    if (g.queue_event[next] && g.queue_stream[next] != st) HIP_TRY(hipStreamWaitEvent(st, g.queue_event[next], 0));
+    ls->queue_next = g.dqueue + (size_t)next * PT_QUEUE_WORDS;
     return PT_OK;
 }
 
-// After the launch that used ring slot `slot` was enqueued on `st`.
-int queue_done(unsigned slot, hipStream_t st)
+// After the launch that used ring slot `slot` was enqueued on `st`; `zeroed_next`: its kernel ran
+// (a launch with nothing to render returns without one) and zeroes the next slot.
+int queue_done(unsigned slot, hipStream_t st, bool zeroed_next)
 {
     if (!g.queue_event[slot]) HIP_TRY(hipEventCreateWithFlags(&g.queue_event[slot], hipEventDisableTiming));
     HIP_TRY(hipEventRecord(g.queue_event[slot], st));
     g.queue_stream[slot] = st;
+    g.queue_pre_zeroed = zeroed_next;
     return PT_OK;
 }
 
@@ -363,13 +378,14 @@ int launch(PtJob j, hipStream_t st, bool count)
     int rc;
     if ((rc = use_sched(sched_key(j), st, &ls))) return rc;
     j.queue = ls.queue;
+    j.queue_next = ls.queue_next;
     j.order = ls.order;
     j.units = ls.units;
     j.nunits = ls.nunits;
     j.cost = ls.cost;
     hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
-    return queue_done(ls.slot, st);
+    return queue_done(ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_render's early return)
 }
 
 void unpin()
@@ -665,13 +681,14 @@ int v4_launch(PtV4Job j, hipStream_t st, bool count)
     int rc;
     if ((rc = use_sched(sched_key(j), st, &ls))) return rc;
     j.queue = ls.queue;
+    j.queue_next = ls.queue_next;
     j.order = ls.order;
     j.units = ls.units;
     j.nunits = ls.nunits;
     j.cost = ls.cost;
     hipError_t e = pt_launch_v4(j, g.v4scene, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "v4 render launch failed: %s", hipGetErrorString(e));
-    return queue_done(ls.slot, st);
+    return queue_done(ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_v4's early return)
 }
 
 }  // namespace
@@ -727,6 +744,8 @@ int pt_init(const pt_config* cfg)
     if (hipMalloc(&g.dscene, sizeof(PtScene)) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc(scene) failed");
     HIP_TRY(hipMemcpy(g.dscene, &g.scene, sizeof(PtScene), hipMemcpyHostToDevice));
     g.frame = 0;
+    g.queue_next = 0;
+    g.queue_pre_zeroed = false;
     g.inited = true;
     return PT_OK;
 }

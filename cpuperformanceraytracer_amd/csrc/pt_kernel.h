@@ -39,7 +39,8 @@ struct PtJob {
     const float* env;           // device env map (H x W x 3), nullptr => ambient
     int32_t env_w, env_h;
     unsigned long long* counters;  // PT_CNT_N u64, COUNT build only
-    unsigned int* queue;           // PT_QUEUE_WORDS tile-queue words (zeroed on the stream before each launch)
+    unsigned int* queue;           // PT_QUEUE_WORDS tile-queue words, zero at the launch's start
+    unsigned int* queue_next;      // the next launch's words, zeroed by this launch (nullptr: none)
     const uint32_t* order;         // tile schedule: position -> tile (a permutation), nullptr = identity
     const uint32_t* units;         // schedule runs: unit k = positions [units[k], units[k+1]), nullptr = one tile each
     const uint32_t* nunits;        // device word: number of units (with units)

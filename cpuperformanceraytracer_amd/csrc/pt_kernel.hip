@@ -765,6 +765,9 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     unsigned long long n_tiles_diag = 0;
 #endif
 
+    // the next launch's queue counters start at zero: this launch clears them (pt_capi.cpp use_sched;
+    // it saves the stream a 1-KiB fill before every launch)
+    if (job.queue_next && blockIdx.x == 0 && threadIdx.x < PT_NQUEUES) job.queue_next[threadIdx.x * 32u] = 0u;
     // tiles from the launch's queue (pt_tile_queue.h)
     constexpr uint32_t kNone = PtTileQueue<kWavesPerBlock>::kNone;
     PtTileQueue<kWavesPerBlock> tq(job.queue, job.order, job.units, job.nunits, total_tiles, wv);
@@ -1107,8 +1110,6 @@ hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 {
     constexpr int wpb = waves_per_block<ENV>();
     const unsigned tiles = (unsigned)((job.ncols + 7) / 8) * (unsigned)((job.nrows + 7) / 8);
-    hipError_t e = hipMemsetAsync(job.queue, 0, PT_QUEUE_WORDS * sizeof(unsigned), st);
-    if (e != hipSuccess) return e;
     if (count) {
         auto k = kernel_of<LAYOUT, ENV, true>();
         const unsigned blocks = (unsigned)std::min<long>(pt_resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);

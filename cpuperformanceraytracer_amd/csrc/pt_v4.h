@@ -54,7 +54,8 @@ struct PtV4Job {
     unsigned long long* counters;   // COUNT launches: [0] segments, [1] samples, [2] escaped, [3] lane slots
     int32_t default_scene;          // the scene is InitializeScene's: literal-geometry instantiation
     // persistent-grid tile queue and schedule (pt_tile_queue.h; as PtJob, pt_kernel.h)
-    unsigned int* queue;            // PT_QUEUE_WORDS words, zeroed on the stream before each launch
+    unsigned int* queue;            // PT_QUEUE_WORDS words, zero at the launch's start
+    unsigned int* queue_next;       // the next launch's words, zeroed by this launch (nullptr: none)
     const uint32_t* order;          // tile schedule (longest first) or nullptr
     const uint32_t* units;
     const uint32_t* nunits;

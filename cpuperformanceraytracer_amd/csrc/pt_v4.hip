@@ -556,6 +556,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (job.queue_next && blockIdx.x == 0 && threadIdx.x < PT_NQUEUES) job.queue_next[threadIdx.x * 32u] = 0u;   // (as pt_kernel.hip)
     const int tiles_x = (job.ncols + 7) >> 3;
     const int ntiles = tiles_x * ((job.nrows + 7) >> 3);
     float* const col = s_col[wv];
@@ -886,8 +887,6 @@ hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool 
 {
     const int tiles = ((j.ncols + 7) / 8) * ((j.nrows + 7) / 8);
     const dim3 block(64 * kWaves);
-    hipError_t e = hipMemsetAsync(j.queue, 0, PT_QUEUE_WORDS * sizeof(unsigned), st);
-    if (e != hipSuccess) return e;
     auto go = [&](auto kern) {   // persistent grid: the resident blocks, at most one tile per wave
         const long blocks = std::min<long>(pt_resident_blocks(kern, 64 * kWaves), (tiles + kWaves - 1) / kWaves);
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), block, 0, st, j, sc);
