@@ -90,6 +90,7 @@ struct State {
     size_t pinned_bytes = 0;
     hipStream_t s_in = nullptr, s_out = nullptr;
     hipEvent_t ev_in[kBands] = {}, ev_done[kBands] = {};
+    hipEvent_t ev_q = nullptr;   // work queues: orders banded copies against g.stream
     // output stage scratch (host-buffer pt_tonemap)
     float* dtone_in = nullptr;
     size_t dtone_in_cap = 0;
@@ -735,6 +736,7 @@ int pt_init(const pt_config* cfg)
         HIP_TRY(hipEventCreateWithFlags(&g.ev_in[k], hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&g.ev_done[k], hipEventDisableTiming));
     }
+    HIP_TRY(hipEventCreateWithFlags(&g.ev_q, hipEventDisableTiming));
     if (hipMalloc(&g.dcounters, kCounterSlots * sizeof(unsigned long long)) != hipSuccess)
         return fail(PT_ENOMEM, "hipMalloc(counters) failed");
     if (hipMalloc(&g.dqueue, (size_t)kQueueRing * PT_QUEUE_WORDS * sizeof(unsigned)) != hipSuccess)
@@ -771,6 +773,7 @@ void pt_shutdown(void)
         if (g.ev_in[k]) (void)hipEventDestroy(g.ev_in[k]);
         if (g.ev_done[k]) (void)hipEventDestroy(g.ev_done[k]);
     }
+    if (g.ev_q) (void)hipEventDestroy(g.ev_q);
     if (g.s_in) (void)hipStreamDestroy(g.s_in);
     if (g.s_out) (void)hipStreamDestroy(g.s_out);
     if (g.stream) (void)hipStreamDestroy(g.stream);
@@ -1340,6 +1343,39 @@ int run_queue(pt_work_queue* q, bool wait)
         }
         const size_t bytes = (size_t)b.width * b.height * 3 * sizeof(float);
         const size_t tlen = (size_t)tw * th * 3 * sizeof(float);
+        if (full && (g.cfg.flags & PT_FLAG_PIN_HOST) && !(g.cfg.flags & PT_FLAG_DEFER_READBACK)) {
+            // A whole frame of tiles with PT_FLAG_PIN_HOST: the frame calls' band pipeline (bands of
+            // whole tile rows, upload / render / download overlapped on three streams).  The bands'
+            // copies run on s_in / s_out, so they are ordered after the work already queued on
+            // g.stream (an earlier buffer's download from the mirror), and g.stream -- which the
+            // completion calls synchronise -- after the last download.
+            HIP_TRY(hipEventRecord(g.ev_q, g.stream));
+            HIP_TRY(hipStreamWaitEvent(g.s_in, g.ev_q, 0));
+            bool banded = false;
+            if (v4) {
+                PtV4Job j = v4_job(nullptr, b.width, b.height);
+                j.layout = PT_LAYOUT_TILED_PLANAR8;
+                j.tile_w = tw;
+                j.tile_h = th;
+                j.frame_first = g.v4_frame;
+                if ((rc = v4_use_env(j))) return rc;
+                rc = render_bands(b.data, j, th, [](const PtV4Job& bj) { return v4_launch(bj, g.stream, false); }, &banded);
+            } else {
+                pt_tile_info t = t0;
+                t.tile_min_x = 0;
+                t.tile_min_y = 0;
+                PtJob j = tile_job(&b, &t, env);
+                j.ncols = b.width;
+                j.nrows = b.height;
+                rc = render_bands(b.data, j, th, [](const PtJob& bj) { return launch(bj, g.stream, false); }, &banded);
+            }
+            if (rc) return rc;
+            if (banded) {
+                HIP_TRY(hipEventRecord(g.ev_q, g.s_out));
+                HIP_TRY(hipStreamWaitEvent(g.stream, g.ev_q, 0));
+                continue;
+            }
+        }
         if (full) {
             if ((rc = stage_in(b.data, bytes, 0, bytes))) return rc;
         } else {

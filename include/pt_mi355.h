@@ -42,8 +42,10 @@ extern "C" {
 #define PT_FLAG_PIN_HOST 2u        /* page-lock the caller's frame buffer (hipHostRegister; kept until */
                                    /* pt_unpin_host, pt_shutdown, ReinitializeRenderTileData or      */
                                    /* another buffer is passed) and overlap its PCIe transfers with  */
-                                   /* rendering, in row bands (same results).  Free a pinned buffer  */
-                                   /* only after pt_unpin_host(buf) (a Resize that reallocates it).  */
+                                   /* rendering, in row bands (same results) -- frame calls, and work */
+                                   /* queues whose entries are a whole frame of tiles of one buffer. */
+                                   /* Free a pinned buffer only after pt_unpin_host(buf) (a Resize   */
+                                   /* that reallocates it).                                          */
 
 /* Runtime form of the reference's compile-time configuration (global_preprocessor_flags.h and the
  * file-scope constants of demofox_path_tracing_scalar.cpp:6-25). */

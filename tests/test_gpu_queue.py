@@ -126,3 +126,75 @@ def test_queue_errors():
         pt.CompleteAllWork(q)
     with pytest.raises(N.PtError):
         pt.MakeWorkQueue(7)
+
+
+def test_queue_pinned_full_frames_and_partial():
+    """PT_FLAG_PIN_HOST: a whole frame of tiles takes the frame calls' band pipeline (bands of whole
+    tile rows uploaded, rendered and downloaded on three overlapping streams), synchronous and
+    async; a partial queue on top keeps the per-tile path.  Bit-identical to the oracle."""
+    pt.init(num_bounces=8, pin_host=True)
+    buf = np.zeros(W * H * 3, np.float32)
+    q = pt.MakeWorkQueue()
+    bi = pt.RenderBufferInfo(buf, W, H, 3)
+    for i in range(3):
+        pt.BeginFrame()
+        for t in _tiles():
+            pt.AddWorkQueueEntry(q, bi, t)
+        if i == 1:
+            q.complete(wait=False)
+            q.wait()
+        else:
+            pt.CompleteAllWork(q)
+    ref = po.render(W, H, nframes=3, num_bounces=8)
+    got = tiled_to_interleaved(buf, W, H, TW, TH)
+    assert bits_equal(got, ref), mismatch_report(got, ref)
+    pt.BeginFrame()   # frame 4, a partial queue
+    chosen = _tiles()[2::9]
+    for t in chosen:
+        pt.AddWorkQueueEntry(q, bi, t)
+    pt.CompleteAllWork(q)
+    full = po.render(W, H, frame_first=4, nframes=1, num_bounces=8, buf=ref.copy())
+    for t in chosen:
+        ref[t.TileMinY:t.TileMaxY + 1, t.TileMinX:t.TileMaxX + 1] = full[t.TileMinY:t.TileMaxY + 1,
+                                                                         t.TileMinX:t.TileMaxX + 1]
+    got = tiled_to_interleaved(buf, W, H, TW, TH)
+    assert bits_equal(got, ref), mismatch_report(got, ref)
+    pt.unpin_host(buf)
+
+
+def test_queue_pinned_two_buffers_and_v4():
+    """PIN_HOST with two buffers in one queue (each re-pinned in turn; the second's uploads wait for
+    the first's downloads from the shared device mirror) and a pinned v4 queue."""
+    pt.init(num_bounces=8, pin_host=True)
+    env = np.random.default_rng(7).random((32, 64, 3), dtype=np.float32) + 0.01
+    pt.set_env_map(env)
+    a = np.zeros(W * H * 3, np.float32)
+    b = np.zeros(W * H * 3, np.float32)
+    q = pt.MakeWorkQueue(N.PT_RENDERER_SIMT_TEXTURED)
+    pt.BeginFrame()
+    for t in _tiles():
+        pt.AddWorkQueueEntry(q, pt.RenderBufferInfo(a, W, H, 3), t)
+        pt.AddWorkQueueEntry(q, pt.RenderBufferInfo(b, W, H, 3), t)
+    q.complete(wait=False)
+    q.wait()
+    ref = po.render(W, H, nframes=1, num_bounces=8, env=env)
+    for x in (a, b):
+        got = tiled_to_interleaved(x, W, H, TW, TH)
+        assert bits_equal(got, ref), mismatch_report(got, ref)
+    pt.unpin_host(None)
+
+    pt.init(pin_host=True)
+    pt.v4_config(env_mode=N.PT_V4_ENV_EQUIRECT)
+    env4 = np.random.default_rng(8).random((64, 128, 3), dtype=np.float32) + 0.01
+    pt.set_env_map(env4)
+    buf = np.zeros(W * H * 3, np.float32)
+    q4 = pt.MakeWorkQueue(N.PT_RENDERER_V4)
+    for _ in range(2):
+        pt.v4_begin_frame()
+        for t in _tiles():
+            pt.AddWorkQueueEntry(q4, pt.RenderBufferInfo(buf, W, H, 3), t)
+        pt.CompleteAllWork(q4)
+    ref4 = po.render4(W, H, nframes=2, env=env4)
+    got = tiled_to_interleaved(buf, W, H, TW, TH)
+    assert bits_equal(got, ref4), mismatch_report(got, ref4)
+    pt.unpin_host(buf)
