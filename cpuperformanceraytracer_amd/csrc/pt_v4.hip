@@ -124,6 +124,17 @@ __device__ __forceinline__ V3 ruv_rejection(uint32_t& s)   // v4 :109-130
     return v3(u, v, w) * rcp(sqrt_(d2));   // rsroot -> 1/sqrtf (mathlib.h:437)
 }
 
+// the same unit vector from three draws already taken (h0, h1, h2 = wang's outputs in draw order)
+__device__ __forceinline__ float randf_of(uint32_t h) { return (float)(int32_t)(h & 0x7FFFFFFFu) * 0x1p-31f; }
+__device__ __forceinline__ V3 ruv_rejection_of(uint32_t h0, uint32_t h1, uint32_t h2)
+{
+    const float u = fma_(2.0f, randf_of(h0), -1.0f);
+    const float v = fma_(2.0f, randf_of(h1), -1.0f);
+    const float w = fma_(2.0f, randf_of(h2), -1.0f);
+    const float d2 = fma_(w, w, fma_(u, u, v * v));
+    return v3(u, v, w) * rcp(sqrt_(d2));
+}
+
 __device__ __forceinline__ V3 ruv_angle(uint32_t& s)   // mathutils.h:33-46 (sincos -> glibc sinf/cosf)
 {
     const float wz = randf(s);
@@ -718,20 +729,31 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                         // directions and selects one; only the selected one (and the diffuse direction
                         // the specular one lerps towards) is evaluated here.  Both random unit vectors
                         // are still drawn, in the reference's order (diffuse first).
-                        const uint32_t s_diff = rng;
-                        rng_skip(rng, rejection ? 3 : 2);
-                        const uint32_t s_refr = rng;
-                        rng_skip(rng, rejection ? 3 : 2);
+                        const bool unified = PT_V4_UNIFIED_DIR && rejection;
+                        uint32_t s_diff = rng, s_refr = rng;
+                        uint32_t h0 = 0, h1 = 0, h2 = 0;   // unified: the chosen stream's three draws
+                        if (unified) {
+                            // both streams' draws once (6 hashes, not 6 skipped + 3 redrawn), then the
+                            // chosen stream's three selected -- the same values in the same order
+                            const uint32_t d0 = wang(rng), d1 = wang(rng), d2 = wang(rng);
+                            const uint32_t r0 = wang(rng), r1 = wang(rng), r2 = wang(rng);
+                            h0 = do_refr ? r0 : d0;
+                            h1 = do_refr ? r1 : d1;
+                            h2 = do_refr ? r2 : d2;
+                        } else {
+                            rng_skip(rng, rejection ? 3 : 2);
+                            s_refr = rng;
+                            rng_skip(rng, rejection ? 3 : 2);
+                        }
                         V3 ndir;
-                        if (PT_V4_UNIFIED_DIR && rejection) {
+                        if (unified) {
                             // The three outcomes share one shape: a unit vector u drawn from the chosen
                             // stream, nb = (u +- n) * rcp(sqrt(|u +- n|^2)) (diffuse: n + u; refraction:
                             // u - n == u + (-n) exactly), and -- for specular and refraction -- the
                             // reference's fma lerp from a mirror direction R (reflect or refract) towards
                             // nb.  Evaluated once per lane with per-lane operands instead of as two
                             // divergent branches; every value is the branch's own, bit for bit.
-                            uint32_t r = do_refr ? s_refr : s_diff;
-                            const V3 u = ruv_rejection(r);
+                            const V3 u = ruv_rejection_of(h0, h1, h2);
                             const V3 sn = do_refr ? neg(h.n) : h.n;
                             const V3 a = u + sn;
                             const V3 nb = a * rcp(sqrt_(dot(a, a)));
