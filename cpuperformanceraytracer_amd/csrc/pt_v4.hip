@@ -422,6 +422,33 @@ static_assert(default_spheres_disjoint(), "the closest-sphere trace needs pairwi
 #ifndef PT_V4_SPHERE_CLOSEST
 #define PT_V4_SPHERE_CLOSEST 1
 #endif
+// The candidate with the largest b without tracking it (PT_V4_SPHERE_ORDER).  InitializeScene's
+// spheres lie on one line parallel to x, in ascending x, `spacing` apart, radius r, 2r < spacing
+// (asserted below).  Then b_i = (pos - c_i).dir = b_0 - i spacing dir.x exactly, so the largest b of
+// the candidates is the lowest candidate index when dir.x > 0 and the highest when dir.x < 0 --
+// provided the computed b's keep that order.  They do: two candidates i < j mean the line passes
+// within r (+ the discriminant's rounding, ~1e-4) of both centres, so its closest approaches are
+// >= (j - i) spacing - 2r >= 0.4 apart along the line, |dir.x| >= 0.4 / ((j - i) spacing) and the
+// exact b's differ by >= 0.4 -- against rounding errors of ~1e-5 in b.  (dir.x == 0 admits at most
+// one candidate.)  A NaN ray makes every b NaN: the reference's b > bmax never takes one, and the
+// recomputed b of the chosen index is NaN too, which drops it.  The kernel keeps the per-sphere
+// early tests (exactly) and replaces the per-sphere compare + three selects by a candidate bit mask.
+#ifndef PT_V4_SPHERE_ORDER
+#define PT_V4_SPHERE_ORDER 1
+#endif
+constexpr bool default_spheres_on_x_line()
+{
+    namespace D = pt_v4_default;
+    for (int i = 1; i < D::kSpheres; ++i) {
+        if (D::kSphere[i][1] != D::kSphere[0][1] || D::kSphere[i][2] != D::kSphere[0][2] ||
+            D::kSphere[i][3] != D::kSphere[0][3])
+            return false;
+        if (!(D::kSphere[i][0] - D::kSphere[i - 1][0] >= 2.0f * D::kSphere[0][3] + 0.4f)) return false;
+    }
+    return D::kSpheres <= 32;
+}
+static_assert(!PT_V4_SPHERE_ORDER || default_spheres_on_x_line(),
+              "PT_V4_SPHERE_ORDER needs InitializeScene's spheres on one x line, >= 0.4 apart");
 #ifndef PT_V4_UNIFIED_DIR
 #define PT_V4_UNIFIED_DIR 1   // rejection sampling: one straight-line direction for all three outcomes
 #endif
@@ -470,6 +497,26 @@ __device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir, const 
         if (PT_V4_SPHERE_CLOSEST) {
             float bmax = -__builtin_huge_valf(), dsel = 0.0f;
             int ksel = -1;
+#if PT_V4_SPHERE_ORDER
+            uint32_t cand = 0;   // spheres that pass the early test
+#pragma unroll
+            for (int i = 0; i < D::kSpheres; ++i) {   // :645-657, the early test exactly
+                const V3 m = pos - v3(D::kSphere[i][0], D::kSphere[i][1], D::kSphere[i][2]);
+                const float b = dot(m, dir);
+                const float cc = fma_(-D::kSphere[i][3], D::kSphere[i][3], dot(m, m));
+                const float discr = fma_(b, b, -cc);
+                const bool early = discr < 0.0f || (cc > 0.0f && b > 0.0f);
+                cand |= early ? 0u : 1u << i;
+            }
+            if (cand) {   // the largest b: by the sign of dir.x (see PT_V4_SPHERE_ORDER)
+                ksel = dir.x > 0.0f ? __builtin_ctz(cand) : 31 - __builtin_clz(cand);
+                const float4 c = s_sc[ksel];
+                const V3 m = pos - v3(c.x, c.y, c.z);
+                bmax = dot(m, dir);
+                dsel = fma_(bmax, bmax, -fma_(-c.w, c.w, dot(m, m)));
+                if (!(bmax == bmax)) ksel = -1;
+            }
+#else
 #pragma unroll
             for (int i = 0; i < D::kSpheres; ++i) {   // :645-657, the early test exactly
                 const V3 m = pos - v3(D::kSphere[i][0], D::kSphere[i][1], D::kSphere[i][2]);
@@ -482,6 +529,7 @@ __device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir, const 
                 dsel = take ? discr : dsel;
                 ksel = take ? i : ksel;
             }
+#endif
             bool seq = false;
             if (ksel >= 0) {
                 const float4 c = s_sc[ksel];

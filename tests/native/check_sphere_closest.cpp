@@ -148,6 +148,27 @@ void check(F3 P, F3 D, const float (*sph)[4], int n)
         cands += sphere_pre<V4>(P, D, sph[k], b, discr);
     }
     n_multi += cands > 1;
+    if (V4) {   // pt_v4.hip PT_V4_SPHERE_ORDER: the argmax of b is the first / last candidate by sign(D.x)
+        float bmax = -INFINITY;
+        int karg = -1;
+        uint32_t cand = 0;
+        for (int k = 0; k < n; ++k) {
+            float b, discr;
+            const bool c = sphere_pre<V4>(P, D, sph[k], b, discr);
+            if (c) cand |= 1u << k;
+            if (c && b > bmax) bmax = b, karg = k;
+        }
+        int kord = -1;
+        if (cand) {
+            kord = D.x > 0.0f ? __builtin_ctz(cand) : 31 - __builtin_clz(cand);
+            float b, discr;
+            sphere_pre<V4>(P, D, sph[kord], b, discr);
+            if (!(b == b)) kord = -1;
+        }
+        if (kord != karg && ++n_bad <= 20)
+            std::printf("ORDER MISMATCH P=(%a,%a,%a) D=(%a,%a,%a) argmax=%d order=%d\n", P.x, P.y, P.z, D.x, D.y, D.z,
+                        karg, kord);
+    }
     if (std::memcmp(&a.dist, &c.dist, 4) || a.id != c.id || (a.id >= 0 && a.inside != c.inside)) {
         if (++n_bad <= 20)
             std::printf("MISMATCH %s P=(%a,%a,%a) D=(%a,%a,%a) seq=(%a,%d,%d) closest=(%a,%d,%d)\n", V4 ? "v4" : "diffuse",
