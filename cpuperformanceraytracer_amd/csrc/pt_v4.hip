@@ -722,7 +722,11 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
             int qslot = 0;
             // default scene: when every busy lane traces a camera ray that leaves the scene's
             // silhouette (sky_ray_v4), the wave skips TestSceneTrace -- the reference's miss
-            const bool all_sky = DEF && PT_V4_SKY_SKIP && __ballot(item >= 0 && !(bounce == 0 && sky_ray_v4(dir))) == 0;
+            // (the slope test runs only in iterations where every busy lane is at bounce 0: a wave-
+            // uniform branch, instead of the test on every lane in every iteration)
+            bool all_sky = false;
+            if (DEF && PT_V4_SKY_SKIP && __ballot(item >= 0 && bounce != 0) == 0)
+                all_sky = __ballot(item >= 0 && !sky_ray_v4(dir)) == 0;
             if (item >= 0) {
                 // one iteration of GetColorForRay's bounce loop (:733-909)
                 int fb = 0;
