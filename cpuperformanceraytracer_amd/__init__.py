@@ -40,6 +40,7 @@ from .renderer import (  # noqa: F401
     get_frame,
     init,
     initialized_device,
+    initialized_devices,
     make_tiles,
     readback,
     set_env_map,
@@ -48,6 +49,8 @@ from .renderer import (  # noqa: F401
     texture,
     tonemap,
     unpin_host,
+    release_buffer,
+    v4_get_config,
     WriteImage,
 )
 
@@ -58,5 +61,6 @@ __all__ = [
     "DemofoxRenderOptV4", "InitializeGlobalRenderResources", "ReinitializeRenderTileData", "InitializeScene",
     "ClearScene", "AddMaterialToScene", "AddQuadObjectToScene", "AddSphereObjectToScene", "LoadCubemapTexture",
     "v4_config", "v4_begin_frame", "v4_get_frame", "v4_set_frame", "MakeWorkQueue", "AddWorkQueueEntry",
-    "CompleteAllWork", "WorkQueue", "initialized_device", "unpin_host",
+    "CompleteAllWork", "WorkQueue", "initialized_device", "initialized_devices", "unpin_host", "release_buffer",
+    "v4_get_config",
 ]

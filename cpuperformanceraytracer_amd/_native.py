@@ -25,6 +25,8 @@ PT_LAYOUT_TILED_PLANAR8 = 2
 PT_FLAG_DEFER_READBACK = 1
 PT_FLAG_PIN_HOST = 2
 
+PT_MAX_DEVICES = 16
+
 PT_PIXEL_RGBA8 = 0
 PT_PIXEL_XRGB8 = 1
 
@@ -32,10 +34,11 @@ PT_PIXEL_XRGB8 = 1
 EXPORTED_SYMBOLS = (
     "pt_init", "pt_shutdown", "pt_last_error", "pt_default_config", "pt_set_frame", "pt_get_frame",
     "pt_render_scalar", "pt_render_simd", "pt_render_simd_tiled", "pt_render_tile", "pt_begin_frame",
-    "pt_readback", "pt_unpin_host", "pt_initialized_device", "pt_render_device", "pt_count_device",
+    "pt_readback", "pt_unpin_host", "pt_release_buffer", "pt_initialized_device", "pt_device_count",
+    "pt_device_ordinal", "pt_render_device", "pt_count_device",
     "pt_load_texture", "pt_decode_hdr", "pt_free_texture", "pt_set_env_map", "pt_render_simt_textured",
     "pt_tonemap", "pt_tonemap_device", "pt_write_bmp", "pt_load_cubemap_texture",
-    "pt_v4_default_config", "pt_v4_set_config", "pt_v4_initialize_global_render_resources",
+    "pt_v4_default_config", "pt_v4_set_config", "pt_v4_get_config", "pt_v4_initialize_global_render_resources",
     "pt_v4_reinitialize_render_tile_data", "pt_v4_initialize_scene", "pt_v4_clear_scene", "pt_v4_add_material",
     "pt_v4_add_quad", "pt_v4_add_sphere", "pt_v4_set_frame", "pt_v4_get_frame", "pt_v4_get_scene_tables", "pt_render_opt_v4",
     "pt_copy_output_to_file", "pt_v4_render_device", "pt_v4_count_device", "pt_v4_begin_frame",
@@ -56,7 +59,8 @@ PT_V4_MAX_OBJECTS = 12
 class PtConfig(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("num_bounces", ctypes.c_int32),
                 ("samples_per_frame", ctypes.c_int32), ("flags", ctypes.c_uint32),
-                ("ambient", ctypes.c_float * 3)]
+                ("ambient", ctypes.c_float * 3), ("device_count", ctypes.c_int32),
+                ("devices", ctypes.c_int32 * PT_MAX_DEVICES)]
 
 
 class PtBufferInfo(ctypes.Structure):
@@ -92,7 +96,9 @@ class PtWorkCounts(ctypes.Structure):
 
 class PtV4Config(ctypes.Structure):
     _fields_ = [("env_mode", ctypes.c_int32), ("random_jitter", ctypes.c_int32), ("rejection", ctypes.c_int32),
-                ("num_bounces", ctypes.c_int32), ("output_to_screen", ctypes.c_int32)]
+                ("num_bounces", ctypes.c_int32), ("output_to_screen", ctypes.c_int32),
+                ("accumulate_frames", ctypes.c_int32), ("fast_aces", ctypes.c_int32), ("fast_gamma", ctypes.c_int32),
+                ("fast_exp", ctypes.c_int32)]
 
 
 class PtV4Material(ctypes.Structure):
@@ -147,7 +153,10 @@ def load() -> ctypes.CDLL:
         "pt_begin_frame": (i32, []),
         "pt_readback": (i32, [vp]),
         "pt_unpin_host": (i32, [vp]),
+        "pt_release_buffer": (i32, [vp]),
         "pt_initialized_device": (i32, []),
+        "pt_device_count": (i32, []),
+        "pt_device_ordinal": (i32, [i32]),
         "pt_render_device": (i32, [ctypes.POINTER(PtDeviceJob), vp]),
         "pt_count_device": (i32, [ctypes.POINTER(PtDeviceJob), vp, ctypes.POINTER(PtWorkCounts)]),
         "pt_load_texture": (i32, [ctypes.c_char_p, ctypes.POINTER(PtTexture)]),
@@ -161,6 +170,7 @@ def load() -> ctypes.CDLL:
         "pt_load_cubemap_texture": (i32, [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(PtTexture)]),
         "pt_v4_default_config": (None, [ctypes.POINTER(PtV4Config)]),
         "pt_v4_set_config": (i32, [ctypes.POINTER(PtV4Config)]),
+        "pt_v4_get_config": (i32, [ctypes.POINTER(PtV4Config)]),
         "pt_v4_initialize_global_render_resources": (i32, []),
         "pt_v4_reinitialize_render_tile_data": (i32, []),
         "pt_v4_initialize_scene": (i32, []),

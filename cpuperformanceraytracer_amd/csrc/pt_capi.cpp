@@ -1,5 +1,6 @@
 // pt_capi.cpp -- the C ABI of libpt_mi355.so (include/pt_mi355.h): validation, frame state,
-// host<->device buffer mirroring, and dispatch to the HIP kernels (pt_kernel.hip).
+// host<->device buffer mirroring, dispatch to the HIP kernels (pt_kernel.hip, pt_v4.hip,
+// pt_output.hip), and the fan-out of every host-buffer entry point over one or several GPUs.
 //
 // Reference behaviour mirrored here (paths relative to CPUPerformanceRayTracer/):
 //   - frame counter: `static f32 iFrame; iFrame += 1` before rendering (scalar.cpp:798-799,
@@ -7,6 +8,15 @@
 //   - settings checks of ApplicationState::CheckValidSettings (Application.cpp:36-94), returned
 //     as PT_EINVAL instead of __debugbreak();
 //   - the caller owns the host buffer, the call returns after it is updated (Application.cpp:474).
+//
+// Several devices (pt_config.device_count > 1, or PT_MI355_DEVICES): the reference fans a frame's
+// tiles out over its CPU threads (simd_tiled.cpp:549-571, v4 :1696-1721); here a frame's ROWS are
+// dealt to the devices, row Y to device Y mod N (neighbouring rows cost alike, so every device gets
+// the same mix of cheap sky rows and expensive rows into the box).  Every pixel's value depends only
+// on its global (x, y) and the frame, so any split renders bit-identical pixels.  Each device keeps
+// its own mirror of its rows: a compact sub-image for the row layouts (interleaved, planar8) and a
+// full-size buffer of which it owns the rows for the tiled layout (whose rows are not contiguous in
+// the host buffer); transfers move only the owned rows (pitched 2D copies).
 #include "pt_kernel.h"
 #include "pt_output.h"
 #include "pt_v4.h"
@@ -53,51 +63,65 @@ constexpr int kSchedSlots = 16;
 constexpr int kBands = 4;   // PT_FLAG_PIN_HOST: row bands of a pipelined frame
 constexpr uint32_t kSchedMinTiles = 512;   // smaller jobs (e.g. one RenderTile) are not scheduled
 constexpr unsigned kQueueRing = 256;       // tile-queue ring slots (reuse across streams is event-ordered)
-#ifndef PT_SCHED_REBUILD
-#define PT_SCHED_REBUILD 64
-#endif
-constexpr unsigned long long kSchedRebuild = PT_SCHED_REBUILD;
+constexpr unsigned long long kSchedRebuild = 64;
 
-struct State {
-    bool inited = false;
-    pt_config cfg{};
+// One (logical) device: its streams, scene, tile queues, schedules, env map and the mirror of its
+// share of the caller's host accumulator.  Several logical devices may name the same HIP device
+// (tests shard a frame over N logical devices on one GPU).
+struct Dev {
+    int32_t ordinal = 0;
     hipStream_t stream = nullptr;
-    PtScene scene{};
-    PtScene* dscene = nullptr;          // device copy of `scene`
-    uint32_t frame = 0;                 // value of the reference's static iFrame
-    // device mirror of the caller's host accumulator (host-buffer entry points)
-    float* dbuf = nullptr;
+    PtScene* dscene = nullptr;          // device copy of State::scene
+    float* dbuf = nullptr;              // mirror of this device's rows of the host accumulator
     size_t dbuf_cap = 0;
-    const float* mirror_host = nullptr; // host buffer the mirror currently represents
-    size_t mirror_bytes = 0;
-    bool mirror_valid = false;          // deferred mode: device copy is authoritative
     unsigned long long* dcounters = nullptr;
     unsigned int* dqueue = nullptr;     // ring of kQueueRing tile-queue blocks (PT_QUEUE_WORDS each)
     unsigned queue_next = 0;
-    bool queue_pre_zeroed = false;      // the last launch's kernel zeroed ring slot queue_next % kQueueRing
+    bool queue_pre_zeroed = false;      // the last launch's kernel zeroes ring slot queue_next % kQueueRing
+    hipStream_t last_stream = nullptr;  // the stream of the last launch
     // per ring slot: the stream of the last launch that used it and an event recorded after that
     // launch; a launch on another stream waits for it before re-zeroing the slot
     hipStream_t queue_stream[kQueueRing] = {};
     hipEvent_t queue_event[kQueueRing] = {};
-    // env map in HBM (pt_set_env_map / pt_render_simt_textured)
-    float* denv = nullptr;
-    int32_t env_w = 0, env_h = 0;
-    const float* env_src = nullptr;     // host data the device copy was made from
+    float* denv = nullptr;              // env map in HBM (pt_set_env_map / textured / v4)
     Sched sched[kSchedSlots];
     unsigned long long sched_clock = 0;
-    // PT_FLAG_PIN_HOST: the registered host buffer, copy streams and band events
+    float* dtone_in = nullptr;          // output stage scratch
+    size_t dtone_in_cap = 0;
+    uint32_t* dtone_out = nullptr;
+    size_t dtone_out_cap = 0;
+};
+
+// The host buffer the device mirrors currently represent, and the geometry they were split by.
+struct Mirror {
+    const float* host = nullptr;
+    size_t bytes = 0;
+    int32_t width = 0, height = 0;
+    bool tiled = false;
+    int32_t tile_w = 0, tile_h = 0;
+    bool valid = false;                 // deferred mode: the device copies are authoritative
+};
+
+struct State {
+    bool inited = false;
+    pt_config cfg{};
+    int ndev = 0;
+    Dev dev[PT_MAX_DEVICES];
+    PtScene scene{};
+    uint32_t frame = 0;                 // value of the reference's static iFrame
+    Mirror m;
+    // env map (the same texture on every device)
+    const float* env_src = nullptr;     // host data the device copies were made from
+    int32_t env_w = 0, env_h = 0;
+    bool have_env = false;
+    // PT_FLAG_PIN_HOST (one device): the registered host buffer, copy streams and band events
     const float* pinned = nullptr;
     size_t pinned_bytes = 0;
     hipStream_t s_in = nullptr, s_out = nullptr;
     hipEvent_t ev_in[kBands] = {}, ev_done[kBands] = {};
-    hipEvent_t ev_q = nullptr;   // work queues: orders banded copies against g.stream
-    // output stage scratch (host-buffer pt_tonemap)
-    float* dtone_in = nullptr;
-    size_t dtone_in_cap = 0;
-    uint32_t* dtone_out = nullptr;
-    size_t dtone_out_cap = 0;
+    hipEvent_t ev_q = nullptr;          // work queues: orders banded copies against the stream
     // v4 renderer (demofox_path_tracing_optimization_v4.cpp): its own iFrame (v4 :34) and scene
-    pt_v4_config v4cfg{PT_V4_ENV_EQUIRECT, 1, 1, 8, 1};
+    pt_v4_config v4cfg{PT_V4_ENV_EQUIRECT, 1, 1, 8, 1, 1, 1, 1, 1};
     bool v4_scene_ready = false;
     PtV4SceneDesc v4desc{};
     PtV4Scene v4scene{};
@@ -136,73 +160,209 @@ constexpr int kCounterSlots = 32 + 4 * 65536 + 96 * 65536;   // + per-wave recor
 constexpr int kCounterSlots = 32;
 #endif
 
+// The caller's current HIP device is restored when an entry point returns (the library switches to
+// each device it drives).
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() { (void)hipGetDevice(&prev); }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int use_dev(const Dev& d)
+{
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != d.ordinal) HIP_TRY(hipSetDevice(d.ordinal));
+    return PT_OK;
+}
+
 int ensure_init()
 {
     if (g.inited) return PT_OK;
     return pt_init(nullptr);
 }
 
-int ensure_dbuf(size_t bytes)
+// ---- shards -----------------------------------------------------------------------------------
+// Device d of n owns the global rows d, d + n, ...
+int32_t shard_rows(int32_t h, int n, int d) { return d < h ? (h - 1 - d) / n + 1 : 0; }
+
+// Geometry of a host accumulator: size and whether it is tile-major (RenderTile layout).
+struct Geo {
+    int32_t w = 0, h = 0;
+    bool tiled = false;
+    int32_t tw = 0, th = 0;
+};
+
+// Bytes of device d's mirror: the whole buffer with one device or the tiled layout, else the
+// compact rows.
+size_t dev_bytes(const Geo& geo, int d)
 {
-    if (bytes <= g.dbuf_cap) return PT_OK;
-    if (g.dbuf) {
-        HIP_TRY(hipStreamSynchronize(g.stream));
-        HIP_TRY(hipFree(g.dbuf));
-        g.dbuf = nullptr;
-        g.dbuf_cap = 0;
+    if (g.ndev == 1 || geo.tiled) return (size_t)geo.w * geo.h * 3 * sizeof(float);
+    return (size_t)shard_rows(geo.h, g.ndev, d) * geo.w * 3 * sizeof(float);
+}
+
+// A region of the host buffer: the whole frame, or one RenderTile slice (tile index k).
+struct Region {
+    bool whole = true;
+    int32_t tile_x = 0, tile_y = 0;
+};
+
+// Copy device d's part of `rg` between the host buffer and its mirror (async on its stream).
+int xfer(int d, const Geo& geo, float* host, bool to_device, const Region& rg)
+{
+    Dev& dv = g.dev[d];
+    const hipMemcpyKind kind = to_device ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost;
+    const int n = g.ndev;
+    if (n == 1) {
+        size_t off = 0, len = (size_t)geo.w * geo.h * 3 * sizeof(float);
+        if (!rg.whole) {   // simd_tiled.cpp:499-502: the tile is one contiguous slice
+            off = ((size_t)rg.tile_y * geo.th * geo.w * 3 + (size_t)rg.tile_x * geo.tw * geo.th * 3) * sizeof(float);
+            len = (size_t)geo.tw * geo.th * 3 * sizeof(float);
+        }
+        char* hp = (char*)host + off;
+        char* dp = (char*)dv.dbuf + off;
+        HIP_TRY(hipMemcpyAsync(to_device ? (void*)dp : (void*)hp, to_device ? (void*)hp : (void*)dp, len, kind, dv.stream));
+        return PT_OK;
     }
-    if (hipMalloc(&g.dbuf, bytes) != hipSuccess) {
-        g.dbuf = nullptr;
-        return fail(PT_ENOMEM, "hipMalloc(%zu) failed", bytes);
+    if (!geo.tiled) {   // compact rows: one pitched copy
+        const int32_t nr = shard_rows(geo.h, n, d);
+        if (nr == 0) return PT_OK;
+        const size_t row = (size_t)geo.w * 3 * sizeof(float);
+        char* hp = (char*)host + (size_t)d * row;
+        if (to_device) HIP_TRY(hipMemcpy2DAsync(dv.dbuf, row, hp, row * n, row, nr, kind, dv.stream));
+        else HIP_TRY(hipMemcpy2DAsync(hp, row * n, dv.dbuf, row, row, nr, kind, dv.stream));
+        return PT_OK;
     }
-    g.dbuf_cap = bytes;
-    g.mirror_valid = false;
+    // tiled: every tile is contiguous (TW x TH x 3 floats, raster tile order); the device's rows of a
+    // tile are every n-th of its tile rows -- one pitched copy per tile, same offsets on both sides
+    const int32_t ntx = geo.w / geo.tw, nty = geo.h / geo.th;
+    const size_t tile_f = (size_t)geo.tw * geo.th * 3, trow = (size_t)geo.tw * 3 * sizeof(float);
+    const int32_t k0 = rg.whole ? 0 : rg.tile_y * ntx + rg.tile_x, k1 = rg.whole ? ntx * nty : k0 + 1;
+    for (int32_t k = k0; k < k1; ++k) {
+        const int32_t ty = k / ntx;
+        const int32_t ly0 = (int32_t)((((int64_t)d - (int64_t)ty * geo.th) % n + n) % n);
+        if (ly0 >= geo.th) continue;
+        const int32_t cnt = (geo.th - 1 - ly0) / n + 1;
+        const size_t off = (k * tile_f + (size_t)ly0 * geo.tw * 3) * sizeof(float);
+        char* hp = (char*)host + off;
+        char* dp = (char*)dv.dbuf + off;
+        HIP_TRY(hipMemcpy2DAsync(to_device ? (void*)dp : (void*)hp, trow * n, to_device ? (void*)hp : (void*)dp,
+                                 trow * n, trow, cnt, kind, dv.stream));
+    }
     return PT_OK;
+}
+
+int sync_all()
+{
+    for (int d = 0; d < g.ndev; ++d) {
+        int rc;
+        if ((rc = use_dev(g.dev[d]))) return rc;
+        HIP_TRY(hipStreamSynchronize(g.dev[d].stream));
+    }
+    return PT_OK;
+}
+
+int ensure_dbuf(int d, size_t bytes)
+{
+    Dev& dv = g.dev[d];
+    if (bytes <= dv.dbuf_cap) return PT_OK;
+    if (dv.dbuf) {
+        HIP_TRY(hipStreamSynchronize(dv.stream));
+        HIP_TRY(hipFree(dv.dbuf));
+        dv.dbuf = nullptr;
+        dv.dbuf_cap = 0;
+    }
+    if (hipMalloc(&dv.dbuf, bytes) != hipSuccess) {
+        dv.dbuf = nullptr;
+        return fail(PT_ENOMEM, "hipMalloc(%zu) failed on device %d", bytes, dv.ordinal);
+    }
+    dv.dbuf_cap = bytes;
+    g.m.valid = false;
+    return PT_OK;
+}
+
+Geo mirror_geo()
+{
+    Geo geo;
+    geo.w = g.m.width;
+    geo.h = g.m.height;
+    geo.tiled = g.m.tiled;
+    geo.tw = g.m.tile_w;
+    geo.th = g.m.tile_h;
+    return geo;
 }
 
 // Deferred mode: a valid mirror is the only up-to-date copy of its host buffer's accumulation.
 // Before the mirror is given to another buffer it is written back to its own host buffer (as if
-// pt_readback had been called), so alternating buffers loses nothing.
+// pt_readback had been called), so alternating buffers loses nothing.  The caller must release a
+// deferred buffer (pt_release_buffer) before freeing it.
 int flush_mirror()
 {
-    if (!g.mirror_valid || !g.dbuf || !g.mirror_host) {
-        g.mirror_valid = false;
+    int rc;
+    if (!g.m.valid || !g.m.host) {
+        g.m.valid = false;
         return PT_OK;
     }
-    HIP_TRY(hipMemcpyAsync((void*)g.mirror_host, g.dbuf, g.mirror_bytes, hipMemcpyDeviceToHost, g.stream));
-    HIP_TRY(hipStreamSynchronize(g.stream));
-    g.mirror_valid = false;
+    const Geo geo = mirror_geo();
+    for (int d = 0; d < g.ndev; ++d) {
+        if ((rc = use_dev(g.dev[d])) || (rc = xfer(d, geo, (float*)g.m.host, false, Region{}))) return rc;
+    }
+    if ((rc = sync_all())) return rc;
+    g.m.valid = false;
     return PT_OK;
 }
 
-// Make the device mirror hold the host buffer [0, bytes).  In deferred mode an already valid
-// mirror of the same buffer is authoritative and nothing is copied.
-int stage_in(const float* host, size_t bytes, size_t off, size_t len)
+void drop_mirror()
+{
+    g.m = Mirror{};
+}
+
+bool same_split(const Geo& geo)
+{
+    if (g.m.width != geo.w || g.m.height != geo.h) return false;
+    if (g.ndev == 1) return true;   // one device mirrors the whole buffer in any layout
+    return g.m.tiled == geo.tiled && (!geo.tiled || (g.m.tile_w == geo.tw && g.m.tile_h == geo.th));
+}
+
+// Make the device mirrors hold region `rg` of the host buffer `host` (geometry `geo`).  In
+// deferred mode an already valid mirror of the same buffer is authoritative and nothing is copied.
+int stage_in(float* host, const Geo& geo, const Region& rg)
 {
     const bool deferred = (g.cfg.flags & PT_FLAG_DEFER_READBACK) != 0;
+    const size_t bytes = (size_t)geo.w * geo.h * 3 * sizeof(float);
     int rc;
-    if (g.mirror_host != host || g.mirror_bytes != bytes)
-        if ((rc = flush_mirror())) return rc;
-    rc = ensure_dbuf(bytes);
-    if (rc) return rc;
-    if (deferred && g.mirror_valid) return PT_OK;
-    if (deferred) {   // first deferred touch: the whole buffer becomes device-resident
-        off = 0;
-        len = bytes;
+    if (g.m.valid) {
+        if (g.m.host == host && g.m.bytes != bytes) drop_mirror();   // reallocated in place: never write back
+        else if (g.m.host != host || !same_split(geo))
+            if ((rc = flush_mirror())) return rc;
     }
-    HIP_TRY(hipMemcpyAsync((char*)g.dbuf + off, (const char*)host + off, len, hipMemcpyHostToDevice, g.stream));
-    g.mirror_host = host;
-    g.mirror_bytes = bytes;
-    g.mirror_valid = deferred;
+    for (int d = 0; d < g.ndev; ++d)
+        if ((rc = use_dev(g.dev[d])) || (rc = ensure_dbuf(d, dev_bytes(geo, d)))) return rc;
+    if (deferred && g.m.valid) return PT_OK;
+    const Region r = deferred ? Region{} : rg;   // first deferred touch: the whole buffer becomes device-resident
+    for (int d = 0; d < g.ndev; ++d)
+        if ((rc = use_dev(g.dev[d])) || (rc = xfer(d, geo, host, true, r))) return rc;
+    g.m.host = host;
+    g.m.bytes = bytes;
+    g.m.width = geo.w;
+    g.m.height = geo.h;
+    g.m.tiled = geo.tiled;
+    g.m.tile_w = geo.tw;
+    g.m.tile_h = geo.th;
+    g.m.valid = deferred;
     return PT_OK;
 }
 
-int stage_out(float* host, size_t off, size_t len)
+int stage_out(float* host, const Geo& geo, const Region& rg)
 {
+    int rc;
     if (!(g.cfg.flags & PT_FLAG_DEFER_READBACK))
-        HIP_TRY(hipMemcpyAsync((char*)host + off, (const char*)g.dbuf + off, len, hipMemcpyDeviceToHost, g.stream));
-    HIP_TRY(hipStreamSynchronize(g.stream));
-    return PT_OK;
+        for (int d = 0; d < g.ndev; ++d)
+            if ((rc = use_dev(g.dev[d])) || (rc = xfer(d, geo, host, false, rg))) return rc;
+    return sync_all();
 }
 
 int check_frame_budget(uint32_t add)
@@ -235,7 +395,7 @@ PtJob base_job(float* buf, int32_t w, int32_t h)
     j.units = nullptr;
     j.nunits = nullptr;
     j.cost = nullptr;
-    j.scene = g.dscene;
+    j.scene = nullptr;
     return j;
 }
 
@@ -281,14 +441,14 @@ SchedKey sched_key(const PtV4Job& j)
     return k;
 }
 
-Sched* find_sched(const SchedKey& key, hipStream_t st)
+Sched* find_sched(Dev& dv, const SchedKey& key, hipStream_t st)
 {
     const uint32_t n = key.ntiles;
     if (n < kSchedMinTiles) return nullptr;
-    Sched* lru = &g.sched[0];
-    for (Sched& s : g.sched) {
+    Sched* lru = &dv.sched[0];
+    for (Sched& s : dv.sched) {
         if (s.used && s.stream == st && s.key == key) {
-            s.last_use = ++g.sched_clock;
+            s.last_use = ++dv.sched_clock;
             return &s;
         }
         if (!s.used || (lru->used && s.last_use < lru->last_use)) lru = &s;
@@ -306,9 +466,15 @@ Sched* find_sched(const SchedKey& key, hipStream_t st)
     s.used = true;
     s.stream = st;
     s.key = key;
-    s.last_use = ++g.sched_clock;
+    s.last_use = ++dv.sched_clock;
     *lru = s;
     return lru;
+}
+
+int slot_event(Dev& dv, unsigned slot)
+{
+    if (!dv.queue_event[slot]) HIP_TRY(hipEventCreateWithFlags(&dv.queue_event[slot], hipEventDisableTiming));
+    return PT_OK;
 }
 
 // The schedule and queue fields of a launch of geometry `key` on stream `st`.
@@ -321,10 +487,11 @@ struct LaunchSched {
     const uint32_t* nunits = nullptr;
     uint32_t* cost = nullptr;
 };
-int use_sched(const SchedKey& key, hipStream_t st, LaunchSched* ls)
+int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls)
 {
+    int rc;
     *ls = LaunchSched{};
-    if (Sched* s = find_sched(key, st)) {
+    if (Sched* s = find_sched(dv, key, st)) {
         // (re)build the schedule from the last launch's costs on the 2nd launch of a geometry and
         // then every kSchedRebuild launches (the costs of a fixed view barely change; the builder
         // is a one-workgroup kernel of ~57 us at 1080p)
@@ -343,41 +510,51 @@ int use_sched(const SchedKey& key, hipStream_t st, LaunchSched* ls)
         ++s->launches;
     }
     // Ring slots are used in order.  Each render kernel zeroes the NEXT slot's counters at its start,
-    // so a launch after a launched kernel finds its slot zero -- ordered after that kernel, on the
-    // same stream or by its event -- and otherwise zeroes it with a memset on `st`.  When a slot's
-    // previous user ran on another stream, wait for its event before the slot is used or zeroed.
-    ls->slot = g.queue_next++ % kQueueRing;
-    const unsigned prev = (ls->slot + kQueueRing - 1) % kQueueRing, next = (ls->slot + 1) % kQueueRing;
-    if (g.queue_event[ls->slot] && g.queue_stream[ls->slot] != st)
-        HIP_TRY(hipStreamWaitEvent(st, g.queue_event[ls->slot], 0));
-    ls->queue = g.dqueue + (size_t)ls->slot * PT_QUEUE_WORDS;
-    if (g.queue_pre_zeroed) {
-        if (g.queue_stream[prev] != st) HIP_TRY(hipStreamWaitEvent(st, g.queue_event[prev], 0));
-    } else {
-        HIP_TRY(hipMemsetAsync(ls->queue, 0, PT_QUEUE_WORDS * sizeof(unsigned), st));
+    // so a launch after a launched kernel on the same stream finds its slot zero.  After a launch on
+    // another stream that slot may still be being zeroed: it is skipped (its next user waits for that
+    // kernel) and this launch zeroes the slot after it with a memset on its own stream, so launches on
+    // different streams overlap.  A slot whose previous user ran on another stream is waited for
+    // before it is zeroed or used.
+    unsigned slot = dv.queue_next++ % kQueueRing;
+    bool pre = dv.queue_pre_zeroed;
+    if (pre && dv.last_stream != st) {
+        const unsigned prev = (slot + kQueueRing - 1) % kQueueRing;
+        if ((rc = slot_event(dv, slot))) return rc;
+        HIP_TRY(hipEventRecord(dv.queue_event[slot], dv.queue_stream[prev]));   // after the zeroing kernel
+        dv.queue_stream[slot] = dv.queue_stream[prev];
+        slot = dv.queue_next++ % kQueueRing;
+        pre = false;
     }
-    g.queue_pre_zeroed = false;   // (set by queue_done once this launch's kernel is enqueued)
-    if (g.queue_event[next] && g.queue_stream[next] != st) HIP_TRY(hipStreamWaitEvent(st, g.queue_event[next], 0));
-    ls->queue_next = g.dqueue + (size_t)next * PT_QUEUE_WORDS;
+    ls->slot = slot;
+    if (dv.queue_event[slot] && dv.queue_stream[slot] != st) HIP_TRY(hipStreamWaitEvent(st, dv.queue_event[slot], 0));
+    ls->queue = dv.dqueue + (size_t)slot * PT_QUEUE_WORDS;
+    if (!pre) HIP_TRY(hipMemsetAsync(ls->queue, 0, PT_QUEUE_WORDS * sizeof(unsigned), st));
+    dv.queue_pre_zeroed = false;   // (set by queue_done once this launch's kernel is enqueued)
+    const unsigned next = (slot + 1) % kQueueRing;
+    if (dv.queue_event[next] && dv.queue_stream[next] != st) HIP_TRY(hipStreamWaitEvent(st, dv.queue_event[next], 0));
+    ls->queue_next = dv.dqueue + (size_t)next * PT_QUEUE_WORDS;
     return PT_OK;
 }
 
 // After the launch that used ring slot `slot` was enqueued on `st`; `zeroed_next`: its kernel ran
 // (a launch with nothing to render returns without one) and zeroes the next slot.
-int queue_done(unsigned slot, hipStream_t st, bool zeroed_next)
+int queue_done(Dev& dv, unsigned slot, hipStream_t st, bool zeroed_next)
 {
-    if (!g.queue_event[slot]) HIP_TRY(hipEventCreateWithFlags(&g.queue_event[slot], hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(g.queue_event[slot], st));
-    g.queue_stream[slot] = st;
-    g.queue_pre_zeroed = zeroed_next;
+    int rc;
+    if ((rc = slot_event(dv, slot))) return rc;
+    HIP_TRY(hipEventRecord(dv.queue_event[slot], st));
+    dv.queue_stream[slot] = st;
+    dv.queue_pre_zeroed = zeroed_next;
+    dv.last_stream = st;
     return PT_OK;
 }
 
-int launch(PtJob j, hipStream_t st, bool count)
+int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
 {
     LaunchSched ls;
     int rc;
-    if ((rc = use_sched(sched_key(j), st, &ls))) return rc;
+    if ((rc = use_dev(dv)) || (rc = use_sched(dv, sched_key(j), st, &ls))) return rc;
+    j.scene = dv.dscene;
     j.queue = ls.queue;
     j.queue_next = ls.queue_next;
     j.order = ls.order;
@@ -386,7 +563,7 @@ int launch(PtJob j, hipStream_t st, bool count)
     j.cost = ls.cost;
     hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
-    return queue_done(ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_render's early return)
+    return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_render's early return)
 }
 
 void unpin()
@@ -399,28 +576,9 @@ void unpin()
     g.pinned_bytes = 0;
 }
 
-// Is the cached registration of `p` still the live one?  A buffer freed and reallocated at the
-// same address (common with numpy) is no longer page-locked by our registration: the runtime then
-// no longer reports `p` as registered host memory, and the buffer is registered afresh.
-bool pin_is_live(const float* p)
-{
-    hipPointerAttribute_t a{};
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return a.type == hipMemoryTypeHost && a.hostPointer == (void*)p;
-}
-
 bool pin(const float* p, size_t bytes)
 {
-    if (g.pinned == p && g.pinned_bytes == bytes && pin_is_live(p)) return true;
-    if (g.pinned == p) {   // stale registration of a freed buffer: forget it without unregistering
-        (void)hipHostUnregister((void*)p);
-        (void)hipGetLastError();
-        g.pinned = nullptr;
-        g.pinned_bytes = 0;
-    }
+    if (g.pinned == p && g.pinned_bytes == bytes) return true;
     unpin();
     if (hipHostRegister((void*)p, bytes, hipHostRegisterDefault) != hipSuccess) {
         (void)hipGetLastError();
@@ -431,21 +589,24 @@ bool pin(const float* p, size_t bytes)
     return true;
 }
 
-// PT_FLAG_PIN_HOST (without deferred readback) and `buf` page-locked: the frame job `j` (whole
-// image, either renderer) is split into kBands row bands (multiples of row_align rows: contiguous
-// in every layout) whose upload, render (`run(band_job)` on g.stream) and download overlap on three
-// streams.  Returns with the downloads queued on g.s_out; *used = false if the path does not apply.
+// PT_FLAG_PIN_HOST (one device, without deferred readback) and `buf` page-locked: the frame job `j`
+// (whole image, either renderer) is split into kBands row bands (multiples of row_align rows:
+// contiguous in every layout) whose upload, render (`run(band_job)` on the device stream) and
+// download overlap on three streams.  Returns with the downloads queued on g.s_out; *used = false if
+// the path does not apply.
 template <typename Job, typename Run>
 int render_bands(float* buf, const Job& j, int32_t row_align, Run&& run, bool* used)
 {
     int rc;
     const size_t bytes = (size_t)j.width * j.height * 3 * sizeof(float);
     *used = false;
-    if (!(g.cfg.flags & PT_FLAG_PIN_HOST) || (g.cfg.flags & PT_FLAG_DEFER_READBACK) || !pin(buf, bytes)) return PT_OK;
+    if (g.ndev != 1 || !(g.cfg.flags & PT_FLAG_PIN_HOST) || (g.cfg.flags & PT_FLAG_DEFER_READBACK)) return PT_OK;
+    Dev& dv = g.dev[0];
+    if ((rc = use_dev(dv))) return rc;
+    if (!pin(buf, bytes)) return PT_OK;
     *used = true;
-    if ((rc = ensure_dbuf(bytes))) return rc;
-    g.mirror_valid = false;
-    g.mirror_host = nullptr;
+    if ((rc = ensure_dbuf(0, bytes))) return rc;
+    drop_mirror();
     const int32_t w = j.width, h = j.height;
     int32_t rows = (h + kBands - 1) / kBands;
     rows = (rows + row_align - 1) / row_align * row_align;
@@ -453,49 +614,90 @@ int render_bands(float* buf, const Job& j, int32_t row_align, Run&& run, bool* u
     for (int32_t r0 = 0; r0 < h && k < kBands; r0 += rows, ++k) {
         const int32_t r1 = r0 + rows < h ? r0 + rows : h;
         const size_t off = (size_t)r0 * w * 3, len = (size_t)(r1 - r0) * w * 3 * sizeof(float);
-        HIP_TRY(hipMemcpyAsync(g.dbuf + off, buf + off, len, hipMemcpyHostToDevice, g.s_in));
+        HIP_TRY(hipMemcpyAsync(dv.dbuf + off, buf + off, len, hipMemcpyHostToDevice, g.s_in));
         HIP_TRY(hipEventRecord(g.ev_in[k], g.s_in));
-        HIP_TRY(hipStreamWaitEvent(g.stream, g.ev_in[k], 0));
+        HIP_TRY(hipStreamWaitEvent(dv.stream, g.ev_in[k], 0));
         Job b = j;
         b.row_start = r0;
         b.nrows = r1 - r0;
-        b.buf = j.layout == PT_LAYOUT_TILED_PLANAR8 ? g.dbuf : g.dbuf + off;   // tiled: global offsets
+        b.buf = j.layout == PT_LAYOUT_TILED_PLANAR8 ? dv.dbuf : dv.dbuf + off;   // tiled: global offsets
         if ((rc = run(b))) return rc;
-        HIP_TRY(hipEventRecord(g.ev_done[k], g.stream));
+        HIP_TRY(hipEventRecord(g.ev_done[k], dv.stream));
         HIP_TRY(hipStreamWaitEvent(g.s_out, g.ev_done[k], 0));
-        HIP_TRY(hipMemcpyAsync(buf + off, g.dbuf + off, len, hipMemcpyDeviceToHost, g.s_out));
+        HIP_TRY(hipMemcpyAsync(buf + off, dv.dbuf + off, len, hipMemcpyDeviceToHost, g.s_out));
     }
     return PT_OK;
 }
 
-// One frame call on a host buffer: the job `j` (whole image) is rendered into the device mirror
-// of `buf` -- pipelined in row bands with PT_FLAG_PIN_HOST, otherwise upload, render, download in
-// turn.
+// Device d's share of a whole-frame job `j` (global geometry): its rows d::n, into its mirror.
+template <typename Job>
+Job shard_job(const Job& j, int d)
+{
+    Job b = j;
+    b.buf = g.dev[d].dbuf;
+    if (g.ndev > 1) {
+        b.row_start = j.row_start + d;
+        b.row_stride = g.ndev;
+        b.nrows = shard_rows(j.nrows, g.ndev, d);
+    }
+    return b;
+}
+
+// Device d's rows of one tile job (tiled layout: rows are global, the buffer is full-size).
+template <typename Job>
+Job tile_shard_job(const Job& j, int d)
+{
+    Job b = j;
+    b.buf = g.dev[d].dbuf;
+    if (g.ndev > 1) {
+        const int32_t ly0 = (int32_t)((((int64_t)d - j.row_start) % g.ndev + g.ndev) % g.ndev);
+        b.row_start = j.row_start + ly0;
+        b.row_stride = g.ndev;
+        b.nrows = ly0 < j.nrows ? (j.nrows - 1 - ly0) / g.ndev + 1 : 0;
+    }
+    return b;
+}
+
+Geo geo_of(int32_t w, int32_t h, int32_t layout, int32_t tw, int32_t th)
+{
+    Geo geo;
+    geo.w = w;
+    geo.h = h;
+    geo.tiled = layout == PT_LAYOUT_TILED_PLANAR8;
+    geo.tw = tw;
+    geo.th = th;
+    return geo;
+}
+
+// One frame call on a host buffer: the job `j` (whole image) is rendered into the device mirrors
+// of `buf` -- pipelined in row bands with PT_FLAG_PIN_HOST on one device, otherwise upload, render,
+// download in turn (every device's share enqueued before any is waited for).
 int render_frame(float* buf, PtJob j, int32_t row_align)
 {
     int rc;
-    const size_t bytes = (size_t)j.width * j.height * 3 * sizeof(float);
     const uint32_t spf = (uint32_t)g.cfg.samples_per_frame;
     bool banded = false;
-    if ((rc = render_bands(buf, j, row_align, [](const PtJob& b) { return launch(b, g.stream, false); }, &banded)))
+    if ((rc = render_bands(buf, j, row_align, [](const PtJob& b) { return launch(g.dev[0], b, g.dev[0].stream, false); },
+                           &banded)))
         return rc;
     if (banded) {
         g.frame += spf;
         HIP_TRY(hipStreamSynchronize(g.s_out));
         return PT_OK;
     }
-    if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
-    j.buf = g.dbuf;
-    if ((rc = launch(j, g.stream, false))) return rc;
+    const Geo geo = geo_of(j.width, j.height, j.layout, j.tile_w, j.tile_h);
+    if ((rc = stage_in(buf, geo, Region{}))) return rc;
+    for (int d = 0; d < g.ndev; ++d)
+        if ((rc = launch(g.dev[d], shard_job(j, d), g.dev[d].stream, false))) return rc;
     g.frame += spf;
-    return stage_out(buf, 0, bytes);
+    return stage_out(buf, geo, Region{});
 }
 
-int grow(void** p, size_t* cap, size_t bytes)
+int grow(Dev& dv, void** p, size_t* cap, size_t bytes)
 {
     if (bytes <= *cap) return PT_OK;
     if (*p) {
-        HIP_TRY(hipStreamSynchronize(g.stream));
+        HIP_TRY(hipStreamSynchronize(dv.stream));
         (void)hipFree(*p);
         *p = nullptr;
         *cap = 0;
@@ -521,6 +723,54 @@ int check_tone_args(const void* accum, const void* out, int32_t w, int32_t h, in
     if (layout != PT_LAYOUT_TILED_PLANAR8) return fail(PT_EINVAL, "unknown layout %d", layout);
     if (tw <= 0 || th <= 0 || tw % 8 || w % tw || h % th)
         return fail(PT_EINVAL, "tiles %dx%d do not divide %dx%d (tile width multiple of 8)", tw, th, w, h);
+    return PT_OK;
+}
+
+PtToneJob tone_job(const float* accum, int32_t w, int32_t h, int32_t layout, int32_t tw, int32_t th, uint32_t* out,
+                   int32_t format)
+{
+    PtToneJob j{};
+    j.accum = accum;
+    j.width = w;
+    j.height = h;
+    j.layout = layout;
+    j.tile_w = tw;
+    j.tile_h = th;
+    j.out = out;
+    j.format = format;
+    j.fast_aces = g.v4cfg.fast_aces;     // USE_FAST_APPROXIMATE_ACES_TONEMAP (flags.h:63)
+    j.fast_gamma = g.v4cfg.fast_gamma;   // USE_FAST_APPROXIMATE_GAMMA (flags.h:62)
+    return j;
+}
+
+// The output stage of the mirrored accumulator, per device on its own rows: every device converts
+// its mirror (its compact rows, or the full-size tiled buffer of which it owns rows d::n) and copies
+// its rows of the w x h pixel image into `out` (host).  Enqueued only; the caller synchronises.
+int tone_mirror(int32_t layout, int32_t tw, int32_t th, uint32_t* out, int32_t format)
+{
+    int rc;
+    const int32_t w = g.m.width, h = g.m.height;
+    const int n = g.ndev;
+    for (int d = 0; d < n; ++d) {
+        Dev& dv = g.dev[d];
+        if ((rc = use_dev(dv))) return rc;
+        const bool compact = n > 1 && layout != PT_LAYOUT_TILED_PLANAR8;
+        const int32_t nr = n > 1 ? shard_rows(h, n, d) : h;
+        if (nr == 0) continue;
+        const int32_t rows = compact ? nr : h;   // rows of the image this device converts
+        if ((rc = grow(dv, (void**)&dv.dtone_out, &dv.dtone_out_cap, (size_t)w * rows * sizeof(uint32_t)))) return rc;
+        const PtToneJob j = tone_job(dv.dbuf, w, rows, layout, tw, th, dv.dtone_out, format);
+        hipError_t e = pt_launch_tonemap(j, dv.stream);
+        if (e != hipSuccess) return fail(PT_EHIP, "tonemap launch failed: %s", hipGetErrorString(e));
+        const size_t row = (size_t)w * sizeof(uint32_t);
+        if (n == 1) {
+            HIP_TRY(hipMemcpyAsync(out, dv.dtone_out, row * h, hipMemcpyDeviceToHost, dv.stream));
+        } else {
+            const uint32_t* src = compact ? dv.dtone_out : dv.dtone_out + (size_t)d * w;
+            HIP_TRY(hipMemcpy2DAsync(out + (size_t)d * w, row * n, src, compact ? row : row * n, row, nr,
+                                     hipMemcpyDeviceToHost, dv.stream));
+        }
+    }
     return PT_OK;
 }
 
@@ -556,13 +806,18 @@ int check_texture(const pt_texture* t)
 
 void release_env()
 {
-    if (g.denv) {
-        (void)hipStreamSynchronize(g.stream);
-        (void)hipFree(g.denv);
+    for (int d = 0; d < g.ndev; ++d) {
+        Dev& dv = g.dev[d];
+        if (dv.denv) {
+            (void)use_dev(dv);
+            (void)hipStreamSynchronize(dv.stream);
+            (void)hipFree(dv.denv);
+        }
+        dv.denv = nullptr;
     }
-    g.denv = nullptr;
     g.env_w = g.env_h = 0;
     g.env_src = nullptr;
+    g.have_env = false;
 }
 
 int upload_env(const pt_texture* t)
@@ -571,15 +826,21 @@ int upload_env(const pt_texture* t)
     if ((rc = check_texture(t))) return rc;
     const size_t bytes = (size_t)t->width * t->height * 3 * sizeof(float);
     release_env();
-    if (hipMalloc(&g.denv, bytes) != hipSuccess) {
-        g.denv = nullptr;
-        return fail(PT_ENOMEM, "hipMalloc(env %zu) failed", bytes);
+    for (int d = 0; d < g.ndev; ++d) {
+        Dev& dv = g.dev[d];
+        if ((rc = use_dev(dv))) return rc;
+        if (hipMalloc(&dv.denv, bytes) != hipSuccess) {
+            dv.denv = nullptr;
+            release_env();
+            return fail(PT_ENOMEM, "hipMalloc(env %zu) failed on device %d", bytes, dv.ordinal);
+        }
+        HIP_TRY(hipMemcpyAsync(dv.denv, t->data, bytes, hipMemcpyHostToDevice, dv.stream));
     }
-    HIP_TRY(hipMemcpyAsync(g.denv, t->data, bytes, hipMemcpyHostToDevice, g.stream));
-    HIP_TRY(hipStreamSynchronize(g.stream));
+    if ((rc = sync_all())) return rc;
     g.env_w = t->width;
     g.env_h = t->height;
     g.env_src = t->data;
+    g.have_env = true;
     return PT_OK;
 }
 
@@ -597,18 +858,15 @@ int check_tile(const pt_buffer_info* b, const pt_tile_info* t)
         return fail(PT_EINVAL, "tile bounds inconsistent with (TileX, TileY, TileWidth, TileHeight)");
     if (t->tile_max_x >= b->width || t->tile_max_y >= b->height) return fail(PT_EINVAL, "tile outside the buffer");
     if (b->width % tw) return fail(PT_EINVAL, "buffer width %d not a multiple of tile width %d", b->width, tw);
+    if (g.ndev > 1 && b->height % th)
+        return fail(PT_EINVAL, "several devices: buffer height %d must be a multiple of the tile height %d", b->height, th);
     return PT_OK;
 }
 
-size_t tile_offset(const pt_buffer_info* b, const pt_tile_info* t)   // in floats (simd_tiled.cpp:499-502)
+// the diffuse-path job of one tile at the current frame (env: the config-4 miss term)
+PtJob tile_job(const pt_buffer_info* b, const pt_tile_info* t, bool env)
 {
-    return (size_t)t->tile_y * t->tile_height * b->width * 3 + (size_t)t->tile_x * t->tile_width * t->tile_height * 3;
-}
-
-// the diffuse-path job of one tile at the current frame (env: the config-4 miss term or nullptr)
-PtJob tile_job(const pt_buffer_info* b, const pt_tile_info* t, const float* env)
-{
-    PtJob j = base_job(g.dbuf, b->width, b->height);
+    PtJob j = base_job(nullptr, b->width, b->height);
     j.layout = PT_LAYOUT_TILED_PLANAR8;
     j.tile_w = t->tile_width;
     j.tile_h = t->tile_height;
@@ -618,10 +876,15 @@ PtJob tile_job(const pt_buffer_info* b, const pt_tile_info* t, const float* env)
     j.nrows = t->tile_height;
     j.frame_first = g.frame - (uint32_t)g.cfg.samples_per_frame + 1;
     if (env) {
-        j.env = env;
         j.env_w = g.env_w;
         j.env_h = g.env_h;
     }
+    return j;
+}
+
+PtJob with_env(PtJob j, const Dev& dv, bool env)
+{
+    if (env) j.env = dv.denv;
     return j;
 }
 
@@ -661,6 +924,8 @@ PtV4Job v4_job(float* buf, int32_t w, int32_t h)
     j.env_mode = PT_V4_ENV_NONE;
     j.random_jitter = g.v4cfg.random_jitter;
     j.rejection = g.v4cfg.rejection;
+    j.accumulate = g.v4cfg.accumulate_frames;   // ACCUMULATE_FRAMES (flags.h:60)
+    j.fast_exp = g.v4cfg.fast_exp;              // USE_FAST_APPROXIMATE_EXP (flags.h:64)
     j.default_scene = pt_v4_is_default_geometry(g.v4scene) ? 1 : 0;
     return j;
 }
@@ -668,19 +933,19 @@ PtV4Job v4_job(float* buf, int32_t w, int32_t h)
 int v4_use_env(PtV4Job& j)
 {
     if (g.v4cfg.env_mode == PT_V4_ENV_NONE) return PT_OK;
-    if (!g.denv) return fail(PT_ESTATE, "v4 env mode %d without an env map", g.v4cfg.env_mode);
+    if (!g.have_env) return fail(PT_ESTATE, "v4 env mode %d without an env map", g.v4cfg.env_mode);
     j.env_mode = g.v4cfg.env_mode;
-    j.env = g.denv;
     j.env_w = g.env_w;
     j.env_h = g.env_h;
     return PT_OK;
 }
 
-int v4_launch(PtV4Job j, hipStream_t st, bool count)
+int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count)
 {
     LaunchSched ls;
     int rc;
-    if ((rc = use_sched(sched_key(j), st, &ls))) return rc;
+    if ((rc = use_dev(dv)) || (rc = use_sched(dv, sched_key(j), st, &ls))) return rc;
+    if (j.env_mode != PT_V4_ENV_NONE) j.env = dv.denv;
     j.queue = ls.queue;
     j.queue_next = ls.queue_next;
     j.order = ls.order;
@@ -689,7 +954,86 @@ int v4_launch(PtV4Job j, hipStream_t st, bool count)
     j.cost = ls.cost;
     hipError_t e = pt_launch_v4(j, g.v4scene, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "v4 render launch failed: %s", hipGetErrorString(e));
-    return queue_done(ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_v4's early return)
+    return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_v4's early return)
+}
+
+// The logical device a device-resident job runs on: the device holding its buffer.
+int dev_of(const void* p, Dev** out)
+{
+    if (g.ndev == 1) {
+        *out = &g.dev[0];
+        return PT_OK;
+    }
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(PT_EINVAL, "device job buffer is not device memory");
+    }
+    for (int d = 0; d < g.ndev; ++d)
+        if (g.dev[d].ordinal == a.device) {
+            *out = &g.dev[d];
+            return PT_OK;
+        }
+    return fail(PT_ESTATE, "device job on device %d, which the library was not initialised with", a.device);
+}
+
+int parse_device_list(const char* s, pt_config* c)
+{
+    if (!s || !*s) return 0;
+    int n = 0;
+    if (!strcmp(s, "all")) {
+        int cnt = 0;
+        if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0) return 0;
+        for (int i = 0; i < cnt && i < PT_MAX_DEVICES; ++i) c->devices[n++] = i;
+    } else {
+        const char* p = s;
+        while (*p && n < PT_MAX_DEVICES) {
+            char* end = nullptr;
+            const long v = strtol(p, &end, 10);
+            if (end == p || v < 0) return 0;
+            c->devices[n++] = (int32_t)v;
+            p = end;
+            while (*p == ',' || *p == ' ') ++p;
+        }
+    }
+    if (n == 0) return 0;
+    c->device = c->devices[0];
+    c->device_count = n;
+    return n;
+}
+
+void free_dev(Dev& dv)
+{
+    if (use_dev(dv)) return;
+    if (dv.stream) (void)hipStreamSynchronize(dv.stream);
+    if (dv.dbuf) (void)hipFree(dv.dbuf);
+    if (dv.dcounters) (void)hipFree(dv.dcounters);
+    if (dv.dscene) (void)hipFree(dv.dscene);
+    if (dv.dqueue) (void)hipFree(dv.dqueue);
+    if (dv.denv) (void)hipFree(dv.denv);
+    if (dv.dtone_in) (void)hipFree(dv.dtone_in);
+    if (dv.dtone_out) (void)hipFree(dv.dtone_out);
+    for (Sched& sc : dv.sched)
+        if (sc.used) free_sched(sc);
+    for (hipEvent_t& e : dv.queue_event)
+        if (e) (void)hipEventDestroy(e);
+    if (dv.stream) (void)hipStreamDestroy(dv.stream);
+    dv = Dev{};
+}
+
+int init_dev(Dev& dv, int32_t ordinal)
+{
+    dv = Dev{};
+    dv.ordinal = ordinal;
+    HIP_TRY(hipSetDevice(ordinal));
+    HIP_TRY(hipStreamCreateWithFlags(&dv.stream, hipStreamNonBlocking));
+    if (hipMalloc(&dv.dcounters, kCounterSlots * sizeof(unsigned long long)) != hipSuccess)
+        return fail(PT_ENOMEM, "hipMalloc(counters) failed");
+    if (hipMalloc(&dv.dqueue, (size_t)kQueueRing * PT_QUEUE_WORDS * sizeof(unsigned)) != hipSuccess)
+        return fail(PT_ENOMEM, "hipMalloc(queue) failed");
+    if (hipMalloc(&dv.dscene, sizeof(PtScene)) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc(scene) failed");
+    HIP_TRY(hipMemcpy(dv.dscene, &g.scene, sizeof(PtScene), hipMemcpyHostToDevice));
+    return PT_OK;
 }
 
 }  // namespace
@@ -714,6 +1058,11 @@ void pt_default_config(pt_config* c)
     c->samples_per_frame = 1;    // NUM_SAMPLES_PER_FRAME, global_preprocessor_flags.h:30
     c->flags = 0;
     c->ambient[0] = c->ambient[1] = c->ambient[2] = 0.1f;   // scalar.cpp:307
+    c->device_count = 1;
+    c->devices[0] = 0;
+    // the devices of a host that never calls pt_init (the reference-shaped drop-in): PT_MI355_DEVICES
+    // = "all" or a list of HIP ordinals ("0,1,2,3"; repeats make logical shards of one GPU)
+    parse_device_list(getenv("PT_MI355_DEVICES"), c);
 }
 
 int pt_init(const pt_config* cfg)
@@ -724,12 +1073,31 @@ int pt_init(const pt_config* cfg)
     if (c.num_bounces < 0 || c.num_bounces > 1024) return fail(PT_EINVAL, "num_bounces %d out of range", c.num_bounces);
     if (c.samples_per_frame < 1 || c.samples_per_frame > 65536)
         return fail(PT_EINVAL, "samples_per_frame %d out of range", c.samples_per_frame);
+    if (c.device_count < 0 || c.device_count > PT_MAX_DEVICES)
+        return fail(PT_EINVAL, "device_count %d out of range [0, %d]", c.device_count, PT_MAX_DEVICES);
+    if (c.device_count <= 1) {   // one device: `device` (devices[] ignored)
+        c.device_count = 1;
+        c.devices[0] = c.device;
+    }
     if (g.inited) pt_shutdown();
+    DeviceGuard guard;
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
-    if (c.device < 0 || c.device >= ndev) return fail(PT_EHIP, "device %d not available (%d devices)", c.device, ndev);
-    HIP_TRY(hipSetDevice(c.device));
-    HIP_TRY(hipStreamCreateWithFlags(&g.stream, hipStreamNonBlocking));
+    for (int d = 0; d < c.device_count; ++d)
+        if (c.devices[d] < 0 || c.devices[d] >= ndev)
+            return fail(PT_EHIP, "device %d not available (%d devices)", c.devices[d], ndev);
+    c.device = c.devices[0];
+    g.cfg = c;
+    pt_build_demofox_scene(&g.scene, c.ambient);
+    int rc;
+    g.ndev = c.device_count;
+    for (int d = 0; d < g.ndev; ++d)
+        if ((rc = init_dev(g.dev[d], c.devices[d]))) {
+            g.inited = true;   // release what was created
+            pt_shutdown();
+            return rc;
+        }
+    HIP_TRY(hipSetDevice(g.dev[0].ordinal));
     HIP_TRY(hipStreamCreateWithFlags(&g.s_in, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&g.s_out, hipStreamNonBlocking));
     for (int k = 0; k < kBands; ++k) {
@@ -737,17 +1105,7 @@ int pt_init(const pt_config* cfg)
         HIP_TRY(hipEventCreateWithFlags(&g.ev_done[k], hipEventDisableTiming));
     }
     HIP_TRY(hipEventCreateWithFlags(&g.ev_q, hipEventDisableTiming));
-    if (hipMalloc(&g.dcounters, kCounterSlots * sizeof(unsigned long long)) != hipSuccess)
-        return fail(PT_ENOMEM, "hipMalloc(counters) failed");
-    if (hipMalloc(&g.dqueue, (size_t)kQueueRing * PT_QUEUE_WORDS * sizeof(unsigned)) != hipSuccess)
-        return fail(PT_ENOMEM, "hipMalloc(queue) failed");
-    g.cfg = c;
-    pt_build_demofox_scene(&g.scene, c.ambient);
-    if (hipMalloc(&g.dscene, sizeof(PtScene)) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc(scene) failed");
-    HIP_TRY(hipMemcpy(g.dscene, &g.scene, sizeof(PtScene), hipMemcpyHostToDevice));
     g.frame = 0;
-    g.queue_next = 0;
-    g.queue_pre_zeroed = false;
     g.inited = true;
     return PT_OK;
 }
@@ -755,19 +1113,9 @@ int pt_init(const pt_config* cfg)
 void pt_shutdown(void)
 {
     if (!g.inited) return;
-    (void)hipSetDevice(g.cfg.device);
-    if (g.stream) (void)hipStreamSynchronize(g.stream);
-    if (g.dbuf) (void)hipFree(g.dbuf);
-    if (g.dcounters) (void)hipFree(g.dcounters);
-    if (g.dscene) (void)hipFree(g.dscene);
-    if (g.dqueue) (void)hipFree(g.dqueue);
-    if (g.denv) (void)hipFree(g.denv);
-    if (g.dtone_in) (void)hipFree(g.dtone_in);
-    if (g.dtone_out) (void)hipFree(g.dtone_out);
-    for (Sched& sc : g.sched)
-        if (sc.used) free_sched(sc);
-    for (hipEvent_t& e : g.queue_event)
-        if (e) (void)hipEventDestroy(e);
+    DeviceGuard guard;
+    for (int d = 0; d < g.ndev; ++d) free_dev(g.dev[d]);
+    if (g.ndev > 0) (void)hipSetDevice(g.cfg.devices[0]);
     unpin();
     for (int k = 0; k < kBands; ++k) {
         if (g.ev_in[k]) (void)hipEventDestroy(g.ev_in[k]);
@@ -776,7 +1124,6 @@ void pt_shutdown(void)
     if (g.ev_q) (void)hipEventDestroy(g.ev_q);
     if (g.s_in) (void)hipStreamDestroy(g.s_in);
     if (g.s_out) (void)hipStreamDestroy(g.s_out);
-    if (g.stream) (void)hipStreamDestroy(g.stream);
     g = State{};
 }
 
@@ -796,6 +1143,7 @@ int pt_render_scalar(float* buf, int32_t w, int32_t h, int32_t nc)
     int rc;
     if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
     if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
+    DeviceGuard guard;
     return render_frame(buf, base_job(nullptr, w, h), 8);
 }
 
@@ -805,6 +1153,7 @@ int pt_render_simd(float* buf, int32_t w, int32_t h, int32_t nc)
     if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
     if (w % 8) return fail(PT_EINVAL, "image width %d must be a multiple of 8 (SIMD lane width)", w);
     if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
+    DeviceGuard guard;
     PtJob j = base_job(nullptr, w, h);
     j.layout = PT_LAYOUT_PLANAR8;
     return render_frame(buf, j, 8);
@@ -816,6 +1165,7 @@ int pt_render_simd_tiled(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t 
     if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
     if ((rc = tiled_settings(w, h, ntx, nty, tw, th))) return rc;
     if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
+    DeviceGuard guard;
     PtJob j = base_job(nullptr, w, h);
     j.layout = PT_LAYOUT_TILED_PLANAR8;
     j.tile_w = tw;
@@ -827,11 +1177,21 @@ int pt_set_env_map(const pt_texture* tex)
 {
     int rc;
     if ((rc = ensure_init())) return rc;
+    DeviceGuard guard;
     if (!tex) {
         release_env();
         return PT_OK;
     }
     return upload_env(tex);
+}
+
+static int ensure_env(const pt_texture* tex)
+{
+    int rc;
+    if ((rc = check_texture(tex))) return rc;
+    if (!g.have_env || g.env_src != tex->data || g.env_w != tex->width || g.env_h != tex->height)
+        return upload_env(tex);
+    return PT_OK;
 }
 
 int pt_render_simt_textured(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty, int32_t tw, int32_t th,
@@ -842,16 +1202,31 @@ int pt_render_simt_textured(float* buf, int32_t w, int32_t h, int32_t ntx, int32
     if ((rc = check_frame_args(buf, w, h, nc)) || (rc = ensure_init())) return rc;
     if ((rc = tiled_settings(w, h, ntx, nty, tw, th)) || (rc = check_texture(tex))) return rc;
     if ((rc = check_frame_budget((uint32_t)g.cfg.samples_per_frame))) return rc;
-    if (!g.denv || g.env_src != tex->data || g.env_w != tex->width || g.env_h != tex->height)
-        if ((rc = upload_env(tex))) return rc;
+    DeviceGuard guard;
+    if ((rc = ensure_env(tex))) return rc;
     PtJob j = base_job(nullptr, w, h);
     j.layout = PT_LAYOUT_TILED_PLANAR8;   // RenderTile, simt_textured.cpp:491-533
     j.tile_w = tw;
     j.tile_h = th;
-    j.env = g.denv;
     j.env_w = g.env_w;
     j.env_h = g.env_h;
-    return render_frame(buf, j, th);
+    const uint32_t spf = (uint32_t)g.cfg.samples_per_frame;
+    bool banded = false;
+    if ((rc = render_bands(buf, j, th, [](const PtJob& b) {
+             return launch(g.dev[0], with_env(b, g.dev[0], true), g.dev[0].stream, false);
+         }, &banded)))
+        return rc;
+    if (banded) {
+        g.frame += spf;
+        HIP_TRY(hipStreamSynchronize(g.s_out));
+        return PT_OK;
+    }
+    const Geo geo = geo_of(w, h, j.layout, tw, th);
+    if ((rc = stage_in(buf, geo, Region{}))) return rc;
+    for (int d = 0; d < g.ndev; ++d)
+        if ((rc = launch(g.dev[d], with_env(shard_job(j, d), g.dev[d], true), g.dev[d].stream, false))) return rc;
+    g.frame += spf;
+    return stage_out(buf, geo, Region{});
 }
 
 int pt_begin_frame(void)
@@ -866,25 +1241,43 @@ int pt_begin_frame(void)
 int pt_render_tile(const pt_buffer_info* b, const pt_tile_info* t)
 {
     int rc;
-    if ((rc = check_tile(b, t)) || (rc = ensure_init())) return rc;
+    if ((rc = ensure_init()) || (rc = check_tile(b, t))) return rc;
     if (g.frame < (uint32_t)g.cfg.samples_per_frame)
         return fail(PT_ESTATE, "RenderTile before the first frame was started (pt_begin_frame)");
-    const int32_t tw = t->tile_width, th = t->tile_height;
-    const size_t bytes = (size_t)b->width * b->height * 3 * sizeof(float);
-    // simd_tiled.cpp:499-502: the tile is one contiguous slice
-    const size_t off = tile_offset(b, t) * sizeof(float);
-    const size_t len = (size_t)tw * th * 3 * sizeof(float);
-    if ((rc = stage_in(b->data, bytes, off, len))) return rc;
-    if ((rc = launch(tile_job(b, t, nullptr), g.stream, false))) return rc;
-    return stage_out(b->data, off, len);
+    DeviceGuard guard;
+    const Geo geo = geo_of(b->width, b->height, PT_LAYOUT_TILED_PLANAR8, t->tile_width, t->tile_height);
+    Region rg;
+    rg.whole = false;
+    rg.tile_x = t->tile_x;
+    rg.tile_y = t->tile_y;
+    if ((rc = stage_in(b->data, geo, rg))) return rc;
+    const PtJob j = tile_job(b, t, false);
+    for (int d = 0; d < g.ndev; ++d)
+        if ((rc = launch(g.dev[d], tile_shard_job(j, d), g.dev[d].stream, false))) return rc;
+    return stage_out(b->data, geo, rg);
 }
 
 int pt_readback(float* buf)
 {
-    if (!g.inited || !g.dbuf || !g.mirror_valid || buf != g.mirror_host)
+    if (!g.inited || !g.m.valid || buf != g.m.host)
         return fail(PT_ESTATE, "no deferred device accumulator for this buffer");
-    HIP_TRY(hipMemcpyAsync(buf, g.dbuf, g.mirror_bytes, hipMemcpyDeviceToHost, g.stream));
-    HIP_TRY(hipStreamSynchronize(g.stream));
+    DeviceGuard guard;
+    int rc;
+    const Geo geo = mirror_geo();
+    for (int d = 0; d < g.ndev; ++d)
+        if ((rc = use_dev(g.dev[d])) || (rc = xfer(d, geo, buf, false, Region{}))) return rc;
+    return sync_all();
+}
+
+int pt_release_buffer(const void* buf)
+{
+    if (!g.inited) return PT_OK;
+    DeviceGuard guard;
+    if (!buf || buf == (const void*)g.m.host) {
+        (void)sync_all();   // nothing in flight may still copy into it
+        drop_mirror();
+    }
+    if (g.pinned && (!buf || buf == (const void*)g.pinned)) unpin();
     return PT_OK;
 }
 
@@ -912,8 +1305,7 @@ static int device_job(const pt_device_job* dj, PtJob* j)
     j->nframes = dj->nframes;
     j->num_bounces = dj->num_bounces;
     if (dj->use_env) {
-        if (!g.denv) return fail(PT_ESTATE, "use_env without an env map (pt_set_env_map)");
-        j->env = g.denv;
+        if (!g.have_env) return fail(PT_ESTATE, "use_env without an env map (pt_set_env_map)");
         j->env_w = g.env_w;
         j->env_h = g.env_h;
     }
@@ -946,7 +1338,10 @@ int pt_tonemap_device(const float* accum, int32_t w, int32_t h, int32_t layout, 
 {
     int rc;
     if ((rc = ensure_init()) || (rc = check_tone_args(accum, out, w, h, layout, tw, th, format))) return rc;
-    const PtToneJob j{accum, w, h, layout, tw, th, out, format};
+    DeviceGuard guard;
+    Dev* dv = nullptr;
+    if ((rc = dev_of(accum, &dv)) || (rc = use_dev(*dv))) return rc;
+    const PtToneJob j = tone_job(accum, w, h, layout, tw, th, out, format);
     hipError_t e = pt_launch_tonemap(j, (hipStream_t)stream);
     if (e != hipSuccess) return fail(PT_EHIP, "tonemap launch failed: %s", hipGetErrorString(e));
     return PT_OK;
@@ -957,21 +1352,25 @@ int pt_tonemap(const float* accum, int32_t w, int32_t h, int32_t layout, int32_t
 {
     int rc;
     if ((rc = ensure_init()) || (rc = check_tone_args(accum, out, w, h, layout, tw, th, format))) return rc;
+    DeviceGuard guard;
     const size_t in_bytes = (size_t)w * h * 3 * sizeof(float), out_bytes = (size_t)w * h * sizeof(uint32_t);
-    const float* src = nullptr;
-    if (g.mirror_valid && accum == g.mirror_host && g.mirror_bytes == in_bytes) {
-        src = g.dbuf;   // the deferred accumulator is already in HBM
-    } else {
-        if ((rc = grow((void**)&g.dtone_in, &g.dtone_in_cap, in_bytes))) return rc;
-        HIP_TRY(hipMemcpyAsync(g.dtone_in, accum, in_bytes, hipMemcpyHostToDevice, g.stream));
-        src = g.dtone_in;
+    const bool tiled = layout == PT_LAYOUT_TILED_PLANAR8;
+    if (g.m.valid && accum == g.m.host && g.m.bytes == in_bytes && g.m.width == w && g.m.height == h &&
+        (g.ndev == 1 || (g.m.tiled == tiled && (!tiled || (g.m.tile_w == tw && g.m.tile_h == th))))) {
+        // the deferred accumulator is already in HBM: each device converts its own rows
+        if ((rc = tone_mirror(layout, tw, th, out, format))) return rc;
+        return sync_all();
     }
-    if ((rc = grow((void**)&g.dtone_out, &g.dtone_out_cap, out_bytes))) return rc;
-    const PtToneJob j{src, w, h, layout, tw, th, g.dtone_out, format};
-    hipError_t e = pt_launch_tonemap(j, g.stream);
+    Dev& dv = g.dev[0];
+    if ((rc = use_dev(dv))) return rc;
+    if ((rc = grow(dv, (void**)&dv.dtone_in, &dv.dtone_in_cap, in_bytes))) return rc;
+    HIP_TRY(hipMemcpyAsync(dv.dtone_in, accum, in_bytes, hipMemcpyHostToDevice, dv.stream));
+    if ((rc = grow(dv, (void**)&dv.dtone_out, &dv.dtone_out_cap, out_bytes))) return rc;
+    const PtToneJob j = tone_job(dv.dtone_in, w, h, layout, tw, th, dv.dtone_out, format);
+    hipError_t e = pt_launch_tonemap(j, dv.stream);
     if (e != hipSuccess) return fail(PT_EHIP, "tonemap launch failed: %s", hipGetErrorString(e));
-    HIP_TRY(hipMemcpyAsync(out, g.dtone_out, out_bytes, hipMemcpyDeviceToHost, g.stream));
-    HIP_TRY(hipStreamSynchronize(g.stream));
+    HIP_TRY(hipMemcpyAsync(out, dv.dtone_out, out_bytes, hipMemcpyDeviceToHost, dv.stream));
+    HIP_TRY(hipStreamSynchronize(dv.stream));
     return PT_OK;
 }
 
@@ -979,25 +1378,26 @@ int pt_render_device(const pt_device_job* dj, void* stream)
 {
     int rc;
     PtJob j;
-    if ((rc = ensure_init()) || (rc = device_job(dj, &j))) return rc;
+    Dev* dv = nullptr;
+    DeviceGuard guard;
+    if ((rc = ensure_init()) || (rc = device_job(dj, &j)) || (rc = dev_of(dj->buf, &dv))) return rc;
+    if (dj->use_env) j.env = dv->denv;
 #if PT_DIAG   // diagnostic build: with PT_DIAG_OUT set, a device launch records and dumps its
               // timeline (synchronous); without it launches run as usual (warm-up at full clocks)
-    if (!getenv("PT_DIAG_OUT")) return launch(j, (hipStream_t)stream, false);
+    if (!getenv("PT_DIAG_OUT")) return launch(*dv, j, (hipStream_t)stream, false);
     hipStream_t st = (hipStream_t)stream;
-    const char* mode = getenv("PT_DIAG_MODE");   // experiment switches: "nomemset", "nocounters"
-    const bool nomemset = mode && !strcmp(mode, "nomemset"), nocounters = mode && !strcmp(mode, "nocounters");
-    HIP_TRY(hipMemsetAsync(g.dcounters, 0, (nomemset ? 32 + 4 * 65536 : kCounterSlots) * sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(g.dcounters + PT_CNT_N + 9, 0xff, sizeof(unsigned long long), st));
-    HIP_TRY(hipMemsetAsync(g.dcounters + PT_CNT_N + 12, 0xff, sizeof(unsigned long long), st));
-    j.counters = nocounters ? nullptr : g.dcounters;
-    if ((rc = launch(j, st, false))) return rc;
+    HIP_TRY(hipMemsetAsync(dv->dcounters, 0, kCounterSlots * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(dv->dcounters + PT_CNT_N + 9, 0xff, sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(dv->dcounters + PT_CNT_N + 12, 0xff, sizeof(unsigned long long), st));
+    j.counters = dv->dcounters;
+    if ((rc = launch(*dv, j, st, false))) return rc;
     static unsigned long long h[kCounterSlots];
-    HIP_TRY(hipMemcpyAsync(h, g.dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(h, dv->dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     diag_dump(h);
     return PT_OK;
 #else
-    return launch(j, (hipStream_t)stream, false);
+    return launch(*dv, j, (hipStream_t)stream, false);
 #endif
 }
 
@@ -1005,18 +1405,21 @@ int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
 {
     int rc;
     PtJob j;
+    Dev* dv = nullptr;
+    DeviceGuard guard;
     if (!out) return fail(PT_EINVAL, "null counts");
-    if ((rc = ensure_init()) || (rc = device_job(dj, &j))) return rc;
+    if ((rc = ensure_init()) || (rc = device_job(dj, &j)) || (rc = dev_of(dj->buf, &dv)) || (rc = use_dev(*dv))) return rc;
+    if (dj->use_env) j.env = dv->denv;
     hipStream_t st = (hipStream_t)stream;
-    HIP_TRY(hipMemsetAsync(g.dcounters, 0, kCounterSlots * sizeof(unsigned long long), st));
+    HIP_TRY(hipMemsetAsync(dv->dcounters, 0, kCounterSlots * sizeof(unsigned long long), st));
 #if PT_DIAG
-    HIP_TRY(hipMemsetAsync(g.dcounters + PT_CNT_N + 9, 0xff, sizeof(unsigned long long), st));    // min
-    HIP_TRY(hipMemsetAsync(g.dcounters + PT_CNT_N + 12, 0xff, sizeof(unsigned long long), st));   // min
+    HIP_TRY(hipMemsetAsync(dv->dcounters + PT_CNT_N + 9, 0xff, sizeof(unsigned long long), st));    // min
+    HIP_TRY(hipMemsetAsync(dv->dcounters + PT_CNT_N + 12, 0xff, sizeof(unsigned long long), st));   // min
 #endif
-    j.counters = g.dcounters;
-    if ((rc = launch(j, st, true))) return rc;
+    j.counters = dv->dcounters;
+    if ((rc = launch(*dv, j, st, true))) return rc;
     static unsigned long long h[kCounterSlots];
-    HIP_TRY(hipMemcpyAsync(h, g.dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(h, dv->dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
 #if PT_DIAG
     diag_dump(h);
@@ -1032,6 +1435,21 @@ int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
     return PT_OK;
 }
 
+int32_t pt_initialized_device(void) { return g.inited ? g.dev[0].ordinal : -1; }
+
+int32_t pt_device_count(void) { return g.inited ? g.ndev : 0; }
+
+int32_t pt_device_ordinal(int32_t i) { return g.inited && i >= 0 && i < g.ndev ? g.dev[i].ordinal : -1; }
+
+int pt_unpin_host(const void* buf)
+{
+    if (!g.inited || !g.pinned) return PT_OK;
+    if (buf && buf != (const void*)g.pinned) return PT_OK;
+    DeviceGuard guard;
+    unpin();
+    return PT_OK;
+}
+
 // ---- v4 renderer -------------------------------------------------------------------------------
 
 void pt_v4_default_config(pt_v4_config* c)
@@ -1042,6 +1460,10 @@ void pt_v4_default_config(pt_v4_config* c)
     c->rejection = 1;                   // USE_UNIT_VECTOR_REJECTION_SAMPLING 1
     c->num_bounces = 8;                 // c_numBounces, v4 :23
     c->output_to_screen = 1;            // OUTPUT_TO_SCREEN = !RENDER_OFFLINE
+    c->accumulate_frames = 1;           // ACCUMULATE_FRAMES 1
+    c->fast_aces = 1;                   // USE_FAST_APPROXIMATE_ACES_TONEMAP 1
+    c->fast_gamma = 1;                  // USE_FAST_APPROXIMATE_GAMMA 1
+    c->fast_exp = 1;                    // USE_FAST_APPROXIMATE_EXP 1
 }
 
 int pt_v4_set_config(const pt_v4_config* c)
@@ -1053,6 +1475,17 @@ int pt_v4_set_config(const pt_v4_config* c)
     g.v4cfg.random_jitter = c->random_jitter != 0;
     g.v4cfg.rejection = c->rejection != 0;
     g.v4cfg.output_to_screen = c->output_to_screen != 0;
+    g.v4cfg.accumulate_frames = c->accumulate_frames != 0;
+    g.v4cfg.fast_aces = c->fast_aces != 0;
+    g.v4cfg.fast_gamma = c->fast_gamma != 0;
+    g.v4cfg.fast_exp = c->fast_exp != 0;
+    return PT_OK;
+}
+
+int pt_v4_get_config(pt_v4_config* c)
+{
+    if (!c) return fail(PT_EINVAL, "null v4 config");
+    *c = g.v4cfg;
     return PT_OK;
 }
 
@@ -1065,20 +1498,9 @@ int pt_v4_initialize_global_render_resources(void)
 
 int pt_v4_reinitialize_render_tile_data(void)
 {
-    // Resize reallocated the render target (Application.cpp:142-154): the old buffer's page-lock
-    // must not outlive it
-    if (g.inited) unpin();
-    return PT_OK;
-}
-
-int32_t pt_initialized_device(void) { return g.inited ? g.cfg.device : -1; }
-
-int pt_unpin_host(const void* buf)
-{
-    if (!g.inited || !g.pinned) return PT_OK;
-    if (buf && buf != (const void*)g.pinned) return PT_OK;
-    unpin();
-    return PT_OK;
+    // Resize reallocated the render target (Application.cpp:142-154): the old buffer is gone, so
+    // neither its page-lock nor its deferred device copy may outlive it (dropped, not written back)
+    return pt_release_buffer(nullptr);
 }
 
 int pt_v4_initialize_scene(void)
@@ -1170,41 +1592,46 @@ int pt_render_opt_v4(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty,
     if ((int64_t)ntx * nty > 1024) return fail(PT_EINVAL, "%d x %d tiles exceed NumMaxThreads (1024, v4 :1341)", ntx, nty);
     if ((rc = v4_ensure_scene())) return rc;
     if (g.v4_frame + 1u >= kMaxFrame) return fail(PT_EINVAL, "v4 frame counter exceeds the exact f32 range 2^24");
+    DeviceGuard guard;
     if (g.v4cfg.env_mode != PT_V4_ENV_NONE) {
         if (!tex) return fail(PT_EINVAL, "env mode %d needs a texture", g.v4cfg.env_mode);
-        if ((rc = check_texture(tex))) return rc;
-        if (!g.denv || g.env_src != tex->data || g.env_w != tex->width || g.env_h != tex->height)
-            if ((rc = upload_env(tex))) return rc;
+        if ((rc = ensure_env(tex))) return rc;
     }
-    const size_t bytes = (size_t)w * h * 3 * sizeof(float);
     PtV4Job j = v4_job(nullptr, w, h);
     j.layout = PT_LAYOUT_TILED_PLANAR8;   // RenderTile v4 :1186-1191
     j.tile_w = tw;
     j.tile_h = th;
     if ((rc = v4_use_env(j))) return rc;
     bool banded = false;   // PT_FLAG_PIN_HOST: bands of whole tile rows
-    if ((rc = render_bands(buf, j, th, [](const PtV4Job& b) { return v4_launch(b, g.stream, false); }, &banded)))
+    if ((rc = render_bands(buf, j, th, [](const PtV4Job& b) { return v4_launch(g.dev[0], b, g.dev[0].stream, false); },
+                           &banded)))
         return rc;
+    const Geo geo = geo_of(w, h, PT_LAYOUT_TILED_PLANAR8, tw, th);
     if (!banded) {
-        if ((rc = stage_in(buf, bytes, 0, bytes))) return rc;
-        j.buf = g.dbuf;
-        if ((rc = v4_launch(j, g.stream, false))) return rc;
+        if ((rc = stage_in(buf, geo, Region{}))) return rc;
+        for (int d = 0; d < g.ndev; ++d)
+            if ((rc = v4_launch(g.dev[d], shard_job(j, d), g.dev[d].stream, false))) return rc;
     }
     g.v4_frame += 1;   // iFrame += 1.0f (v4 :1703), before rendering
     if (screen && g.v4cfg.output_to_screen) {   // OutputToScreen per tile (v4 :1562-1564)
-        const size_t out_bytes = (size_t)w * h * sizeof(uint32_t);
-        if ((rc = grow((void**)&g.dtone_out, &g.dtone_out_cap, out_bytes))) return rc;
-        const PtToneJob tj{g.dbuf, w, h, PT_LAYOUT_TILED_PLANAR8, tw, th, g.dtone_out, PT_PIXEL_XRGB8};
-        hipError_t e = pt_launch_tonemap(tj, g.stream);
-        if (e != hipSuccess) return fail(PT_EHIP, "tonemap launch failed: %s", hipGetErrorString(e));
-        HIP_TRY(hipMemcpyAsync(screen, g.dtone_out, out_bytes, hipMemcpyDeviceToHost, g.stream));
+        if (banded) {
+            Dev& dv = g.dev[0];
+            const size_t out_bytes = (size_t)w * h * sizeof(uint32_t);
+            if ((rc = grow(dv, (void**)&dv.dtone_out, &dv.dtone_out_cap, out_bytes))) return rc;
+            const PtToneJob tj = tone_job(dv.dbuf, w, h, PT_LAYOUT_TILED_PLANAR8, tw, th, dv.dtone_out, PT_PIXEL_XRGB8);
+            hipError_t e = pt_launch_tonemap(tj, dv.stream);
+            if (e != hipSuccess) return fail(PT_EHIP, "tonemap launch failed: %s", hipGetErrorString(e));
+            HIP_TRY(hipMemcpyAsync(screen, dv.dtone_out, out_bytes, hipMemcpyDeviceToHost, dv.stream));
+        } else if ((rc = tone_mirror(PT_LAYOUT_TILED_PLANAR8, tw, th, (uint32_t*)screen, PT_PIXEL_XRGB8))) {
+            return rc;
+        }
     }
     if (banded) {
         HIP_TRY(hipStreamSynchronize(g.s_out));
-        HIP_TRY(hipStreamSynchronize(g.stream));
+        HIP_TRY(hipStreamSynchronize(g.dev[0].stream));
         return PT_OK;
     }
-    return stage_out(buf, 0, bytes);
+    return stage_out(buf, geo, Region{});
 }
 
 int pt_copy_output_to_file(const float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty, int32_t tw, int32_t th,
@@ -1246,22 +1673,26 @@ int pt_v4_render_device(const pt_device_job* dj, void* stream)
 {
     int rc;
     PtV4Job j;
-    if ((rc = ensure_init()) || (rc = v4_device_job(dj, &j))) return rc;
-    return v4_launch(j, (hipStream_t)stream, false);
+    Dev* dv = nullptr;
+    DeviceGuard guard;
+    if ((rc = ensure_init()) || (rc = v4_device_job(dj, &j)) || (rc = dev_of(dj->buf, &dv))) return rc;
+    return v4_launch(*dv, j, (hipStream_t)stream, false);
 }
 
 int pt_v4_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
 {
     int rc;
     PtV4Job j;
+    Dev* dv = nullptr;
+    DeviceGuard guard;
     if (!out) return fail(PT_EINVAL, "null counts");
-    if ((rc = ensure_init()) || (rc = v4_device_job(dj, &j))) return rc;
+    if ((rc = ensure_init()) || (rc = v4_device_job(dj, &j)) || (rc = dev_of(dj->buf, &dv)) || (rc = use_dev(*dv))) return rc;
     hipStream_t st = (hipStream_t)stream;
-    HIP_TRY(hipMemsetAsync(g.dcounters, 0, kCounterSlots * sizeof(unsigned long long), st));
-    j.counters = g.dcounters;
-    if ((rc = v4_launch(j, st, true))) return rc;
+    HIP_TRY(hipMemsetAsync(dv->dcounters, 0, kCounterSlots * sizeof(unsigned long long), st));
+    j.counters = dv->dcounters;
+    if ((rc = v4_launch(*dv, j, st, true))) return rc;
     unsigned long long h[6];
-    HIP_TRY(hipMemcpyAsync(h, g.dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(h, dv->dcounters, sizeof(h), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     out->segments = h[0];
     out->lane_slots = h[3];
@@ -1293,9 +1724,10 @@ struct pt_work_queue {
 
 namespace {
 
-// Render the queued entries: per buffer (in first-use order) either one full-frame launch (the
-// entries are exactly the buffer's NTX x NTY tiles) or one launch per tile; uploads / downloads of
-// only what is rendered.  Everything is enqueued on g.stream; `wait` synchronises at the end.
+// Render the queued entries: per buffer (in first-use order) either one full-frame launch per device
+// (the entries are exactly the buffer's NTX x NTY tiles) or per tile one launch per device; uploads /
+// downloads of only what is rendered.  Everything is enqueued on the device streams; `wait`
+// synchronises at the end.
 int run_queue(pt_work_queue* q, bool wait)
 {
     int rc;
@@ -1307,11 +1739,10 @@ int run_queue(pt_work_queue* q, bool wait)
     } else if (g.frame < (uint32_t)g.cfg.samples_per_frame) {
         return fail(PT_ESTATE, "work queue before the first frame was started (pt_begin_frame)");
     }
-    const float* env = nullptr;
-    if (q->renderer == PT_RENDERER_SIMT_TEXTURED) {
-        if (!g.denv) return fail(PT_ESTATE, "textured work queue without an env map (pt_set_env_map)");
-        env = g.denv;
-    }
+    const bool env = q->renderer == PT_RENDERER_SIMT_TEXTURED;
+    if (env && !g.have_env) return fail(PT_ESTATE, "textured work queue without an env map (pt_set_env_map)");
+    DeviceGuard guard;
+    Dev& d0 = g.dev[0];
     std::vector<bool> done(q->entries.size(), false);
     for (size_t i = 0; i < q->entries.size(); ++i) {
         if (done[i]) continue;
@@ -1327,6 +1758,11 @@ int run_queue(pt_work_queue* q, bool wait)
             }
         const pt_tile_info& t0 = q->entries[mine[0]].second;
         const int32_t tw = t0.tile_width, th = t0.tile_height;
+        for (size_t k : mine) {
+            const pt_tile_info& t = q->entries[k].second;
+            if (t.tile_width != tw || t.tile_height != th)
+                return fail(PT_EINVAL, "entries of one buffer disagree on the tile size");
+        }
         bool full = b.width % tw == 0 && b.height % th == 0 &&
                     mine.size() == (size_t)(b.width / tw) * (size_t)(b.height / th);
         if (full) {   // exactly every tile once?
@@ -1334,22 +1770,22 @@ int run_queue(pt_work_queue* q, bool wait)
             for (size_t k : mine) {
                 const pt_tile_info& t = q->entries[k].second;
                 const size_t id = (size_t)t.tile_y * (b.width / tw) + t.tile_x;
-                if (t.tile_width != tw || t.tile_height != th || seen[id]) {
+                if (seen[id]) {
                     full = false;
                     break;
                 }
                 seen[id] = 1;
             }
         }
-        const size_t bytes = (size_t)b.width * b.height * 3 * sizeof(float);
-        const size_t tlen = (size_t)tw * th * 3 * sizeof(float);
-        if (full && (g.cfg.flags & PT_FLAG_PIN_HOST) && !(g.cfg.flags & PT_FLAG_DEFER_READBACK)) {
+        const Geo geo = geo_of(b.width, b.height, PT_LAYOUT_TILED_PLANAR8, tw, th);
+        if (full && g.ndev == 1 && (g.cfg.flags & PT_FLAG_PIN_HOST) && !(g.cfg.flags & PT_FLAG_DEFER_READBACK)) {
             // A whole frame of tiles with PT_FLAG_PIN_HOST: the frame calls' band pipeline (bands of
             // whole tile rows, upload / render / download overlapped on three streams).  The bands'
             // copies run on s_in / s_out, so they are ordered after the work already queued on
-            // g.stream (an earlier buffer's download from the mirror), and g.stream -- which the
-            // completion calls synchronise -- after the last download.
-            HIP_TRY(hipEventRecord(g.ev_q, g.stream));
+            // the device stream (an earlier buffer's download from the mirror), and that stream --
+            // which the completion calls synchronise -- after the last download.
+            if ((rc = use_dev(d0))) return rc;
+            HIP_TRY(hipEventRecord(g.ev_q, d0.stream));
             HIP_TRY(hipStreamWaitEvent(g.s_in, g.ev_q, 0));
             bool banded = false;
             if (v4) {
@@ -1359,7 +1795,8 @@ int run_queue(pt_work_queue* q, bool wait)
                 j.tile_h = th;
                 j.frame_first = g.v4_frame;
                 if ((rc = v4_use_env(j))) return rc;
-                rc = render_bands(b.data, j, th, [](const PtV4Job& bj) { return v4_launch(bj, g.stream, false); }, &banded);
+                rc = render_bands(b.data, j, th, [](const PtV4Job& bj) { return v4_launch(g.dev[0], bj, g.dev[0].stream, false); },
+                                  &banded);
             } else {
                 pt_tile_info t = t0;
                 t.tile_min_x = 0;
@@ -1367,73 +1804,76 @@ int run_queue(pt_work_queue* q, bool wait)
                 PtJob j = tile_job(&b, &t, env);
                 j.ncols = b.width;
                 j.nrows = b.height;
-                rc = render_bands(b.data, j, th, [](const PtJob& bj) { return launch(bj, g.stream, false); }, &banded);
+                if (env)
+                    rc = render_bands(b.data, j, th, [](const PtJob& bj) {
+                        return launch(g.dev[0], with_env(bj, g.dev[0], true), g.dev[0].stream, false);
+                    }, &banded);
+                else
+                    rc = render_bands(b.data, j, th, [](const PtJob& bj) { return launch(g.dev[0], bj, g.dev[0].stream, false); },
+                                      &banded);
             }
             if (rc) return rc;
             if (banded) {
                 HIP_TRY(hipEventRecord(g.ev_q, g.s_out));
-                HIP_TRY(hipStreamWaitEvent(g.stream, g.ev_q, 0));
+                HIP_TRY(hipStreamWaitEvent(d0.stream, g.ev_q, 0));
                 continue;
             }
         }
+        // one job per device for the whole frame, or per tile
+        std::vector<Region> regions;
         if (full) {
-            if ((rc = stage_in(b.data, bytes, 0, bytes))) return rc;
+            regions.push_back(Region{});
         } else {
             for (size_t k : mine) {
-                const pt_tile_info& t = q->entries[k].second;
-                if ((rc = stage_in(b.data, bytes, tile_offset(&b, &t) * sizeof(float),
-                                   (size_t)t.tile_width * t.tile_height * 3 * sizeof(float))))
-                    return rc;
+                Region rg;
+                rg.whole = false;
+                rg.tile_x = q->entries[k].second.tile_x;
+                rg.tile_y = q->entries[k].second.tile_y;
+                regions.push_back(rg);
             }
         }
-        // one job for the whole frame, or one per tile
-        const size_t njobs = full ? 1 : mine.size();
-        for (size_t n = 0; n < njobs; ++n) {
-            pt_tile_info t = q->entries[mine[n]].second;
-            if (full) {   // the frame as one "tile" region in the tiled layout
-                t.tile_min_x = 0;
-                t.tile_min_y = 0;
-            }
-            if (v4) {
-                PtV4Job j = v4_job(g.dbuf, b.width, b.height);
-                j.layout = PT_LAYOUT_TILED_PLANAR8;
-                j.tile_w = t.tile_width;
-                j.tile_h = t.tile_height;
-                j.col0 = t.tile_min_x;
-                j.ncols = full ? b.width : t.tile_width;
-                j.row_start = t.tile_min_y;
-                j.nrows = full ? b.height : t.tile_height;
-                j.frame_first = g.v4_frame;   // the frame pt_v4_begin_frame started
-                if ((rc = v4_use_env(j)) || (rc = v4_launch(j, g.stream, false))) return rc;
-            } else {
-                PtJob j = tile_job(&b, &t, env);
-                if (full) {
-                    j.ncols = b.width;
-                    j.nrows = b.height;
-                }
-                if ((rc = launch(j, g.stream, false))) return rc;
-            }
-        }
-        if (!(g.cfg.flags & PT_FLAG_DEFER_READBACK)) {
-            if (full) {
-                HIP_TRY(hipMemcpyAsync(b.data, g.dbuf, bytes, hipMemcpyDeviceToHost, g.stream));
-            } else {
-                for (size_t k : mine) {
-                    const pt_tile_info& t = q->entries[k].second;
-                    const size_t off = tile_offset(&b, &t) * sizeof(float);
-                    HIP_TRY(hipMemcpyAsync((char*)b.data + off, (const char*)g.dbuf + off,
-                                           (size_t)t.tile_width * t.tile_height * 3 * sizeof(float),
-                                           hipMemcpyDeviceToHost, g.stream));
+        for (const Region& rg : regions)
+            if ((rc = stage_in(b.data, geo, rg))) return rc;
+        for (const Region& rg : regions) {
+            // the frame as one "tile" region in the tiled layout, or the entry's tile
+            const int32_t col0 = rg.whole ? 0 : rg.tile_x * tw, row0 = rg.whole ? 0 : rg.tile_y * th;
+            const int32_t ncols = rg.whole ? b.width : tw, nrows = rg.whole ? b.height : th;
+            for (int d = 0; d < g.ndev; ++d) {
+                Dev& dv = g.dev[d];
+                if (v4) {
+                    PtV4Job j = v4_job(nullptr, b.width, b.height);
+                    j.layout = PT_LAYOUT_TILED_PLANAR8;
+                    j.tile_w = tw;
+                    j.tile_h = th;
+                    j.col0 = col0;
+                    j.ncols = ncols;
+                    j.row_start = row0;
+                    j.nrows = nrows;
+                    j.frame_first = g.v4_frame;   // the frame pt_v4_begin_frame started
+                    if ((rc = v4_use_env(j)) || (rc = v4_launch(dv, tile_shard_job(j, d), dv.stream, false))) return rc;
+                } else {
+                    pt_tile_info t{};
+                    t.tile_width = tw;
+                    t.tile_height = th;
+                    t.tile_min_x = col0;
+                    t.tile_min_y = row0;
+                    PtJob j = tile_job(&b, &t, env);
+                    j.ncols = ncols;
+                    j.nrows = nrows;
+                    if ((rc = launch(dv, with_env(tile_shard_job(j, d), dv, env), dv.stream, false))) return rc;
                 }
             }
         }
-        (void)tlen;
+        if (!(g.cfg.flags & PT_FLAG_DEFER_READBACK))
+            for (const Region& rg : regions)
+                for (int d = 0; d < g.ndev; ++d)
+                    if ((rc = use_dev(g.dev[d])) || (rc = xfer(d, geo, b.data, false, rg))) return rc;
         // the mirror holds one buffer at a time: another buffer of the queue must not start
         // overwriting it before this one's downloads are done (stream order guarantees that)
     }
     q->entries.clear();
     if (wait) {
-        HIP_TRY(hipStreamSynchronize(g.stream));
+        if ((rc = sync_all())) return rc;
         q->pending = false;
     } else {
         q->pending = true;
@@ -1487,7 +1927,11 @@ int pt_complete_all_work_async(pt_work_queue* q)
 int pt_wait_work(pt_work_queue* q)
 {
     if (!q) return fail(PT_EINVAL, "null queue");
-    if (q->pending && g.inited) HIP_TRY(hipStreamSynchronize(g.stream));
+    if (q->pending && g.inited) {
+        DeviceGuard guard;
+        int rc;
+        if ((rc = sync_all())) return rc;
+    }
     q->pending = false;
     return PT_OK;
 }
@@ -1497,7 +1941,10 @@ int32_t pt_work_queue_size(const pt_work_queue* q) { return q ? (int32_t)q->entr
 void pt_free_work_queue(pt_work_queue* q)
 {
     if (!q) return;
-    if (q->pending && g.inited) (void)hipStreamSynchronize(g.stream);
+    if (q->pending && g.inited) {
+        DeviceGuard guard;
+        (void)sync_all();
+    }
     delete q;
 }
 

@@ -46,27 +46,12 @@ __device__ __forceinline__ float div_rn(float a, float b, float y)
 // tests/native/exactmath_probe.hip: 1 912 602 624 inputs, 0 mismatches; v_sqrt_f32 alone misses
 // 15 % of them).  Five VALU operations, none a compare or select: the previous neighbour check
 // around v_sqrt_f32 needed two compares and two selects.
-#ifndef PT_SQRT_MARKSTEIN
-#define PT_SQRT_MARKSTEIN 1
-#endif
 __device__ __forceinline__ float sqrt_rn(float x)
 {
-#if PT_SQRT_MARKSTEIN
     const float y = __builtin_amdgcn_rsqf(x);
     const float s = x * y, h = 0.5f * y;
     const float r = __builtin_fmaf(-s, s, x);
     return __builtin_fmaf(r, h, s);
-#else   // hardware square root, then a neighbour check with exact FMA residuals
-    const float s = sqrt_approx(x);
-    const float s_dn = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, s) - 1u);
-    const float s_up = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, s) + 1u);
-    const float r_dn = __builtin_fmaf(-s_dn, s, x);   // x - s_dn*s  (> 0 iff x > s_dn*s)
-    const float r_up = __builtin_fmaf(-s_up, s, x);   // x - s_up*s
-    float res = s;
-    res = (r_dn <= 0.0f) ? s_dn : res;
-    res = (r_up > 0.0f) ? s_up : res;
-    return res;
-#endif
 }
 
 // General-purpose guarded forms: the fast path where its preconditions provably hold, IEEE

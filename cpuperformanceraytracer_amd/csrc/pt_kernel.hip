@@ -44,13 +44,6 @@
 #include <math.h>
 #include <algorithm>
 
-#ifndef PT_AXIS_FROM_LDS
-#define PT_AXIS_FROM_LDS 1   // 0: select from literals (177 VGPRs, 0.89 ms) vs LDS row (127, 0.79 ms)
-#endif
-#ifndef PT_TRACE_UNROLL
-#define PT_TRACE_UNROLL 6   // primitive loops fully unrolled: the constexpr geometry becomes
-#endif                      // instruction literals (rolled: 1.05 ms vs 0.81 ms per 1080p step)
-
 namespace {
 
 struct V3 {
@@ -84,15 +77,6 @@ __device__ __forceinline__ float rcp_x(float x)
 // comparisons (see quad_test) or cannot occur (camera: 0 <= a <= 2^24).
 __device__ __forceinline__ float div_x(float a, float b, float y) { return pt::div_rn(a, b, y); }
 
-#ifndef PT_QUAD_CULL
-#define PT_QUAD_CULL 1   // one exact quad test per ray (pt_quadcull.h), the six exact tests as fallback
-#endif
-#ifndef PT_ENV_CULL
-#define PT_ENV_CULL 1    // the env kernel too (vertices from the per-axis rows, no extra LDS)
-#endif
-#ifndef PT_CULL_SPHERES_FIRST
-#define PT_CULL_SPHERES_FIRST 0   // 1: sphere distances computed while the culled quad's LDS record
-#endif                            // loads (straight-line, all lanes): measured slower (0.334 vs 0.318 ms)
 }  // namespace
 #define PTQC_HD __device__ __forceinline__
 #define PTQC_RCP_APPROX(x) pt::rcp_approx(x)
@@ -129,29 +113,17 @@ __device__ __forceinline__ V3 random_unit_vector(uint32_t& s)
     return v3(r * ca, r * sa, z);
 }
 
-#ifndef PT_AXIS_ASM
-#define PT_AXIS_ASM 1     // per-quad LDS rows read one quad ahead by inline asm (see trace)
-#endif
-#ifndef PT_AXIS_EARLY
-#define PT_AXIS_EARLY 1   // select the quad's axis components before the early exit (see quad_test)
-#endif
-#ifndef PT_FLIP_FOLD
-#define PT_FLIP_FOLD 1    // facing test of an axis-aligned quad normal = one component's sign
-#endif
-
 // dot(n, D) > 0 (scalar.cpp:69) for the compile-time normal n.  For a signed unit axis n and finite
 // D this is exactly the sign test of that component: the products with n's zero components are
 // signed zeros, which neither change a non-zero sum nor make a zero sum positive.
 __device__ __forceinline__ bool facing(V3 n, V3 D)
 {
-#if PT_FLIP_FOLD
     if (n.x == 0.0f && n.z == 0.0f && n.y == 1.0f) return D.y > 0.0f;
     if (n.x == 0.0f && n.z == 0.0f && n.y == -1.0f) return D.y < 0.0f;
     if (n.y == 0.0f && n.z == 0.0f && n.x == 1.0f) return D.x > 0.0f;
     if (n.y == 0.0f && n.z == 0.0f && n.x == -1.0f) return D.x < 0.0f;
     if (n.x == 0.0f && n.y == 0.0f && n.z == 1.0f) return D.z > 0.0f;
     if (n.x == 0.0f && n.y == 0.0f && n.z == -1.0f) return D.z < 0.0f;
-#endif
     return dot(n, D) > 0.0f;
 }
 
@@ -161,25 +133,13 @@ struct AxisRow {
 };
 
 // TestQuadTrace, scalar.cpp:65-143.  `pq` = (rayPos + rayDir) - rayPos (ray-constant, hoisted),
-// `axis`/`dP`/`dD`/`yD` = the component :121-133 divides by, its ray origin, direction, RN(1/dir).
+// `axis`/`dP`/`dD`/`yD` = the component :121-133 divides by, its ray origin, direction, RN(1/dir),
+// `ax` = the quad's vertex components on that axis (its LDS row, read one quad ahead by quads_exact).
 // On a closer hit: best = dist, id = q, flag = flipped.
 template <class SC>
-__device__ __forceinline__ void quad_test(const AxisRow* s_axis, int q, V3 P, V3 D, V3 pq, int axis, float dP,
-                                          float dD, float yD, float& best, int& id, int& flag, AxisRow pre = {})
+__device__ __forceinline__ void quad_test(int q, V3 P, V3 D, V3 pq, float dP, float dD, float yD, float& best, int& id,
+                                          int& flag, AxisRow ax)
 {
-#if PT_AXIS_ASM
-    const AxisRow ax = pre;                                   // read one quad ahead (trace)
-    (void)s_axis;
-#elif PT_AXIS_FROM_LDS
-    const AxisRow ax = s_axis[q * 3 + axis];                  // LDS (the compiler places the read)
-#else
-    // the lane's axis component of each vertex, selected from the compile-time scene
-    auto comp = [&](int k) {
-        return axis == 0 ? SC::qv[q][k][0] : (axis == 1 ? SC::qv[q][k][1] : SC::qv[q][k][2]);
-    };
-    const AxisRow ax{comp(0), comp(1), comp(2), comp(3)};
-    (void)s_axis;
-#endif
     const V3 n = v3(SC::qn[q][0], SC::qn[q][1], SC::qn[q][2]);
     const bool flip = facing(n, D);                           // :69-80 (flipped order d,c,b,a)
     const V3 PA = sub(v3(SC::qv[q][0][0], SC::qv[q][0][1], SC::qv[q][0][2]), P);
@@ -196,20 +156,12 @@ __device__ __forceinline__ void quad_test(const AxisRow* s_axis, int q, V3 P, V3
     // :98 w = ScalarTriple(pq, pb, pa)  |  :111 w = ScalarTriple(pq, pa, pd)
     float w = dot(cross(pq, sel(t1, pb, pa)), sel(t1, pa, pd));
     v = t1 ? v : -v;                                          // :113
-    // :104 / :118 intersectPos = u*a + v*e + w*c (e = b or d), component `axis` only.
-#if PT_AXIS_EARLY
-    // selected for every lane BEFORE the divergent exit: the LDS row is then read at the top of
-    // the test and its latency hidden by the arithmetic above (inside the branch it is exposed)
+    // :104 / :118 intersectPos = u*a + v*e + w*c (e = b or d), component `axis` only; selected for
+    // every lane BEFORE the divergent exit (inside the branch the LDS row's latency is exposed)
     const float ak = flip ? ax.d : ax.a;
     const float ck = flip ? ax.b : ax.c;
     const float ek = t1 ? (flip ? ax.c : ax.b) : (flip ? ax.a : ax.d);
     if (u < 0.0f || w < 0.0f) return;                         // :97,99,110,112
-#else
-    if (u < 0.0f || w < 0.0f) return;                         // :97,99,110,112
-    const float ak = flip ? ax.d : ax.a;
-    const float ck = flip ? ax.b : ax.c;
-    const float ek = t1 ? (flip ? ax.c : ax.b) : (flip ? ax.a : ax.d);
-#endif
     // :100-103 / :114-117
     const float denom = rcp_x((u + v) + w);
     u *= denom;
@@ -251,29 +203,6 @@ __device__ __forceinline__ void sphere_test(int s, V3 P, V3 D, float& best, int&
     }
 }
 
-// TestSphereTrace (scalar.cpp:145-184) up to its distance, straight-line: hit = the reference
-// reaches the distance test (:157, :164), dist/inside as it computes them.  The acceptance
-// (0.01 < dist < best, :176) is applied by the caller.
-struct SphereHit {
-    float dist;
-    bool hit, inside;
-};
-template <class SC>
-__device__ __forceinline__ SphereHit sphere_dist(int s, V3 P, V3 D)
-{
-    const V3 m = sub(P, v3(SC::sph[s][0], SC::sph[s][1], SC::sph[s][2]));
-    const float b = dot(m, D);
-    const float c = dot(m, m) - SC::sph_r2[s];
-    const float discr = b * b - c;
-    SphereHit r;
-    r.hit = !(c > 0.0f && b > 0.0f) && !(discr < 0.0f);
-    const float sq = sqrt_x(r.hit ? discr : 1.0f);
-    const float d1 = -b - sq;                                 // :169
-    r.inside = d1 < 0.0f;                                     // :170-174
-    r.dist = r.inside ? -b + sq : d1;
-    return r;
-}
-
 // The three TestSphereTrace calls (scalar.cpp:274-285) with one root.  The spheres are pairwise
 // disjoint balls (static_assert: 3 apart), so along a ray the chords of two balls it meets are
 // disjoint, at least that far apart, and ordered like the centres' projections -b (see pt_v4.hip's
@@ -295,9 +224,6 @@ constexpr bool scene_spheres_disjoint()
     return true;
 }
 static_assert(scene_spheres_disjoint(), "the closest-sphere stage needs pairwise disjoint spheres");
-#ifndef PT_SPHERE_CLOSEST
-#define PT_SPHERE_CLOSEST 1
-#endif
 #ifndef PT_SPHERE_FORCE_SEQ
 #define PT_SPHERE_FORCE_SEQ 0   // test builds: every candidate ray takes the sequential fallback
 #endif
@@ -402,10 +328,6 @@ __device__ __forceinline__ bool sky_ray(V3 D)
 {
     return __builtin_fabsf(D.x) > kSkySlope * D.z || __builtin_fabsf(D.y) > kSkySlope * D.z;
 }
-#ifndef PT_SKY_SKIP
-#define PT_SKY_SKIP 1
-#endif
-constexpr bool SKY_SKIP = PT_SKY_SKIP != 0;
 static_assert(DemofoxScene::qv[0][0][2] == 35.0f && DemofoxScene::qv[3][0][0] == -12.5f && DemofoxScene::qv[4][0][0] == 12.5f &&
                   DemofoxScene::qv[1][0][1] == -12.45f && DemofoxScene::qv[2][0][1] == 12.5f && DemofoxScene::qv[5][0][1] == 12.4f &&
                   DemofoxScene::sph[0][0] == -9.0f && DemofoxScene::sph[2][0] == 9.0f && DemofoxScene::sph[0][3] == 3.0f,
@@ -434,7 +356,6 @@ template <class SC>
 __device__ __forceinline__ void quads_exact(const AxisRow* s_axis, V3 P, V3 D, V3 pq, int axis, float dP, float dD,
                                             float yD, Hit& h)
 {
-#if PT_AXIS_ASM
     // software pipeline of the per-quad LDS rows: row q+1 is read while quad q is tested, so the
     // LDS latency hides under a quad test instead of stalling inside its divergent tail
     typedef __attribute__((address_space(3))) const AxisRow lds_row_t;
@@ -448,23 +369,19 @@ __device__ __forceinline__ void quads_exact(const AxisRow* s_axis, V3 P, V3 D, V
         const AxisRow cur{row.x, row.y, row.z, row.w};
         if (q + 1 < PT_NQUADS)
             asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(row) : "v"(base), "i"((q + 1) * 3 * (int)sizeof(AxisRow)));
-        quad_test<SC>(s_axis, q, P, D, pq, axis, dP, dD, yD, h.best, h.id, h.flag, cur);
+        quad_test<SC>(q, P, D, pq, dP, dD, yD, h.best, h.id, h.flag, cur);
     }
-#else
-#pragma unroll PT_TRACE_UNROLL
-    for (int q = 0; q < PT_NQUADS; ++q) quad_test<SC>(s_axis, q, P, D, pq, axis, dP, dD, yD, h.best, h.id, h.flag);
-#endif
 }
 
 // Per (quad, flip): the vertices in the reference's order after its facing flip (a, b, c, d or
 // d, c, b, a), 12 floats in 3 float4 -- the exact test of the culling's chosen quad reads them.
 constexpr int kQuadVecs = PT_NQUADS * 2 * 3;
 
-// TestSceneTrace (scalar.cpp:186-287).  CAMERA: P is the camera origin (0, 0, 0).  CULL: the
-// culled quad stage (else the six exact tests).  QV: the culled quad's vertices come from the
-// flip-ordered table s_qv (else from its three per-axis rows of s_axis, flipped by selects -- the
-// env kernel, whose LDS has no room for the 576-B table at 4 blocks per CU).
-template <class SC, bool CAMERA, bool CULL, bool QV = true, bool SPH_CLOSEST = true>
+// TestSceneTrace (scalar.cpp:186-287).  CAMERA: P is the camera origin (0, 0, 0).  QV: the culled
+// quad's vertices come from the flip-ordered table s_qv (else from its three per-axis rows of
+// s_axis, flipped by selects -- the env kernel, whose LDS has no room for the 576-B table at 4
+// blocks per CU).  SPH_CLOSEST: the closest-sphere stage (else the three sequential tests).
+template <class SC, bool CAMERA, bool QV = true, bool SPH_CLOSEST = true>
 __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, V3 P, V3 D)
 {
     const V3 pq = sub(add(P, D), P);
@@ -474,84 +391,58 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, 
     const float dD = axis == 0 ? D.x : (axis == 1 ? D.y : D.z);
     const float yD = rcp_x(dD);
     Hit h{PT_SUPER_FAR, -1, 0, 0};
-    if (CULL) {
-        // classify the six quads cheaply, test the one candidate W exactly (pt_quadcull.h); a ray
-        // whose result is not certified runs the six exact tests (wave-uniform branch, rare).
-        // Straight-line order: W's vertex record is read from LDS, the spheres' distances are
-        // computed while the read is in flight, then W's exact test, then the spheres' updates in
-        // the reference's order (a sphere's distance does not depend on the running best).
-        const ptqc::F3 Pf{P.x, P.y, P.z}, pqf{pq.x, pq.y, pq.z};
-        const ptqc::Cull cl = ptqc::cull<CAMERA>(Pf, pqf, dP, yD);
-        const int W = cl.W < 0 ? 0 : cl.W;
-        const uint32_t jW = (ptqc::kAxisBits >> (2u * (uint32_t)W)) & 3u;
-        const float DjW = jW == 0 ? D.x : (jW == 1 ? D.y : D.z);
-        const bool fl = DjW > 0.0f;                                          // :69 (unit normal +e_j)
-        float4 r0, r1, r2;
-        AxisRow ar;
-        if (QV) {
-            const float4* rec = s_qv + (W * 2 + (fl ? 1 : 0)) * 3;
-            r0 = rec[0], r1 = rec[1], r2 = rec[2];
-            ar = s_axis[W * 3 + axis];
-        } else {
-            // rows x, y, z of quad W: (a_k, b_k, c_k, d_k); flipped order d, c, b, a
-            const AxisRow rx = s_axis[W * 3 + 0], ry = s_axis[W * 3 + 1], rz = s_axis[W * 3 + 2];
-            ar = axis == 0 ? rx : (axis == 1 ? ry : rz);
-            const V3 va = v3(fl ? rx.d : rx.a, fl ? ry.d : ry.a, fl ? rz.d : rz.a);
-            const V3 vb = v3(fl ? rx.c : rx.b, fl ? ry.c : ry.b, fl ? rz.c : rz.b);
-            const V3 vc = v3(fl ? rx.b : rx.c, fl ? ry.b : ry.c, fl ? rz.b : rz.c);
-            const V3 vd = v3(fl ? rx.a : rx.d, fl ? ry.a : ry.d, fl ? rz.a : rz.d);
-            r0 = make_float4(va.x, va.y, va.z, vb.x);
-            r1 = make_float4(vb.y, vb.z, vc.x, vc.y);
-            r2 = make_float4(vc.z, vd.x, vd.y, vd.z);
+    // classify the six quads cheaply, test the one candidate W exactly (pt_quadcull.h); a ray whose
+    // result is not certified runs the six exact tests (wave-uniform branch, rare).  Then the
+    // spheres' updates in the reference's order (a sphere's distance does not depend on the
+    // running best).
+    const ptqc::F3 Pf{P.x, P.y, P.z}, pqf{pq.x, pq.y, pq.z};
+    const ptqc::Cull cl = ptqc::cull<CAMERA>(Pf, pqf, dP, yD);
+    const int W = cl.W < 0 ? 0 : cl.W;
+    const uint32_t jW = (ptqc::kAxisBits >> (2u * (uint32_t)W)) & 3u;
+    const float DjW = jW == 0 ? D.x : (jW == 1 ? D.y : D.z);
+    const bool fl = DjW > 0.0f;                                          // :69 (unit normal +e_j)
+    float4 r0, r1, r2;
+    AxisRow ar;
+    if (QV) {
+        const float4* rec = s_qv + (W * 2 + (fl ? 1 : 0)) * 3;
+        r0 = rec[0], r1 = rec[1], r2 = rec[2];
+        ar = s_axis[W * 3 + axis];
+    } else {
+        // rows x, y, z of quad W: (a_k, b_k, c_k, d_k); flipped order d, c, b, a
+        const AxisRow rx = s_axis[W * 3 + 0], ry = s_axis[W * 3 + 1], rz = s_axis[W * 3 + 2];
+        ar = axis == 0 ? rx : (axis == 1 ? ry : rz);
+        const V3 va = v3(fl ? rx.d : rx.a, fl ? ry.d : ry.a, fl ? rz.d : rz.a);
+        const V3 vb = v3(fl ? rx.c : rx.b, fl ? ry.c : ry.b, fl ? rz.c : rz.b);
+        const V3 vc = v3(fl ? rx.b : rx.c, fl ? ry.b : ry.c, fl ? rz.b : rz.c);
+        const V3 vd = v3(fl ? rx.a : rx.d, fl ? ry.a : ry.d, fl ? rz.a : rz.d);
+        r0 = make_float4(va.x, va.y, va.z, vb.x);
+        r1 = make_float4(vb.y, vb.z, vc.x, vc.y);
+        r2 = make_float4(vc.z, vd.x, vd.y, vd.z);
+    }
+    const float ak = fl ? ar.d : ar.a, bk = fl ? ar.c : ar.b, ck = fl ? ar.b : ar.c, dk = fl ? ar.a : ar.d;
+    float dist;
+    const int code = ptqc::quad_exact(Pf, pqf, ptqc::F3{r0.x, r0.y, r0.z}, ptqc::F3{r0.w, r1.x, r1.y},
+                                      ptqc::F3{r1.z, r1.w, r2.x}, ptqc::F3{r2.y, r2.z, r2.w}, ak, bk, ck, dk, dP, dD,
+                                      yD, PT_SUPER_FAR, dist);
+    const bool ok = code == ptqc::kAccepted && cl.lb2 > dist;
+    bool unc = cl.unc || (cl.W >= 0 && !ok);
+    if (cl.W >= 0 && ok) {
+        h.best = dist;
+        h.id = W;
+        h.flag = fl ? 1 : 0;
+    }
+    if (__any(unc)) {
+        if (unc) {
+            h = Hit{PT_SUPER_FAR, -1, 0, 1};
+            quads_exact<SC>(s_axis, P, D, pq, axis, dP, dD, yD, h);
         }
-#if PT_CULL_SPHERES_FIRST
-        SphereHit sh[PT_NSPHERES];
-#pragma unroll
-        for (int k = 0; k < PT_NSPHERES; ++k) sh[k] = sphere_dist<SC>(k, P, D);
-#endif
-        const float ak = fl ? ar.d : ar.a, bk = fl ? ar.c : ar.b, ck = fl ? ar.b : ar.c, dk = fl ? ar.a : ar.d;
-        float dist;
-        const int code = ptqc::quad_exact(Pf, pqf, ptqc::F3{r0.x, r0.y, r0.z}, ptqc::F3{r0.w, r1.x, r1.y},
-                                          ptqc::F3{r1.z, r1.w, r2.x}, ptqc::F3{r2.y, r2.z, r2.w}, ak, bk, ck, dk, dP, dD,
-                                          yD, PT_SUPER_FAR, dist);
-        const bool ok = code == ptqc::kAccepted && cl.lb2 > dist;
-        bool unc = cl.unc || (cl.W >= 0 && !ok);
-        if (cl.W >= 0 && ok) {
-            h.best = dist;
-            h.id = W;
-            h.flag = fl ? 1 : 0;
-        }
-        if (__any(unc)) {
-            if (unc) {
-                h = Hit{PT_SUPER_FAR, -1, 0, 1};
-                quads_exact<SC>(s_axis, P, D, pq, axis, dP, dD, yD, h);
-            }
-        }
-#if PT_CULL_SPHERES_FIRST
-#pragma unroll
-        for (int k = 0; k < PT_NSPHERES; ++k)                               // :176-181
-            if (sh[k].hit && sh[k].dist > PT_MIN_HIT && sh[k].dist < h.best) {
-                h.best = sh[k].dist;
-                h.id = PT_NQUADS + k;
-                h.flag = sh[k].inside ? 1 : 0;
-            }
-#elif PT_SPHERE_CLOSEST
-        if (SPH_CLOSEST) {
-            spheres_closest<SC>(P, D, h.best, h.id, h.flag);
-        } else {
-#pragma unroll
-            for (int k = 0; k < PT_NSPHERES; ++k) sphere_test<SC>(k, P, D, h.best, h.id, h.flag);
-        }
-#else
+    }
+    if (SPH_CLOSEST) {
+        spheres_closest<SC>(P, D, h.best, h.id, h.flag);
+    } else {
 #pragma unroll
         for (int k = 0; k < PT_NSPHERES; ++k) sphere_test<SC>(k, P, D, h.best, h.id, h.flag);
-#endif
-        return h;
     }
-    (void)s_qv;
-    quads_exact<SC>(s_axis, P, D, pq, axis, dP, dD, yD, h);
-#pragma unroll PT_TRACE_UNROLL
-    for (int k = 0; k < PT_NSPHERES; ++k) sphere_test<SC>(k, P, D, h.best, h.id, h.flag);
     return h;
 }
 
@@ -596,18 +487,6 @@ __device__ __forceinline__ V3 miss_radiance(const PtJob& job, V3 amb, V3 d)
     return amb;
 }
 
-#ifndef PT_PRIO
-#define PT_PRIO 0          // s_setprio by the tile's previous cost (PT_PRIO_T1..T3 thresholds)
-#endif
-#ifndef PT_PRIO_T1
-#define PT_PRIO_T1 24
-#endif
-#ifndef PT_PRIO_T2
-#define PT_PRIO_T2 36
-#endif
-#ifndef PT_PRIO_T3
-#define PT_PRIO_T3 46
-#endif
 #ifndef PT_DIAG_NOATOMIC
 #define PT_DIAG_NOATOMIC 0
 #endif
@@ -627,16 +506,7 @@ __device__ __forceinline__ V3 miss_radiance(const PtJob& job, V3 amb, V3 d)
 #endif
 
 constexpr int kMaxWeights = 64;    // LDS table of the lerp weights 1/(iFrame+1) of a launch
-#ifndef PT_CHUNK
-#define PT_CHUNK 8
-#endif
-#ifndef PT_OWN_LAST
-#define PT_OWN_LAST 1
-#endif
-#ifndef PT_PIXEL_MAJOR   // pool items in pixel-major order: a pixel's frames are taken by
-#define PT_PIXEL_MAJOR 1    // neighbouring lanes (same ray origin); 1-1.3 % faster than frame-major
-#endif
-constexpr int kChunk = PT_CHUNK;   // frames per phase-B/C chunk (LDS colour slots per pixel)
+constexpr int kChunk = 8;   // frames per phase-B/C chunk (LDS colour slots per pixel)
 static_assert(kChunk >= 1 && kChunk < 32, "the pool's k / npf multiply is exact for npf < 32");
 
 // Waves (8x8 tiles in flight) per workgroup.  LDS is allocated per workgroup in 1280-B granules
@@ -644,11 +514,8 @@ static_assert(kChunk >= 1 && kChunk < 32, "the pool's k / npf multiply is exact 
 // model it and over-reports 5 blocks for 32001..32768 B): the ambient kernel's 4-wave workgroup
 // fits 5 per CU only with its LDS at <= 32 000 B (OWN_LAST below).  5-wave workgroups were placed
 // only 3 per CU (15 waves), 10-wave ones 1 per CU: slower.
-#ifndef PT_AMBIENT_BLOCK_WAVES
-#define PT_AMBIENT_BLOCK_WAVES 4
-#endif
 template <bool ENV>
-constexpr int waves_per_block() { return ENV ? 4 : PT_AMBIENT_BLOCK_WAVES; }
+constexpr int waves_per_block() { return 4; }
 
 // Env variant: a phase-B miss adds EquirectangularTextureSample(dir) to the sample's radiance
 // (simt_textured.cpp:408), two glibc inverse-trig calls and a texel gather.  Evaluated where the
@@ -658,10 +525,6 @@ constexpr int waves_per_block() { return ENV ? 4 : PT_AMBIENT_BLOCK_WAVES; }
 // so the sum is the reference's bit for bit).  The queue is drained before phase C.  Measured at
 // 1920x1080 x 8 spp, 8 bounces: 0.625 -> 0.541 ms per launch (LDS 32.7 -> 40.9 KiB per block,
 // still 4 blocks per CU, the VGPR-bound occupancy of this kernel).
-#ifndef PT_ENV_DEFER
-#define PT_ENV_DEFER 1
-#endif
-constexpr bool kEnvDefer = PT_ENV_DEFER != 0;
 
 // One 8x8 tile of pixels per wave at a time, in three phases:
 //   A  every lane traces its pixel's camera ray (coherent, once per pixel: the camera ray, its
@@ -684,8 +547,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     __shared__ AxisRow s_axis[PT_NQUADS * 3];
     // the culled quad stage (pt_quadcull.h); the env kernel's 40 912 B of LDS leave no room for the
     // 576-B flip-ordered vertex table at 4 blocks per CU, so it reads the per-axis rows (QV false)
-    constexpr bool CULL = PT_QUAD_CULL && (!ENV || PT_ENV_CULL);
-    constexpr bool QV = CULL && !ENV;
+    constexpr bool QV = !ENV;
     __shared__ float4 s_qv[QV ? kQuadVecs : 1];
     __shared__ float s_w[kMaxWeights];
     constexpr int CH = kChunk;
@@ -693,7 +555,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     // that lane's registers, and the LDS holds CH - 1 frames per pixel -- 3 KiB less per block,
     // which brings the ambient kernel to 29 648 B = 24 LDS granules and 5 blocks per CU (5 waves
     // per SIMD, what its 96 VGPRs allow).  The env kernel (4 waves per SIMD by VGPRs) keeps CH.
-    constexpr bool OWN_LAST = !ENV && PT_OWN_LAST != 0 && CH > 1;
+    constexpr bool OWN_LAST = !ENV && CH > 1;
     constexpr int CHS = OWN_LAST ? CH - 1 : CH;   // LDS colour slots per pixel
     __shared__ float s_col[kWavesPerBlock][64 * CHS * 3];   // phase-B radiance per (pixel, frame)
     // per item pixel: P1.xyz + (id | lane << 8) and n1 (planar), 28 B
@@ -701,7 +563,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     __shared__ float s_nrm[kWavesPerBlock][3][64];
     // env variant: the misses of phase B queue their direction (+ colour slot) here, and the queue
     // is drained 64 at a time by the whole wave (see kEnvDefer); 8 KiB, 40 KiB per block in all
-    constexpr bool DEFER = ENV && kEnvDefer;
+    constexpr bool DEFER = ENV;
     __shared__ float4 s_envq[DEFER ? kWavesPerBlock : 1][DEFER ? 128 : 1];
     {
         const int t = threadIdx.x;
@@ -776,18 +638,6 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     tile = __builtin_amdgcn_readfirstlane(tile);
     while (tile != kNone) {
         const int tyi = (int)(tile / (uint32_t)tiles_x), txi = (int)(tile % (uint32_t)tiles_x);
-#if PT_PRIO
-        // issue priority by the tile's cost in the previous launch (the schedule's input): the
-        // longest tiles are the launch's critical path, and on their SIMD they take the issue
-        // slots first while the cheaper tiles' waves fill the gaps
-        if (job.order) {
-            const uint32_t c = job.cost[tile];
-            if (c >= (uint32_t)PT_PRIO_T3) __builtin_amdgcn_s_setprio(3);
-            else if (c >= (uint32_t)PT_PRIO_T2) __builtin_amdgcn_s_setprio(2);
-            else if (c >= (uint32_t)PT_PRIO_T1) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-#endif
         DIAG_MARK(t_tile);
 #if PT_DIAG && !PT_DIAG_WAVES_ONLY
         const unsigned long long r_tile0 = __builtin_amdgcn_s_memrealtime();
@@ -811,12 +661,12 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         // A tile whose camera rays all leave the box's silhouette skips their TestSceneTrace: the
         // result is the reference's miss (sky_ray below), and the trace is the whole cost of such
         // a tile's phase A -- about half of all 1080p tiles are sky.
-        const bool all_sky = SKY_SKIP && __ballot(valid && !sky_ray(D0)) == 0;
+        const bool all_sky = __ballot(valid && !sky_ray(D0)) == 0;
         if (valid) {
             const float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
             acc = v3(px[0], px[cs], px[2 * cs]);
             const Hit h = all_sky ? Hit{PT_SUPER_FAR, -1, 0, 0}
-                                  : trace<DemofoxScene, true, CULL, QV, !ENV>(s_axis, s_qv, zero, D0);   // :335 rayPos = origin
+                                  : trace<DemofoxScene, true, QV, !ENV>(s_axis, s_qv, zero, D0);   // :335 rayPos = origin
             if (COUNT) ++n_seg, ++n_prim, n_fb += (unsigned long long)h.fb, n_sky += all_sky ? 1ull : 0ull;
             if (h.best == PT_SUPER_FAR) {                                 // :305-310
                 kind = 0;
@@ -898,20 +748,14 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                     const int k = next_item + rank;
                     const bool take = !has_item && k < nitems;
-#if PT_PIXEL_MAJOR   // consecutive items = the frames of one pixel (shared ray origin)
-                    // k / npf as (k * ceil(2^16 / npf)) >> 16: exact for k < 64 npf, npf < 32 (the
-                    // error k (M - 2^16 / npf) / 2^16 < npf / 1024 stays below the 1/npf gap)
+                    // pixel-major: consecutive items are the frames of one pixel (shared ray
+                    // origin; 1-1.3 % faster than frame-major).  k / npf as (k * ceil(2^16 / npf)) >>
+                    // 16: exact for k < 64 npf, npf < 32 (the error k (M - 2^16 / npf) / 2^16 <
+                    // npf / 1024 stays below the 1/npf gap)
                     const int slot_pm = take ? (int)(__umul24((uint32_t)k, div_m) >> 16) : 0;   // k * div_m < 2^25
                     const int fi = take ? k - (int)__umul24((uint32_t)slot_pm, (uint32_t)npf) : 0;
-#else
-                    const int fi = take ? k / nh : 0;
-#endif
                     if (take) {
-#if PT_PIXEL_MAJOR
-                        const int slot = slot_pm;
-#else
-                        const int slot = k - fi * nh;                 // the item's pixel record
-#endif
+                        const int slot = slot_pm;                     // the item's pixel record
                         const float4 a0 = s_rec[wv][slot];
                         const int packed = __builtin_bit_cast(int, a0.w);
                         const int sId = packed & 0xff;
@@ -947,7 +791,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                     }
                     DIAG_ADD(2, t_dir);
                     DIAG_MARK(t_tr);
-                    const Hit h = trace<DemofoxScene, false, CULL, QV, !ENV>(s_axis, s_qv, P, D);
+                    const Hit h = trace<DemofoxScene, false, QV, !ENV>(s_axis, s_qv, P, D);
                     DIAG_ADD(3, t_tr);
                     DIAG_MARK(t_sh);
                     if (COUNT) ++n_seg, n_fb += (unsigned long long)h.fb;
@@ -1134,9 +978,6 @@ constexpr int kCostBins = 1024;
 // waves idle while ~1500 ran 60-us units (per-tile timeline, scripts/diag_timeline.py).  Units
 // of ~tiles / (1.5 x waves) iterations, clamped to [2, 12]: 1080p 4 (c2 360 -> 353 us), 4K 12
 // (its 4x more cheap tiles keep every wave busy; 4 measured 1-2 % slower there).
-#ifndef PT_UNIT_COST
-#define PT_UNIT_COST 0   // 0: adaptive (above); else a fixed unit cost
-#endif
 constexpr uint32_t kUnitCostMax = 12, kUnitCostMin = 2;
 static_assert(kCostBins == 1024, "the schedule kernel scans one histogram bin per thread");
 
@@ -1241,8 +1082,8 @@ hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* u
 {
     if (ntiles == 0) return hipSuccess;
     if (!cost || !order || !units || !nunits) return hipErrorInvalidValue;
-    uint32_t unit_cost = PT_UNIT_COST;
-    if (unit_cost == 0) {   // adaptive: ~tiles / (1.5 x resident waves), 20 waves per CU
+    uint32_t unit_cost;
+    {   // adaptive: ~tiles / (1.5 x resident waves), 20 waves per CU
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)

@@ -13,6 +13,8 @@ struct PtToneJob {
     int32_t tile_w, tile_h;   // PT_LAYOUT_TILED_PLANAR8
     uint32_t* out;            // device, width * height packed pixels, row 0 = top
     int32_t format;           // PT_PIXEL_*
+    int32_t fast_aces;        // USE_FAST_APPROXIMATE_ACES_TONEMAP (else the unfused fit with '/')
+    int32_t fast_gamma;       // USE_FAST_APPROXIMATE_GAMMA (else 1.055 powf(x, 1/2.4) - 0.055)
 };
 
 hipError_t pt_launch_tonemap(const PtToneJob& job, hipStream_t stream);

@@ -1,7 +1,7 @@
 // pt_output.hip -- the output stage: linear HDR accumulator -> 8-bit display / file pixels.
 //
-// Reference (CPUPerformanceRayTracer/demofox_path_tracing_optimization_v4.cpp; the defaults of
-// global_preprocessor_flags.h:62-63, USE_FAST_APPROXIMATE_GAMMA = USE_FAST_APPROXIMATE_ACES_TONEMAP = 1):
+// Reference (CPUPerformanceRayTracer/demofox_path_tracing_optimization_v4.cpp; both branches of
+// global_preprocessor_flags.h:62-63, USE_FAST_APPROXIMATE_GAMMA / USE_FAST_APPROXIMATE_ACES_TONEMAP):
 //   OutputToScreen :1260-1295 / OutputToFile :1297-1331, called per tile by CopyOutputToFile
 //   :1729-1760 and the frame loop: ACESFilm :165-175 -> LinearToSRGB :177-186 (fast_pow_gamma
 //   :144-155) -> saturate * 255 -> cvtps_epi32 -> packed u32.
@@ -13,6 +13,7 @@
 // rounded 1/x (as in the oracle, oracle/pt_oracle_output.c): at most 1 LSB from any x86 run.
 #include "pt_output.h"
 #include "pt_exactmath.h"
+#include "pt_libmf.h"
 #include <algorithm>
 
 namespace {
@@ -35,27 +36,40 @@ __device__ __forceinline__ float fast_pow_gamma(float x)   // :144-155
     return sqrt_(sqrtx * nit3);
 }
 
-__device__ __forceinline__ float aces(float X)   // :165-175 (fast fit)
+template <bool FAST>
+__device__ __forceinline__ float aces(float X)   // ACESFilm :165-175
 {
     const float a = 2.51f, b = 0.03f, c = 2.43f, d = 0.59f, e = 0.14f;
-    const float rcp_denom = rcp(__builtin_fmaf(X, __builtin_fmaf(c, X, d), e));
-    return saturate((X * __builtin_fmaf(a, X, b)) * rcp_denom);
+    if (FAST) {   // USE_FAST_APPROXIMATE_ACES_TONEMAP 1 (:168-171): rcp of the fused denominator
+        const float rcp_denom = rcp(__builtin_fmaf(X, __builtin_fmaf(c, X, d), e));
+        return saturate((X * __builtin_fmaf(a, X, b)) * rcp_denom);
+    }
+    // 0 (:172-174): f32 scalar * m256x3 operators, unfused (mul, add), then the IEEE division
+    const float num = X * (a * X + b);
+    const float den = X * (c * X + d) + e;
+    return saturate(pt::div_guarded(num, den));
 }
 
+template <bool FAST>
 __device__ __forceinline__ float linear_to_srgb(float x)   // :177-186
 {
     x = saturate(x);
-    return x < 0.0031308f ? x * 12.92f : __builtin_fmaf(1.055f, fast_pow_gamma(x), -0.055f);
+    if (x < 0.0031308f) return x * 12.92f;
+    if (FAST) return __builtin_fmaf(1.055f, fast_pow_gamma(x), -0.055f);   // :182-183 (fmsub)
+    // USE_FAST_APPROXIMATE_GAMMA 0 (:184-185): 1.055f * pow_ps(rgb, 1 / 2.4f) - 0.055f, SVML pow_ps ->
+    // glibc-exact powf (pt_libmf.h; x in [0.0031308, 1] is inside its main path)
+    return 1.055f * pt::lm::powf_glibc_main(x, 1.0f / 2.4f) - 0.055f;
 }
 
+template <bool FAST_ACES, bool FAST_GAMMA>
 __device__ __forceinline__ uint32_t channel(float linear)
 {
     const float c_exposure = 1.0f;
-    const float v = saturate(linear_to_srgb(aces(linear * c_exposure))) * 255.f;
+    const float v = saturate(linear_to_srgb<FAST_GAMMA>(aces<FAST_ACES>(linear * c_exposure))) * 255.f;
     return (uint32_t)(int32_t)__builtin_rintf(v) & 0xFFu;   // cvtps_epi32 (nearest even) & ByteMask
 }
 
-template <int LAYOUT>
+template <int LAYOUT, bool FAST_ACES, bool FAST_GAMMA>
 __global__ __launch_bounds__(256) void pt_tonemap_kernel(PtToneJob j)
 {
     const uint32_t npix = (uint32_t)j.width * (uint32_t)j.height;
@@ -74,10 +88,21 @@ __global__ __launch_bounds__(256) void pt_tonemap_kernel(PtToneJob j)
             base = (size_t)ty * j.tile_h * j.width * 3u + (size_t)tx * j.tile_w * j.tile_h * 3u +
                    ((size_t)ly * j.tile_w + (lx & ~7u)) * 3u + (lx & 7u);
         }
-        const uint32_t r = channel(j.accum[base]), g = channel(j.accum[base + cs]), b = channel(j.accum[base + 2 * cs]);
+        const uint32_t r = channel<FAST_ACES, FAST_GAMMA>(j.accum[base]), g = channel<FAST_ACES, FAST_GAMMA>(j.accum[base + cs]),
+                       b = channel<FAST_ACES, FAST_GAMMA>(j.accum[base + 2 * cs]);
         j.out[p] = j.format == PT_PIXEL_XRGB8 ? ((r << 16) | (g << 8) | b)        // OutputToScreen :1282-1285
                                               : (0xFF000000u | (b << 16) | (g << 8) | r);   // OutputToFile :1319-1323
     }
+}
+
+template <int LAYOUT>
+hipError_t launch_layout(const PtToneJob& j, unsigned blocks, hipStream_t st)
+{
+    if (j.fast_aces && j.fast_gamma) hipLaunchKernelGGL((pt_tonemap_kernel<LAYOUT, true, true>), dim3(blocks), dim3(256), 0, st, j);
+    else if (j.fast_aces) hipLaunchKernelGGL((pt_tonemap_kernel<LAYOUT, true, false>), dim3(blocks), dim3(256), 0, st, j);
+    else if (j.fast_gamma) hipLaunchKernelGGL((pt_tonemap_kernel<LAYOUT, false, true>), dim3(blocks), dim3(256), 0, st, j);
+    else hipLaunchKernelGGL((pt_tonemap_kernel<LAYOUT, false, false>), dim3(blocks), dim3(256), 0, st, j);
+    return hipGetLastError();
 }
 
 }  // namespace
@@ -89,17 +114,11 @@ hipError_t pt_launch_tonemap(const PtToneJob& j, hipStream_t st)
     const long npix = (long)j.width * j.height;
     const unsigned blocks = (unsigned)std::min<long>((npix + 255) / 256, 256L * 16);
     switch (j.layout) {
-        case PT_LAYOUT_INTERLEAVED:
-            hipLaunchKernelGGL(pt_tonemap_kernel<PT_LAYOUT_INTERLEAVED>, dim3(blocks), dim3(256), 0, st, j);
-            break;
-        case PT_LAYOUT_PLANAR8:
-            hipLaunchKernelGGL(pt_tonemap_kernel<PT_LAYOUT_PLANAR8>, dim3(blocks), dim3(256), 0, st, j);
-            break;
+        case PT_LAYOUT_INTERLEAVED: return launch_layout<PT_LAYOUT_INTERLEAVED>(j, blocks, st);
+        case PT_LAYOUT_PLANAR8: return launch_layout<PT_LAYOUT_PLANAR8>(j, blocks, st);
         case PT_LAYOUT_TILED_PLANAR8:
             if (j.tile_w <= 0 || j.tile_h <= 0) return hipErrorInvalidValue;
-            hipLaunchKernelGGL(pt_tonemap_kernel<PT_LAYOUT_TILED_PLANAR8>, dim3(blocks), dim3(256), 0, st, j);
-            break;
+            return launch_layout<PT_LAYOUT_TILED_PLANAR8>(j, blocks, st);
         default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }

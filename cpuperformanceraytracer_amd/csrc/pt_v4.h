@@ -49,6 +49,8 @@ struct PtV4Job {
     int32_t env_mode;           // PT_V4_ENV_*_
     int32_t random_jitter;      // USE_RANDOM_JITTER_TEXTURE_SAMPLING
     int32_t rejection;          // USE_UNIT_VECTOR_REJECTION_SAMPLING
+    int32_t accumulate;         // ACCUMULATE_FRAMES: fused lerp into the accumulator (else store)
+    int32_t fast_exp;           // USE_FAST_APPROXIMATE_EXP: approx_exp_ps (else glibc-exact expf)
     const float* env;           // device texture (H x W x 3), nullptr with PT_V4_ENV_NONE_
     int32_t env_w, env_h;
     unsigned long long* counters;   // COUNT launches: [0] segments, [1] samples, [2] escaped, [3] lane slots

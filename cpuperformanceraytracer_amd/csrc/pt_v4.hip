@@ -21,6 +21,7 @@
 #include "pt_kernel.h"
 #include "pt_exactmath.h"
 #include "pt_sincosf.h"
+#include "pt_libmf.h"
 // atan2f/asinf with the guarded fast '/' and sqrt (bit-identical to IEEE, pt_exactmath.h)
 #define PT_IT_HD __device__ __forceinline__
 #define PT_IT_DIV(a, b) pt::div_guarded((a), (b))
@@ -36,14 +37,8 @@ constexpr float kMinHit = 0.01f;      // c_minimumRayHitTime  v4 :10
 constexpr float kNudge = 0.01f;       // c_rayPosNormalNudge  v4 :14
 constexpr float kSuperFar = 10000.0f; // c_superFar           v4 :17
 constexpr float kPi = 3.14159265359f; // c_pi                 mathutils.h:5
-#ifndef PT_V4_BLOCK_WAVES
-#define PT_V4_BLOCK_WAVES 4
-#endif
-constexpr int kWaves = PT_V4_BLOCK_WAVES;   // waves (tiles) per workgroup
-#ifndef PT_V4_CHUNK
-#define PT_V4_CHUNK 8
-#endif
-constexpr int kChunk = PT_V4_CHUNK;   // frames per LDS chunk
+constexpr int kWaves = 4;    // waves (tiles) per workgroup
+constexpr int kChunk = 8;    // frames per LDS chunk
 // Env modes: a miss adds fma(env(dir), throughput, ret) (:787), two glibc inverse-trig calls (or a
 // cube-face pick) and texel gathers.  Evaluated where the miss happens it runs in most pool
 // iterations for a fraction of the lanes.  Deferred, the miss stores ret in its colour slot and
@@ -54,16 +49,7 @@ constexpr int kChunk = PT_V4_CHUNK;   // frames per LDS chunk
 // granules, so 5 blocks per CU stay resident (the VGPR-bound occupancy; at 56 entries the block
 // needed 26 granules and dropped to 4 per CU, and the queue then measured slower).  1920x1080 x
 // 8 spp, 8 bounces: equirect 0.615 -> 0.561 ms, cubemap 0.525 -> 0.510 ms.
-#ifndef PT_V4_ENV_DEFER
-#define PT_V4_ENV_DEFER 1
-#endif
-#ifndef PT_V4_PIXEL_MAJOR   // A/B: pixel-major item order (1-2.5 % slower here, unlike the
-#define PT_V4_PIXEL_MAJOR 0    // diffuse kernel, where a pixel's frames share their bounce-0 origin)
-#endif
-#ifndef PT_V4_ENV_Q
-#define PT_V4_ENV_Q 48
-#endif
-constexpr int kEnvQ = PT_V4_ENV_Q;
+constexpr int kEnvQ = 48;
 
 struct V3 {
     float x, y, z;
@@ -83,18 +69,14 @@ __device__ __forceinline__ float min_ps(float a, float b) { return a < b ? a : b
 __device__ __forceinline__ float saturate(float x) { return min_ps(max_ps(x, 0.0f), 1.0f); }
 // correctly rounded 1/x and sqrt: the fast sequences of pt_exactmath.h inside their verified
 // ranges, IEEE outside (bit-identical to '1.0f / x' and sqrtf for every input)
-#ifndef PT_V4_IEEE_DIV
-#define PT_V4_IEEE_DIV 0   // A/B / debug builds: the compiler's IEEE sequences
-#endif
 __device__ __forceinline__ float rcp(float x)   // rcp -> 1.f / x (mathlib.h:415)
 {
-    if (PT_V4_IEEE_DIV) return 1.0f / x;
     float r = pt::rcp_rn(x);
     const float ax = __builtin_fabsf(x);
     if (__builtin_expect(!(ax >= 0x1p-125f && ax <= 0x1p125f), 0)) r = 1.0f / x;
     return r;
 }
-__device__ __forceinline__ float sqrt_(float x) { return PT_V4_IEEE_DIV ? __builtin_sqrtf(x) : pt::sqrt_guarded(x); }
+__device__ __forceinline__ float sqrt_(float x) { return pt::sqrt_guarded(x); }
 __device__ __forceinline__ V3 normalize(V3 v) { return v * rcp(sqrt_(dot(v, v))); }  // mathlib.h:759
 
 __device__ __forceinline__ uint32_t wang(uint32_t& s)   // mathutils.h:8-16 (logical shifts)
@@ -419,10 +401,7 @@ constexpr bool default_spheres_disjoint()
     return true;
 }
 static_assert(default_spheres_disjoint(), "the closest-sphere trace needs pairwise disjoint spheres");
-#ifndef PT_V4_SPHERE_CLOSEST
-#define PT_V4_SPHERE_CLOSEST 1
-#endif
-// The candidate with the largest b without tracking it (PT_V4_SPHERE_ORDER).  InitializeScene's
+// The candidate with the largest b without tracking it (the sphere-order rule).  InitializeScene's
 // spheres lie on one line parallel to x, in ascending x, `spacing` apart, radius r, 2r < spacing
 // (asserted below).  Then b_i = (pos - c_i).dir = b_0 - i spacing dir.x exactly, so the largest b of
 // the candidates is the lowest candidate index when dir.x > 0 and the highest when dir.x < 0 --
@@ -433,9 +412,6 @@ static_assert(default_spheres_disjoint(), "the closest-sphere trace needs pairwi
 // one candidate.)  A NaN ray makes every b NaN: the reference's b > bmax never takes one, and the
 // recomputed b of the chosen index is NaN too, which drops it.  The kernel keeps the per-sphere
 // early tests (exactly) and replaces the per-sphere compare + three selects by a candidate bit mask.
-#ifndef PT_V4_SPHERE_ORDER
-#define PT_V4_SPHERE_ORDER 1
-#endif
 constexpr bool default_spheres_on_x_line()
 {
     namespace D = pt_v4_default;
@@ -447,11 +423,8 @@ constexpr bool default_spheres_on_x_line()
     }
     return D::kSpheres <= 32;
 }
-static_assert(!PT_V4_SPHERE_ORDER || default_spheres_on_x_line(),
-              "PT_V4_SPHERE_ORDER needs InitializeScene's spheres on one x line, >= 0.4 apart");
-#ifndef PT_V4_UNIFIED_DIR
-#define PT_V4_UNIFIED_DIR 1   // rejection sampling: one straight-line direction for all three outcomes
-#endif
+static_assert(default_spheres_on_x_line(),
+              "the sphere-order rule needs InitializeScene's spheres on one x line, >= 0.4 apart");
 #ifndef PT_V4_SPHERE_FORCE_SEQ
 #define PT_V4_SPHERE_FORCE_SEQ 0   // test builds: every candidate ray takes the sequential fallback
 #endif
@@ -471,9 +444,6 @@ __device__ __forceinline__ bool sky_ray_v4(V3 D)
     const bool band_hi = D.y > 0.34f * nz && D.y < 0.52f * nz && ax < 0.32f * nz;
     return nz > 0.0f && (D.y < -0.52f * nz || ax > 1.02f * nz || (D.y > -0.03f * nz && !band_hi));
 }
-#ifndef PT_V4_SKY_SKIP
-#define PT_V4_SKY_SKIP 1
-#endif
 static_assert(pt_v4_default::kQuads == 4 && pt_v4_default::kSpheres == 7, "sky_ray_v4 is derived for InitializeScene");
 
 // TestSceneTrace :700-718: quads in order, then spheres (object index = material index).
@@ -494,10 +464,9 @@ __device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir, const 
         for (int i = 0; i < D::kQuads; ++i)
             quad_test(pos, dir, h, i, v3(D::kQuad[i][0], D::kQuad[i][1], D::kQuad[i][2]),
                       v3(D::kQuad[i][3], D::kQuad[i][4], D::kQuad[i][5]), dk, i);
-        if (PT_V4_SPHERE_CLOSEST) {
+        {   // closest-sphere stage
             float bmax = -__builtin_huge_valf(), dsel = 0.0f;
             int ksel = -1;
-#if PT_V4_SPHERE_ORDER
             uint32_t cand = 0;   // spheres that pass the early test
 #pragma unroll
             for (int i = 0; i < D::kSpheres; ++i) {   // :645-657, the early test exactly
@@ -508,7 +477,7 @@ __device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir, const 
                 const bool early = discr < 0.0f || (cc > 0.0f && b > 0.0f);
                 cand |= early ? 0u : 1u << i;
             }
-            if (cand) {   // the largest b: by the sign of dir.x (see PT_V4_SPHERE_ORDER)
+            if (cand) {   // the largest b: by the sign of dir.x (the sphere-order rule above)
                 ksel = dir.x > 0.0f ? __builtin_ctz(cand) : 31 - __builtin_clz(cand);
                 const float4 c = s_sc[ksel];
                 const V3 m = pos - v3(c.x, c.y, c.z);
@@ -516,20 +485,6 @@ __device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir, const 
                 dsel = fma_(bmax, bmax, -fma_(-c.w, c.w, dot(m, m)));
                 if (!(bmax == bmax)) ksel = -1;
             }
-#else
-#pragma unroll
-            for (int i = 0; i < D::kSpheres; ++i) {   // :645-657, the early test exactly
-                const V3 m = pos - v3(D::kSphere[i][0], D::kSphere[i][1], D::kSphere[i][2]);
-                const float b = dot(m, dir);
-                const float cc = fma_(-D::kSphere[i][3], D::kSphere[i][3], dot(m, m));
-                const float discr = fma_(b, b, -cc);
-                const bool early = discr < 0.0f || (cc > 0.0f && b > 0.0f);
-                const bool take = !early && b > bmax;
-                bmax = take ? b : bmax;
-                dsel = take ? discr : dsel;
-                ksel = take ? i : ksel;
-            }
-#endif
             bool seq = false;
             if (ksel >= 0) {
                 const float4 c = s_sc[ksel];
@@ -559,11 +514,6 @@ __device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir, const 
                     }
                 }
             }
-        } else {
-#pragma unroll
-            for (int i = 0; i < D::kSpheres; ++i)
-                sphere_test(pos, dir, h, D::kQuads + i, v3(D::kSphere[i][0], D::kSphere[i][1], D::kSphere[i][2]),
-                            D::kSphere[i][3]);
         }
     } else {
         int obj = 0;
@@ -601,7 +551,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     __shared__ PtV4Mat s_mat[PT_V4_MAX_OBJECTS];
     __shared__ float4 s_sc[DEF ? pt_v4_default::kSpheres : 1];   // default scene: sphere centre, radius
     __shared__ MatX s_mx[PT_V4_MAX_OBJECTS];                        // per-material constants (mat_consts)
-    constexpr bool DEFER = ENV != PT_V4_ENV_NONE_ && PT_V4_ENV_DEFER != 0;
+    constexpr bool DEFER = ENV != PT_V4_ENV_NONE_;
     __shared__ float4 s_qd[DEFER ? kWaves : 1][DEFER ? kEnvQ : 1];   // env dir, rng
     __shared__ float4 s_qt[DEFER ? kWaves : 1][DEFER ? kEnvQ : 1];   // throughput, colour slot
     for (int t = threadIdx.x; t < PT_V4_MAX_OBJECTS * 17; t += 64 * kWaves)
@@ -648,7 +598,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
         // compact layouts index the buffer row; the tiled layout indexes the full image (global row)
         const int orow = LAYOUT == PT_LAYOUT_TILED_PLANAR8 ? job.row_start + pr * job.row_stride : pr;
         acc_p = job.buf + out_index<LAYOUT>(job, px, orow);
-        acc = v3(acc_p[0], acc_p[cs], acc_p[2 * cs]);
+        if (job.accumulate) acc = v3(acc_p[0], acc_p[cs], acc_p[2 * cs]);   // (:1233: only to blend)
     }
 
     for (int c0 = 0; c0 < job.nframes; c0 += kChunk) {
@@ -687,11 +637,9 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                 const int it = next + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
                 if (it < total) {
-#if PT_V4_PIXEL_MAJOR   // a pixel's frames go to neighbouring lanes (close jittered camera rays)
-                    const int p = it / nf, f = it - p * nf;
-#else
+                    // frame-major (pixel-major, a pixel's frames on neighbouring lanes, measured
+                    // 1-2.5 % slower here: the jittered camera rays share no bounce-0 origin)
                     const int p = it & 63, f = it >> 6;
-#endif
                     const int X = job.col0 + tcol + (p & 7), rb = trow + (p >> 3);
                     if ((tcol + (p & 7)) < job.ncols && rb < job.nrows) {
                         item = f * 64 + p;   // colour slot order (phase C)
@@ -725,7 +673,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
             // (the slope test runs only in iterations where every busy lane is at bounce 0: a wave-
             // uniform branch, instead of the test on every lane in every iteration)
             bool all_sky = false;
-            if (DEF && PT_V4_SKY_SKIP && __ballot(item >= 0 && bounce != 0) == 0)
+            if (DEF && __ballot(item >= 0 && bounce != 0) == 0)
                 all_sky = __ballot(item >= 0 && !sky_ray_v4(dir)) == 0;
             if (item >= 0) {
                 // one iteration of GetColorForRay's bounce loop (:733-909)
@@ -751,9 +699,15 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                         wang(rng);
                     }
                     const PtV4Mat& M = s_mat[h.mat];
-                    if (h.inside)   // :797
-                        T = mul(T, v3(approx_exp(-M.refr_color[0] * h.dist), approx_exp(-M.refr_color[1] * h.dist),
-                                      approx_exp(-M.refr_color[2] * h.dist)));
+                    if (h.inside) {   // :797, Beer's law
+                        if (job.fast_exp)   // USE_FAST_APPROXIMATE_EXP 1 (:783-784)
+                            T = mul(T, v3(approx_exp(-M.refr_color[0] * h.dist), approx_exp(-M.refr_color[1] * h.dist),
+                                          approx_exp(-M.refr_color[2] * h.dist)));
+                        else                // 0 (:785-787): exp_ps -> glibc-exact expf (pt_libmf.h)
+                            T = mul(T, v3(pt::lm::expf_glibc(-M.refr_color[0] * h.dist),
+                                          pt::lm::expf_glibc(-M.refr_color[1] * h.dist),
+                                          pt::lm::expf_glibc(-M.refr_color[2] * h.dist)));
+                    }
                     const V3 em = ld3(M.emissive);
                     if (bounce == B) {   // last iteration: only its emissive term is used
                         ret = v3(fma_(em.x, T.x, ret.x), fma_(em.y, T.y, ret.y), fma_(em.z, T.z, ret.z));
@@ -781,7 +735,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                         // directions and selects one; only the selected one (and the diffuse direction
                         // the specular one lerps towards) is evaluated here.  Both random unit vectors
                         // are still drawn, in the reference's order (diffuse first).
-                        const bool unified = PT_V4_UNIFIED_DIR && rejection;
+                        const bool unified = rejection;   // one straight-line direction for all three outcomes
                         uint32_t s_diff = rng, s_refr = rng;
                         uint32_t h0 = 0, h1 = 0, h2 = 0;   // unified: the chosen stream's three draws
                         if (unified) {
@@ -921,8 +875,12 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
         if (pvalid) {
             for (int f = 0; f < nf; ++f) {
                 const float* c = col + (f * 64 + lane) * 3;
-                const float bf = rcp((float)(job.frame_first + (uint32_t)(c0 + f)) + 1.0f);   // :1200
-                acc = v3(fma_(bf, c[0] - acc.x, acc.x), fma_(bf, c[1] - acc.y, acc.y), fma_(bf, c[2] - acc.z, acc.z));
+                if (job.accumulate) {   // ACCUMULATE_FRAMES 1: fmadd(blend_factor, color - last, last) :1233-1241
+                    const float bf = rcp((float)(job.frame_first + (uint32_t)(c0 + f)) + 1.0f);   // :1200
+                    acc = v3(fma_(bf, c[0] - acc.x, acc.x), fma_(bf, c[1] - acc.y, acc.y), fma_(bf, c[2] - acc.z, acc.z));
+                } else {                // ACCUMULATE_FRAMES 0: the frame's colour is stored (:1245-1250)
+                    acc = v3(c[0], c[1], c[2]);
+                }
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -965,10 +923,7 @@ hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool 
         const long blocks = std::min<long>(pt_resident_blocks(kern, 64 * kWaves), (tiles + kWaves - 1) / kWaves);
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), block, 0, st, j, sc);
     };
-#ifndef PT_V4_FORCE_GENERIC
-#define PT_V4_FORCE_GENERIC 0   // A/B builds: the scene-table path even for the default scene
-#endif
-    if (j.default_scene && !PT_V4_FORCE_GENERIC) {
+    if (j.default_scene) {
         if (count) go(pt_v4_kernel<ENV, LAYOUT, true, true>);
         else go(pt_v4_kernel<ENV, LAYOUT, false, true>);
     } else {

@@ -13,17 +13,18 @@ from . import _native as N
 def ensure_backend(device_index: int, num_bounces: int = 4) -> None:
     """Initialise libpt_mi355 on `device_index` (the torch device of this rank) if it is not
     initialised yet.  The library state (env map, schedules, pinned buffer, frame counters) is per
-    process and lives on one device: a job on another device raises PtError(PT_ESTATE) instead of
-    silently re-initialising (one process per GPU, as bench.py and shard.py run).  The caller's
-    current HIP device is restored after an initialisation."""
+    process; a device job runs on the logical device holding its buffer, and a job on a device the
+    library was not initialised with raises PtError(PT_ESTATE) instead of silently re-initialising
+    (renderer.init(devices=[...]) drives several GPUs from one process; bench.py and shard.py run one
+    process per GPU).  The caller's current HIP device is restored after an initialisation."""
     from . import renderer
-    cur = renderer.initialized_device()
-    if cur == device_index:
+    cur = renderer.initialized_devices()
+    if device_index in cur:
         return
-    if cur is not None:
+    if cur:
         raise N.PtError(N.PT_ESTATE, "ensure_backend",
-                        f"libpt_mi355 is initialised on device {cur}; a job on device {device_index} needs "
-                        "its own process (or renderer.shutdown() first)")
+                        f"libpt_mi355 is initialised on devices {cur}; a job on device {device_index} needs "
+                        "renderer.init(devices=[...]) naming it, or its own process")
     import torch
     prev = torch.cuda.current_device()
     try:

@@ -29,34 +29,35 @@ import numpy as np
 
 from . import _native as N
 
-_pin_host = False      # the library was initialised with PT_FLAG_PIN_HOST
-_pin_watch = {}        # (id(owner), ptr) -> weakref.finalize dropping the page-lock of ptr
+_watch_buffers = False  # the library keeps a host buffer associated (PT_FLAG_PIN_HOST / DEFER_READBACK)
+_buf_watch = {}        # (id(owner), ptr) -> weakref.finalize releasing ptr
 
 
-def _unpin_ptr(ptr: int) -> None:
+def _release_ptr(ptr: int) -> None:
     try:
-        N.load().pt_unpin_host(ctypes.c_void_p(ptr))
+        N.load().pt_release_buffer(ctypes.c_void_p(ptr))
     except Exception:   # interpreter shutdown
         pass
 
 
-def _watch_pinned(a: np.ndarray) -> None:
-    """PT_FLAG_PIN_HOST: the library page-locks the frame buffer and keeps it locked across calls.
-    When the array that owns the memory is released (a Resize reallocating the render target,
-    Application.cpp:142-151), drop that page-lock before numpy can hand the address out again."""
+def _watch(a: np.ndarray) -> None:
+    """PT_FLAG_PIN_HOST / PT_FLAG_DEFER_READBACK: the library keeps the frame buffer page-locked or
+    mirrored in HBM across calls.  When the array that owns the memory is released (a Resize
+    reallocating the render target, Application.cpp:142-151), drop that association
+    (pt_release_buffer: no write-back into freed memory) before numpy can hand the address out again."""
     owner = a
     while isinstance(owner.base, np.ndarray):
         owner = owner.base
     ptr = a.ctypes.data
     key = (id(owner), ptr)
-    f = _pin_watch.get(key)
+    f = _buf_watch.get(key)
     if f is not None and f.alive:
         return
-    for k in [k for k, v in _pin_watch.items() if not v.alive]:
-        del _pin_watch[k]
+    for k in [k for k, v in _buf_watch.items() if not v.alive]:
+        del _buf_watch[k]
     try:
-        _pin_watch[key] = weakref.finalize(owner, _unpin_ptr, ptr)
-    except TypeError:   # memory owned by an object without weakref support: unpinned at shutdown
+        _buf_watch[key] = weakref.finalize(owner, _release_ptr, ptr)
+    except TypeError:   # memory owned by an object without weakref support: released at shutdown
         pass
 
 
@@ -67,48 +68,72 @@ def _buf(a: np.ndarray, width: int, height: int, num_channels: int) -> int:
         raise N.PtError(N.PT_EINVAL, "buffer", "BufferOut must be writeable")
     if width > 0 and height > 0 and num_channels > 0 and a.size < width * height * num_channels:
         raise N.PtError(N.PT_EINVAL, "buffer", f"BufferOut holds {a.size} floats < {width}x{height}x{num_channels}")
-    if _pin_host:
-        _watch_pinned(a)
+    if _watch_buffers:
+        _watch(a)
     return a.ctypes.data
 
 
 def init(num_bounces: int = 4, samples_per_frame: int = 1, ambient=(0.1, 0.1, 0.1), device: int = 0,
-         defer_readback: bool = False, pin_host: bool = False) -> None:
+         defer_readback: bool = False, pin_host: bool = False, devices=None) -> None:
     """(Re)initialise the backend: the runtime form of the reference's compile-time settings
     (c_numBounces scalar.cpp:19, NUM_SAMPLES_PER_FRAME global_preprocessor_flags.h:30).
     Resets the frame counter to 0, like a fresh process of the reference.
-    pin_host: page-lock the frame buffer and overlap its transfers with rendering (row bands)."""
+    pin_host: page-lock the frame buffer and overlap its transfers with rendering (row bands).
+    devices: several HIP devices (ordinals may repeat: logical shards of one GPU) that every frame
+    call deals its rows to (row Y -> devices[Y % len]); None: `device` alone (or PT_MI355_DEVICES)."""
     L = N.load()
     c = N.PtConfig()
     L.pt_default_config(ctypes.byref(c))
-    c.device = device
+    if devices is None and c.device_count <= 1:
+        c.device = device
+    if devices is not None:
+        devices = list(devices)
+        if not 1 <= len(devices) <= N.PT_MAX_DEVICES:
+            raise N.PtError(N.PT_EINVAL, "init", f"1..{N.PT_MAX_DEVICES} devices expected")
+        c.device = devices[0]
+        c.device_count = len(devices)
+        for i, d in enumerate(devices):
+            c.devices[i] = d
     c.num_bounces = num_bounces
     c.samples_per_frame = samples_per_frame
     c.flags = (N.PT_FLAG_DEFER_READBACK if defer_readback else 0) | (N.PT_FLAG_PIN_HOST if pin_host else 0)
     for i in range(3):
         c.ambient[i] = float(ambient[i])
-    global _pin_host
-    _pin_host = False
+    global _watch_buffers
+    _watch_buffers = False
     N.check(L.pt_init(ctypes.byref(c)), "pt_init")
-    _pin_host = bool(pin_host)
+    _watch_buffers = bool(pin_host or defer_readback)
 
 
 def shutdown() -> None:
-    global _pin_host
+    global _watch_buffers
     N.load().pt_shutdown()
-    _pin_host = False
+    _watch_buffers = False
 
 
 def initialized_device() -> int | None:
-    """The HIP device the library state lives on (None before init)."""
+    """The (first) HIP device the library state lives on (None before init)."""
     d = int(N.load().pt_initialized_device())
     return None if d < 0 else d
+
+
+def initialized_devices() -> list[int]:
+    """The HIP ordinals of the library's logical devices ([] before init)."""
+    L = N.load()
+    return [int(L.pt_device_ordinal(i)) for i in range(int(L.pt_device_count()))]
 
 
 def unpin_host(BufferOut: np.ndarray | None = None) -> None:
     """pin_host mode: drop the page-lock of BufferOut (None: of any pinned buffer) before freeing it."""
     ptr = None if BufferOut is None else ctypes.c_void_p(BufferOut.ctypes.data)
     N.check(N.load().pt_unpin_host(ptr), "pt_unpin_host")
+
+
+def release_buffer(BufferOut: np.ndarray | None = None) -> None:
+    """Before freeing / reallocating BufferOut (None: whichever buffer): drop its deferred device copy
+    (not written back) and its page-lock (pt_release_buffer)."""
+    ptr = None if BufferOut is None else ctypes.c_void_p(BufferOut.ctypes.data)
+    N.check(N.load().pt_release_buffer(ptr), "pt_release_buffer")
 
 
 def set_frame(frame: int) -> None:
@@ -366,12 +391,20 @@ def LoadCubemapTexture(filenames) -> texture:
 
 
 def v4_config(env_mode: int = N.PT_V4_ENV_EQUIRECT, random_jitter: bool = True, rejection: bool = True,
-              num_bounces: int = 8, output_to_screen: bool = True) -> None:
+              num_bounces: int = 8, output_to_screen: bool = True, accumulate_frames: bool = True,
+              fast_aces: bool = True, fast_gamma: bool = True, fast_exp: bool = True) -> None:
     """The v4 switches of global_preprocessor_flags.h (USE_ENV_MAP / USE_ENV_CUBEMAP,
-    USE_RANDOM_JITTER_TEXTURE_SAMPLING, USE_UNIT_VECTOR_REJECTION_SAMPLING, OUTPUT_TO_SCREEN) and
-    c_numBounces (v4 :23)."""
-    c = N.PtV4Config(env_mode, int(random_jitter), int(rejection), num_bounces, int(output_to_screen))
+    USE_RANDOM_JITTER_TEXTURE_SAMPLING, USE_UNIT_VECTOR_REJECTION_SAMPLING, OUTPUT_TO_SCREEN,
+    ACCUMULATE_FRAMES, USE_FAST_APPROXIMATE_ACES_TONEMAP / _GAMMA / _EXP) and c_numBounces (v4 :23)."""
+    c = N.PtV4Config(env_mode, int(random_jitter), int(rejection), num_bounces, int(output_to_screen),
+                     int(accumulate_frames), int(fast_aces), int(fast_gamma), int(fast_exp))
     N.check(N.load().pt_v4_set_config(ctypes.byref(c)), "pt_v4_set_config")
+
+
+def v4_get_config() -> dict:
+    c = N.PtV4Config()
+    N.check(N.load().pt_v4_get_config(ctypes.byref(c)), "pt_v4_get_config")
+    return {k: int(getattr(c, k)) for k, _ in N.PtV4Config._fields_}
 
 
 def InitializeGlobalRenderResources() -> None:

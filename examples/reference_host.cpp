@@ -3,11 +3,15 @@
 // Mirrors ApplicationState::RenderOffline / Render (CPUPerformanceRayTracer/Application.cpp:400-477)
 // using ONLY the reference's function names and types, from include/demofox_path_tracing_mi355.h:
 // InitializeGlobalRenderResources, DemofoxRenderOptV4 / DemofoxRenderSimdTiled / DemofoxRenderScalar,
-// CopyOutputToFile and WriteImage.  The env map is generated in memory (deterministic hash pattern) so
+// CopyOutputToFile and WriteImage, plus the flags bridge (pt_flags.h) for -D overrides of the
+// reference's global_preprocessor_flags.h switches.  The env map is generated in memory (deterministic hash pattern) so
 // the program needs no texture file; tests/test_gpu_host.py renders the same with the oracle.
 //
 //   reference_host <renderer: scalar|tiled|v4> <width> <height> <frames> <out.f32> [out.bmp]
 #include "demofox_path_tracing_mi355.h"
+// The reference's compile-time switches (global_preprocessor_flags.h) -- given with -D here -- are
+// applied to the backend by the bridge header (include/pt_flags.h).
+#include "pt_flags.h"
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -39,6 +43,10 @@ int main(int argc, char** argv)
     std::vector<uint32_t> Screen((size_t)W * H, 0);
     texture Texture = MakeTexture(128, 64);
 
+    if (pt_apply_global_preprocessor_flags() != PT_OK) {   // the host's global_preprocessor_flags.h
+        fprintf(stderr, "flags: %s\n", pt_last_error());
+        return 1;
+    }
     InitializeGlobalRenderResources();   // Application.cpp:413
     for (i32 f = 0; f < frames; ++f) {   // Render() per frame (Application.cpp:460-477)
         if (!strcmp(renderer, "v4"))

@@ -14,6 +14,8 @@
  * with it; the first call renders frame 1.
  *
  * Threading: like the reference (static state, not re-entrant) -- call from one host thread.
+ * Devices: one or several GPUs per process (pt_config.device_count / PT_MI355_DEVICES); entry points
+ * restore the caller's current HIP device before they return.
  */
 #ifndef PT_MI355_H
 #define PT_MI355_H
@@ -39,22 +41,39 @@ extern "C" {
                                    /* the host buffer is refreshed by pt_readback(), or written back */
                                    /* automatically when a call names a different buffer (the device */
                                    /* mirror holds one buffer at a time).  pt_shutdown discards it.  */
+                                   /* Call pt_release_buffer(buf) before freeing or reallocating a   */
+                                   /* deferred buffer (its device copy is dropped, never written to  */
+                                   /* freed memory); ReinitializeRenderTileData does it for Resize.  */
 #define PT_FLAG_PIN_HOST 2u        /* page-lock the caller's frame buffer (hipHostRegister; kept until */
                                    /* pt_unpin_host, pt_shutdown, ReinitializeRenderTileData or      */
                                    /* another buffer is passed) and overlap its PCIe transfers with  */
                                    /* rendering, in row bands (same results) -- frame calls, and work */
                                    /* queues whose entries are a whole frame of tiles of one buffer. */
-                                   /* Free a pinned buffer only after pt_unpin_host(buf) (a Resize   */
-                                   /* that reallocates it).                                          */
+                                   /* Free a pinned buffer only after pt_unpin_host(buf) or          */
+                                   /* pt_release_buffer(buf) (a Resize that reallocates it): the     */
+                                   /* registration of a freed buffer cannot be detected reliably.    */
+                                   /* One device only (several devices: the plain path).             */
+
+#define PT_MAX_DEVICES 16
 
 /* Runtime form of the reference's compile-time configuration (global_preprocessor_flags.h and the
  * file-scope constants of demofox_path_tracing_scalar.cpp:6-25). */
 typedef struct pt_config {
-    int32_t device;              /* HIP device ordinal                                             */
+    int32_t device;              /* HIP device ordinal (device_count <= 1)                         */
     int32_t num_bounces;         /* c_numBounces (scalar.cpp:19); reference default 4              */
     int32_t samples_per_frame;   /* NUM_SAMPLES_PER_FRAME (flags.h:30): frames accumulated per call */
     uint32_t flags;              /* PT_FLAG_*                                                      */
     float ambient[3];            /* miss radiance (scalar.cpp:307), reference default 0.1          */
+    /* Several GPUs in one process (the reference fans a frame's tiles out over NUM_THREADS CPU
+     * threads, simd_tiled.cpp:549-571, v4 :1696-1721): with device_count > 1 every host-buffer entry
+     * point deals the frame's rows to devices[0..device_count) -- row Y to devices[Y % device_count]
+     * -- and each device mirrors its own rows; results are bit-identical to one device.  An ordinal
+     * may repeat (logical shards of one GPU).  pt_default_config fills these from the environment
+     * variable PT_MI355_DEVICES ("all" or "0,1,2,3"; unset: device 0), so a reference host that
+     * never calls pt_init drives several GPUs unchanged.  Device jobs run on the device holding
+     * their buffer. */
+    int32_t device_count;        /* 0 or 1: `device` alone                                         */
+    int32_t devices[PT_MAX_DEVICES];
 } pt_config;
 
 /* Mirrors of RenderBufferInfo / RenderTileInfo (demofox_path_tracing_simd_tiled.cpp:473-487). */
@@ -134,9 +153,15 @@ int pt_readback(float* buf);
 /* PT_FLAG_PIN_HOST: drop the page-lock of `buf` (NULL: of whichever buffer is pinned) before the
  * caller frees or reallocates it (Application.cpp:142-151 Resize).  No-op if it is not pinned. */
 int pt_unpin_host(const void* buf);
-/* the HIP device the library state lives on, or -1 before pt_init (library state is per process
- * and per device: a job on another device is an error, not a re-initialisation) */
+/* The caller is about to free or reallocate `buf` (NULL: whichever buffer): forget every device-side
+ * association -- the PT_FLAG_DEFER_READBACK device copy (dropped, NOT written back) and the
+ * PT_FLAG_PIN_HOST page-lock.  Mandatory before freeing a deferred or pinned buffer. */
+int pt_release_buffer(const void* buf);
+/* the (first) HIP device the library state lives on, or -1 before pt_init (a device job on a device
+ * the library was not initialised with is an error, not a re-initialisation) */
 int32_t pt_initialized_device(void);
+int32_t pt_device_count(void);               /* logical devices (0 before pt_init)             */
+int32_t pt_device_ordinal(int32_t index);    /* HIP ordinal of logical device `index`, or -1    */
 
 /* --- env map (config 4: miss radiance = EquirectangularTextureSample, texture.cpp:101-139) ----- */
 /* replaces LoadTexture, asset_loading.cpp:9-16 (Radiance RGBE .hdr, flipped vertically) */
@@ -189,6 +214,14 @@ typedef struct pt_v4_config {
     int32_t num_bounces;         /* c_numBounces (v4 :23): 8                                                */
     int32_t output_to_screen;    /* OUTPUT_TO_SCREEN (flags.h:60, 1): DemofoxRenderOptV4 also writes the    */
                                  /*   ScreenBufferData pixels (OutputToScreen v4 :1260-1295) when non-NULL  */
+    int32_t accumulate_frames;   /* ACCUMULATE_FRAMES (flags.h:60, 1): the progressive fused lerp into the  */
+                                 /*   accumulator (RenderTile v4 :1199-1241); 0 stores each frame's colour  */
+    int32_t fast_aces;           /* USE_FAST_APPROXIMATE_ACES_TONEMAP (flags.h:63, 1): ACESFilm by rcp of   */
+                                 /*   the fused denominator (v4 :168-171); 0: unfused ops and '/' (:172-174) */
+    int32_t fast_gamma;          /* USE_FAST_APPROXIMATE_GAMMA (flags.h:62, 1): fast_pow_gamma (v4 :144-155, */
+                                 /*   :182-183); 0: pow(x, 1/2.4) (:184-185, SVML pow_ps -> glibc powf)      */
+    int32_t fast_exp;            /* USE_FAST_APPROXIMATE_EXP (flags.h:64, 1): Beer absorption by           */
+                                 /*   approx_exp_ps (v4 :783-784, :971-972); 0: exp_ps (SVML -> glibc expf) */
 } pt_v4_config;
 
 /* SceneMaterial (v4 :367-378), the argument of AddMaterialToScene. */
@@ -200,6 +233,7 @@ typedef struct pt_v4_material {
 
 void pt_v4_default_config(pt_v4_config* cfg);
 int pt_v4_set_config(const pt_v4_config* cfg);
+int pt_v4_get_config(pt_v4_config* cfg);
 /* InitializeGlobalRenderResources (v4 :1640-1661): camera + InitializeScene on first use */
 int pt_v4_initialize_global_render_resources(void);
 /* ReinitializeRenderTileData (v4 :1723-1726), called by the host's Resize (Application.cpp:154)

@@ -84,6 +84,11 @@ void pto_env_sample(const pto_env* env, const float dir[3], float out3[3]); /* t
 uint32_t pto_tonemap_channel(float linear);
 uint32_t pto_tonemap_pixel(const float rgb[3], int32_t format);
 void pto_tonemap(const float* rgb, int32_t w, int32_t h, int32_t format, uint32_t* out);
+/* the non-default branches: exact_aces = USE_FAST_APPROXIMATE_ACES_TONEMAP 0, exact_gamma =
+ * USE_FAST_APPROXIMATE_GAMMA 0 (global_preprocessor_flags.h:62-63) */
+uint32_t pto_tonemap_channel_ex(float linear, int32_t exact_aces, int32_t exact_gamma);
+void pto_tonemap_ex(const float* rgb, int32_t w, int32_t h, int32_t format, int32_t exact_aces, int32_t exact_gamma,
+                    uint32_t* out);
 
 /* ---- v4 renderer (pt_oracle_v4.c): demofox_path_tracing_optimization_v4.cpp restated ---------- */
 #define PTO4_MAX_OBJECTS 12      /* MAX_OBJECTS / MAX_MATERIALS, v4 :351-352 (quads + spheres <= 12) */
@@ -114,6 +119,8 @@ typedef struct pto4_params {
     int32_t rejection;            /* USE_UNIT_VECTOR_REJECTION_SAMPLING (1) else sin/cos          */
     const pto_env* env;           /* equirect map or stacked cubemap; NULL => ambient             */
     int32_t nthreads;
+    int32_t no_accumulate;        /* ACCUMULATE_FRAMES 0 (flags.h:60): store each frame's colour   */
+    int32_t exact_exp;            /* USE_FAST_APPROXIMATE_EXP 0 (flags.h:64): expf for exp_ps      */
 } pto4_params;
 
 typedef struct pto4_counts {

@@ -2,9 +2,11 @@
  * output stage, the checker for the GPU tonemap kernel (csrc/pt_output.hip).  Never linked into
  * the product.
  *
- * Reference (CPUPerformanceRayTracer/demofox_path_tracing_optimization_v4.cpp, with the
- * global_preprocessor_flags.h:62-63 defaults USE_FAST_APPROXIMATE_GAMMA = 1 and
- * USE_FAST_APPROXIMATE_ACES_TONEMAP = 1):
+ * Reference (CPUPerformanceRayTracer/demofox_path_tracing_optimization_v4.cpp; the defaults of
+ * global_preprocessor_flags.h:62-63, USE_FAST_APPROXIMATE_GAMMA = USE_FAST_APPROXIMATE_ACES_TONEMAP = 1,
+ * and (pto_tonemap_ex) their 0 branches: ACESFilm :172-174 with '/', LinearToSRGB :184-185 with
+ * SVML pow_ps, for which the host libm's powf stands in -- as for the other SVML calls, parity with
+ * SVML itself is unpinned):
  *   fast_pow_gamma        :144-155   x^(1/2.4) = sqrt(sqrt(x) * cbrt(x)), 3 Newton steps for cbrt
  *   ACESFilm              :165-175   saturate(X (a X + b) * rcp(X (c X + d) + e))
  *   LinearToSRGB          :177-186   x < 0.0031308 ? 12.92 x : 1.055 pow - 0.055 (fmsub)
@@ -46,29 +48,52 @@ static float aces(float X)   /* v4 :165-175 (fast path) */
     return saturate((X * fmaf(a, X, b)) * rcp_denom);
 }
 
-static float linear_to_srgb(float x)   /* v4 :177-186 */
+static float aces_exact(float X)   /* v4 :172-174 (USE_FAST_APPROXIMATE_ACES_TONEMAP 0) */
 {
-    x = saturate(x);
-    return x < 0.0031308f ? x * 12.92f : fmaf(1.055f, fast_pow_gamma(x), -0.055f);
+    const float a = 2.51f, b = 0.03f, c = 2.43f, d = 0.59f, e = 0.14f;
+    /* f32 scalar x m256x3 operators: unfused mul / add, then _mm256_div_ps (IEEE) */
+    return saturate((X * (a * X + b)) / (X * (c * X + d) + e));
 }
 
-uint32_t pto_tonemap_channel(float linear)
+static float linear_to_srgb(float x, int exact_gamma)   /* v4 :177-186 */
+{
+    x = saturate(x);
+    if (x < 0.0031308f) return x * 12.92f;
+    if (exact_gamma)   /* :184-185: 1.055f * pow_ps(rgb, 1 / 2.4f) - 0.055f; SVML pow_ps -> libm powf */
+        return 1.055f * powf(x, 1.0f / 2.4f) - 0.055f;
+    return fmaf(1.055f, fast_pow_gamma(x), -0.055f);   /* :182-183 fmsub */
+}
+
+uint32_t pto_tonemap_channel_ex(float linear, int32_t exact_aces, int32_t exact_gamma)
 {
     const float c_exposure = 1.0f;
-    const float v = saturate(linear_to_srgb(aces(linear * c_exposure))) * 255.f;
+    const float t = exact_aces ? aces_exact(linear * c_exposure) : aces(linear * c_exposure);
+    const float v = saturate(linear_to_srgb(t, exact_gamma)) * 255.f;
     const float r = rintf(v);   /* cvtps_epi32, round to nearest even (default MXCSR) */
     return (uint32_t)(int32_t)r & 0xFFu;
 }
 
-uint32_t pto_tonemap_pixel(const float rgb[3], int32_t format)
+uint32_t pto_tonemap_channel(float linear) { return pto_tonemap_channel_ex(linear, 0, 0); }
+
+static uint32_t pixel_ex(const float rgb[3], int32_t format, int32_t exact_aces, int32_t exact_gamma)
 {
-    const uint32_t r = pto_tonemap_channel(rgb[0]), g = pto_tonemap_channel(rgb[1]), b = pto_tonemap_channel(rgb[2]);
+    const uint32_t r = pto_tonemap_channel_ex(rgb[0], exact_aces, exact_gamma);
+    const uint32_t g = pto_tonemap_channel_ex(rgb[1], exact_aces, exact_gamma);
+    const uint32_t b = pto_tonemap_channel_ex(rgb[2], exact_aces, exact_gamma);
     if (format == PTO_PIXEL_XRGB8) return (r << 16) | (g << 8) | b;               /* :1282-1285 */
     return 0xFF000000u | (b << 16) | (g << 8) | r;                               /* :1319-1323 */
 }
 
+uint32_t pto_tonemap_pixel(const float rgb[3], int32_t format) { return pixel_ex(rgb, format, 0, 0); }
+
 /* The whole accumulator, interleaved RGB rows (row 0 = top), to packed pixels. */
+void pto_tonemap_ex(const float* rgb, int32_t w, int32_t h, int32_t format, int32_t exact_aces, int32_t exact_gamma,
+                    uint32_t* out)
+{
+    for (int64_t i = 0; i < (int64_t)w * h; ++i) out[i] = pixel_ex(rgb + 3 * i, format, exact_aces, exact_gamma);
+}
+
 void pto_tonemap(const float* rgb, int32_t w, int32_t h, int32_t format, uint32_t* out)
 {
-    for (int64_t i = 0; i < (int64_t)w * h; ++i) out[i] = pto_tonemap_pixel(rgb + 3 * i, format);
+    pto_tonemap_ex(rgb, w, h, format, 0, 0, out);
 }

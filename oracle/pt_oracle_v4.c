@@ -465,7 +465,7 @@ typedef struct {
  *   per sample      camera 23, c_numRendersPerFrame scale 6, accumulate 9 = 38 */
 #define CNT(c, n) do { if ((c)->cnt) (c)->cnt->flops += (uint64_t)(n); } while (0)
 
-/* GetColorForRay, v4 :722-911 (USE_FAST_APPROXIMATE_EXP = 1) */
+/* GetColorForRay, v4 :722-911 (USE_FAST_APPROXIMATE_EXP: p->exact_exp) */
 static v3 color_for_ray(const ctx4* c, v3 pos, v3 dir, uint32_t* rng)
 {
     const pto4_params* p = c->p;
@@ -497,8 +497,11 @@ static v3 color_for_ray(const ctx4* c, v3 pos, v3 dir, uint32_t* rng)
         }
         const m4* M = &s->mat[h.mat];   /* GatherMaterials :389-427 */
         const v3 rc = mk(M->refr_color[0], M->refr_color[1], M->refr_color[2]);
-        if (h.from_inside) {   /* :797 (Beer's law, approx_exp) */
-            T = mul3(T, mk(approx_exp(-rc.x * h.dist), approx_exp(-rc.y * h.dist), approx_exp(-rc.z * h.dist)));
+        if (h.from_inside) {   /* :797 (Beer's law) */
+            if (p->exact_exp)      /* USE_FAST_APPROXIMATE_EXP 0 (:785-787): exp_ps -> libm expf */
+                T = mul3(T, mk(expf(-rc.x * h.dist), expf(-rc.y * h.dist), expf(-rc.z * h.dist)));
+            else                   /* :783-784: approx_exp_ps */
+                T = mul3(T, mk(approx_exp(-rc.x * h.dist), approx_exp(-rc.y * h.dist), approx_exp(-rc.z * h.dist)));
             CNT(c, 24);
         }
 
@@ -609,6 +612,12 @@ static void row4(const ctx4* c, float* out, int32_t Y)
         for (int32_t f = 0; f < p->nframes; ++f) {
             const uint32_t frame = p->frame_first + (uint32_t)f;
             const v3 col = main_image(c, X, Y, frame);
+            if (p->no_accumulate) {   /* ACCUMULATE_FRAMES 0: the colour is stored (:1245-1250) */
+                px[0] = col.x;
+                px[1] = col.y;
+                px[2] = col.z;
+                continue;
+            }
             const float bf = 1.0f / ((float)frame + 1.0f);   /* :1200, ACCUMULATE_FRAMES */
             px[0] = fmaf(bf, col.x - px[0], px[0]);         /* :1243 */
             px[1] = fmaf(bf, col.y - px[1], px[1]);

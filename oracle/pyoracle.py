@@ -66,6 +66,11 @@ def load() -> ctypes.CDLL:
         L.pto_tonemap_channel.argtypes = [ctypes.c_float]
         L.pto_tonemap.restype = None
         L.pto_tonemap.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
+        L.pto_tonemap_ex.restype = None
+        L.pto_tonemap_ex.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                     ctypes.c_int32, ctypes.c_void_p]
+        L.pto_tonemap_channel_ex.restype = ctypes.c_uint32
+        L.pto_tonemap_channel_ex.argtypes = [ctypes.c_float, ctypes.c_int32, ctypes.c_int32]
         _lib = L
     return _lib
 
@@ -149,17 +154,18 @@ PIXEL_RGBA8 = 0   # PTO_PIXEL_RGBA8 (OutputToFile)
 PIXEL_XRGB8 = 1   # PTO_PIXEL_XRGB8 (OutputToScreen)
 
 
-def tonemap(rgb: np.ndarray, fmt: int = PIXEL_RGBA8) -> np.ndarray:
-    """Output stage of v4 (oracle/pt_oracle_output.c) on an interleaved H x W x 3 accumulator."""
+def tonemap(rgb: np.ndarray, fmt: int = PIXEL_RGBA8, fast_aces: bool = True, fast_gamma: bool = True) -> np.ndarray:
+    """Output stage of v4 (oracle/pt_oracle_output.c) on an interleaved H x W x 3 accumulator;
+    fast_aces / fast_gamma: USE_FAST_APPROXIMATE_ACES_TONEMAP / _GAMMA (global_preprocessor_flags.h:62-63)."""
     a = np.ascontiguousarray(rgb, dtype=np.float32)
     h, w = a.shape[0], a.shape[1]
     out = np.empty((h, w), np.uint32)
-    load().pto_tonemap(a.ctypes.data, w, h, fmt, out.ctypes.data)
+    load().pto_tonemap_ex(a.ctypes.data, w, h, fmt, int(not fast_aces), int(not fast_gamma), out.ctypes.data)
     return out
 
 
-def tonemap_channel(v: float) -> int:
-    return int(load().pto_tonemap_channel(float(v)))
+def tonemap_channel(v: float, fast_aces: bool = True, fast_gamma: bool = True) -> int:
+    return int(load().pto_tonemap_channel_ex(float(v), int(not fast_aces), int(not fast_gamma)))
 
 
 # ---- v4 renderer (pt_oracle_v4.c) -----------------------------------------------------------------
@@ -184,7 +190,7 @@ class Params4(ctypes.Structure):
                 ("row_stride", ctypes.c_int32), ("nrows", ctypes.c_int32), ("frame_first", ctypes.c_uint32),
                 ("nframes", ctypes.c_int32), ("num_bounces", ctypes.c_int32), ("env_mode", ctypes.c_int32),
                 ("random_jitter", ctypes.c_int32), ("rejection", ctypes.c_int32), ("env", ctypes.POINTER(Env)),
-                ("nthreads", ctypes.c_int32)]
+                ("nthreads", ctypes.c_int32), ("no_accumulate", ctypes.c_int32), ("exact_exp", ctypes.c_int32)]
 
 
 class Counts4(ctypes.Structure):
@@ -222,17 +228,19 @@ def render4(width: int, height: int, *, frame_first: int = 1, nframes: int = 1, 
             row_start: int = 0, row_stride: int = 1, nrows: int | None = None, env_mode: int = ENV_EQUIRECT,
             env: np.ndarray | None = None, random_jitter: bool = True, rejection: bool = True,
             scene: Scene4 | None = None, nthreads: int | None = None, buf: np.ndarray | None = None,
-            counts: bool = False):
+            counts: bool = False, accumulate: bool = True, fast_exp: bool = True):
     """v4 renderer (DemofoxRenderOptV4): accumulate frames [frame_first, +nframes) into buf
     (nrows x width x 3, interleaved).  env None => ambient (USE_ENV_MAP 0).  counts=True returns
-    (buf, {samples, segments, escaped}) and renders single-threaded."""
+    (buf, {samples, segments, escaped}) and renders single-threaded.  accumulate / fast_exp:
+    ACCUMULATE_FRAMES / USE_FAST_APPROXIMATE_EXP (global_preprocessor_flags.h:60,64)."""
     nrows = height if nrows is None else nrows
     if buf is None:
         buf = np.zeros((nrows, width, 3), np.float32)
     assert buf.dtype == np.float32 and buf.flags["C_CONTIGUOUS"] and buf.size >= nrows * width * 3
     nthreads = nthreads if nthreads is not None else min(os.cpu_count() or 1, 16)
     p = Params4(width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces,
-                env_mode if env is not None else ENV_NONE, int(random_jitter), int(rejection), None, nthreads)
+                env_mode if env is not None else ENV_NONE, int(random_jitter), int(rejection), None, nthreads,
+                int(not accumulate), int(not fast_exp))
     keep = None
     if env is not None:
         env = np.ascontiguousarray(env, dtype=np.float32)

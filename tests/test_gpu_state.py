@@ -3,7 +3,9 @@
 * PT_FLAG_DEFER_READBACK with two alternating host buffers: the device mirror holds one buffer at a
   time, and handing it to the other buffer first writes the old accumulation back (nothing lost);
 * PT_FLAG_PIN_HOST with the render target freed and reallocated between calls (numpy reuses the
-  address): the stale page-lock is dropped, every call still equals the oracle;
+  address): the page-lock is released by the buffer's finalizer, every call still equals the oracle;
+* a deferred buffer freed or released (pt_release_buffer, ReinitializeRenderTileData) is never
+  written back; the same address with another size is a new buffer;
 * device jobs alternating between two HIP streams for more launches than the tile-queue ring has
   slots: a slot reused across streams waits for its previous launch (event-ordered);
 * a device job on a device other than the initialised one is an error, not a silent re-init.
@@ -92,6 +94,52 @@ def test_pinned_buffer_reallocated_between_calls():
     pt.DemofoxRenderScalar(a, w, h, 3)        # re-pinned on use
     ref = pyoracle.render(w, h, frame_first=5, nframes=2, num_bounces=b)
     assert bits_equal(a, ref), mismatch_report(a, ref)
+    pt.shutdown()
+
+
+def test_deferred_buffer_freed_then_new_size():
+    """A deferred buffer is freed (its finalizer releases it: no write-back into freed memory), then
+    a buffer of another size is rendered (round-2 advisor finding)."""
+    pt.init(num_bounces=4, defer_readback=True)
+    a = np.zeros((60, 80, 3), np.float32)
+    pt.DemofoxRenderScalar(a, 80, 60, 3)
+    pt.DemofoxRenderScalar(a, 80, 60, 3)
+    del a
+    gc.collect()
+    b = np.zeros((96, 128, 3), np.float32)
+    pt.DemofoxRenderScalar(b, 128, 96, 3)   # frame 3
+    pt.readback(b)
+    ref = pyoracle.render(128, 96, frame_first=3, nframes=1, num_bounces=4)
+    assert bits_equal(b, ref), mismatch_report(b, ref)
+    pt.shutdown()
+
+
+def test_release_buffer_drops_without_write_back():
+    """pt_release_buffer (called directly, as a C host would before free): the released buffer is
+    never written to again; the same pointer with another size is treated as a new buffer; the
+    host's Resize hook (ReinitializeRenderTileData) releases too."""
+    L = N.load()
+    pt.init(num_bounces=4, defer_readback=True)
+    a = np.zeros((60, 80, 3), np.float32)
+    pt.DemofoxRenderScalar(a, 80, 60, 3)
+    assert not a.any()                          # deferred: nothing copied back yet
+    assert L.pt_release_buffer(a.ctypes.data) == 0
+    b = np.zeros((40, 64, 3), np.float32)
+    pt.DemofoxRenderScalar(b, 64, 40, 3)        # would have written `a` back before taking the mirror
+    assert not a.any()
+    with pytest.raises(N.PtError):
+        pt.readback(a)
+    # the same address, another size (a reallocation in place): dropped, staged from the host
+    big = np.zeros((60, 80, 3), np.float32)
+    pt.DemofoxRenderScalar(big, 80, 60, 3)      # frame 3 into big's mirror
+    pt.DemofoxRenderScalar(big, 64, 40, 3)      # same pointer, 64x40: not written back, re-staged
+    pt.readback(big)
+    ref = pyoracle.render(64, 40, frame_first=4, nframes=1, num_bounces=4)
+    assert bits_equal(big.reshape(-1)[:64 * 40 * 3].reshape(40, 64, 3), ref)
+    assert not big.reshape(-1)[64 * 40 * 3:].any()
+    pt.ReinitializeRenderTileData()
+    with pytest.raises(N.PtError):
+        pt.readback(big)
     pt.shutdown()
 
 
