@@ -505,8 +505,12 @@ int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls)
             ls->units = s->units;
             ls->nunits = s->units + s->key.ntiles + 1;
         }
-        ls->cost = s->cost;
-        s->have_cost = true;
+        // the kernel records the tiles' costs only when the next launch builds from them (one 4-B
+        // store per tile is a 32-B HBM write: ~1 MB per 1080p launch otherwise)
+        if (!s->built || (s->launches + 1) % kSchedRebuild == 0) {
+            ls->cost = s->cost;
+            s->have_cost = true;
+        }
         ++s->launches;
     }
     // Ring slots are used in order.  Each render kernel zeroes the NEXT slot's counters at its start,

@@ -131,6 +131,12 @@ __device__ __forceinline__ bool facing(V3 n, V3 D)
 struct AxisRow {
     float a, b, c, d;
 };
+// The per-axis rows of a quad, s_axis[(q * F + fl) * 3 + k]: QV kernels keep them for both vertex
+// orders (F = 2: row (q, fl, k) holds the components in the order after the facing flip, so the
+// culled stage reads its quad's row without selects); the env kernel, whose LDS is full at 4
+// blocks per CU, only the unflipped ones (F = 1).
+template <bool QV>
+constexpr int kAxisRowsPerQuad = QV ? 6 : 3;
 
 // TestQuadTrace, scalar.cpp:65-143.  `pq` = (rayPos + rayDir) - rayPos (ray-constant, hoisted),
 // `axis`/`dP`/`dD`/`yD` = the component :121-133 divides by, its ray origin, direction, RN(1/dir),
@@ -352,7 +358,7 @@ struct Hit {
 };
 
 // The six exact quad tests in the reference's order (TestSceneTrace :192-261) into h.
-template <class SC>
+template <class SC, bool QV>
 __device__ __forceinline__ void quads_exact(const AxisRow* s_axis, V3 P, V3 D, V3 pq, int axis, float dP, float dD,
                                             float yD, Hit& h)
 {
@@ -368,7 +374,7 @@ __device__ __forceinline__ void quads_exact(const AxisRow* s_axis, V3 P, V3 D, V
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(row));
         const AxisRow cur{row.x, row.y, row.z, row.w};
         if (q + 1 < PT_NQUADS)
-            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(row) : "v"(base), "i"((q + 1) * 3 * (int)sizeof(AxisRow)));
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(row) : "v"(base), "i"((q + 1) * kAxisRowsPerQuad<QV> * (int)sizeof(AxisRow)));
         quad_test<SC>(q, P, D, pq, dP, dD, yD, h.best, h.id, h.flag, cur);
     }
 }
@@ -397,7 +403,8 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, 
     // running best).
     const ptqc::F3 Pf{P.x, P.y, P.z}, pqf{pq.x, pq.y, pq.z};
     const ptqc::Cull cl = ptqc::cull<CAMERA>(Pf, pqf, dP, yD);
-    const int W = cl.W < 0 ? 0 : cl.W;
+    const bool hasW = cl.k1 < ptqc::kNoKey;
+    const int W = cl.k1 & 7;   // (any quad when there is no candidate: its result is then discarded)
     const uint32_t jW = (ptqc::kAxisBits >> (2u * (uint32_t)W)) & 3u;
     const float DjW = jW == 0 ? D.x : (jW == 1 ? D.y : D.z);
     const bool fl = DjW > 0.0f;                                          // :69 (unit normal +e_j)
@@ -406,7 +413,7 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, 
     if (QV) {
         const float4* rec = s_qv + (W * 2 + (fl ? 1 : 0)) * 3;
         r0 = rec[0], r1 = rec[1], r2 = rec[2];
-        ar = s_axis[W * 3 + axis];
+        ar = s_axis[(W * 2 + (fl ? 1 : 0)) * 3 + axis];   // flip-ordered: (ak, bk, ck, dk)
     } else {
         // rows x, y, z of quad W: (a_k, b_k, c_k, d_k); flipped order d, c, b, a
         const AxisRow rx = s_axis[W * 3 + 0], ry = s_axis[W * 3 + 1], rz = s_axis[W * 3 + 2];
@@ -419,14 +426,15 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, 
         r1 = make_float4(vb.y, vb.z, vc.x, vc.y);
         r2 = make_float4(vc.z, vd.x, vd.y, vd.z);
     }
-    const float ak = fl ? ar.d : ar.a, bk = fl ? ar.c : ar.b, ck = fl ? ar.b : ar.c, dk = fl ? ar.a : ar.d;
+    const float ak = QV ? ar.a : (fl ? ar.d : ar.a), bk = QV ? ar.b : (fl ? ar.c : ar.b);
+    const float ck = QV ? ar.c : (fl ? ar.b : ar.c), dk = QV ? ar.d : (fl ? ar.a : ar.d);
     float dist;
     const int code = ptqc::quad_exact(Pf, pqf, ptqc::F3{r0.x, r0.y, r0.z}, ptqc::F3{r0.w, r1.x, r1.y},
                                       ptqc::F3{r1.z, r1.w, r2.x}, ptqc::F3{r2.y, r2.z, r2.w}, ak, bk, ck, dk, dP, dD,
                                       yD, PT_SUPER_FAR, dist);
-    const bool ok = code == ptqc::kAccepted && cl.lb2 > dist;
-    bool unc = cl.unc || (cl.W >= 0 && !ok);
-    if (cl.W >= 0 && ok) {
+    const bool ok = code == ptqc::kAccepted && ptqc::cull_beyond(cl, dist);
+    bool unc = cl.unc || (hasW && !ok);
+    if (hasW && ok) {
         h.best = dist;
         h.id = W;
         h.flag = fl ? 1 : 0;
@@ -434,7 +442,7 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, 
     if (__any(unc)) {
         if (unc) {
             h = Hit{PT_SUPER_FAR, -1, 0, 1};
-            quads_exact<SC>(s_axis, P, D, pq, axis, dP, dD, yD, h);
+            quads_exact<SC, QV>(s_axis, P, D, pq, axis, dP, dD, yD, h);
         }
     }
     if (SPH_CLOSEST) {
@@ -538,13 +546,13 @@ constexpr int waves_per_block() { return 4; }
 //      (:812), reading the radiance of each frame from LDS (or the constant radiance of a pixel
 //      whose camera ray missed / of c_numBounces = 0).
 // Tiles come from a per-launch atomic queue (persistent waves, next tile prefetched).
-template <int LAYOUT, bool ENV, bool COUNT>
+template <int LAYOUT, bool ENV, bool COUNT, bool MULTI>
 __device__ __forceinline__ void render_body(const PtJob& job)
 {
     const PtScene* __restrict__ sc = job.scene;
     constexpr int kWavesPerBlock = waves_per_block<ENV>();
     __shared__ PtLdsPrim s_prim[PT_NPRIMS];
-    __shared__ AxisRow s_axis[PT_NQUADS * 3];
+    __shared__ AxisRow s_axis[PT_NQUADS * kAxisRowsPerQuad<!ENV>];
     // the culled quad stage (pt_quadcull.h); the env kernel's 40 912 B of LDS leave no room for the
     // 576-B flip-ordered vertex table at 4 blocks per CU, so it reads the per-axis rows (QV false)
     constexpr bool QV = !ENV;
@@ -578,9 +586,11 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             e.er = sc->emissive[t][0]; e.eg = sc->emissive[t][1]; e.eb = sc->emissive[t][2];
             e.pad0 = e.pad1 = e.pad2 = 0.0f;
             s_prim[t] = e;
-        } else if (t >= 64 && t < 64 + PT_NQUADS * 3) {
-            const int q = (t - 64) / 3, k = (t - 64) % 3;
-            s_axis[t - 64] = AxisRow{sc->qv[q][0][k], sc->qv[q][1][k], sc->qv[q][2][k], sc->qv[q][3][k]};
+        } else if (t >= 64 && t < 64 + PT_NQUADS * kAxisRowsPerQuad<!ENV>) {
+            constexpr int F = kAxisRowsPerQuad<!ENV> / 3;
+            const int r = (t - 64) / 3, k = (t - 64) % 3, q = r / F, fl = r % F;
+            const auto vk = [&](int v) { return sc->qv[q][fl ? 3 - v : v][k]; };
+            s_axis[t - 64] = AxisRow{vk(0), vk(1), vk(2), vk(3)};
         } else if (QV && t >= 128 && t < 128 + kQuadVecs) {
             const int r = (t - 128) / 3, part = (t - 128) % 3, q = r >> 1, fl = r & 1;
             float e[4];
@@ -634,7 +644,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     constexpr uint32_t kNone = PtTileQueue<kWavesPerBlock>::kNone;
     PtTileQueue<kWavesPerBlock> tq(job.queue, job.order, job.units, job.nunits, total_tiles, wv);
     uint32_t tile = kNone, next_tile = kNone;
-    if (lane == 0) tile = tq.first();
+    tile = tq.first();   // (the whole wave: uniform, scalar registers)
     tile = __builtin_amdgcn_readfirstlane(tile);
     while (tile != kNone) {
         const int tyi = (int)(tile / (uint32_t)tiles_x), txi = (int)(tile % (uint32_t)tiles_x);
@@ -651,26 +661,32 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         const bool valid = lc < job.ncols && lr < job.nrows;
         const float fx = (float)(job.col0 + lc);                                            // :806
         const float fy = (float)(job.height - 1 - (job.row_start + lr * job.row_stride));   // :803
-        // (the accumulator address is recomputed for the store: held across phase B it was spilled)
+        // Registers live across the pool loop are kept to a minimum (the 96-VGPR budget of 5 waves per
+        // SIMD): the accumulator is loaded in phase C when one chunk covers the launch's frames
+        // (!MULTI) -- its address recomputed there --, the pixel's bounce-0 record is re-read from
+        // LDS when the own-lane sample starts, whether the pixel has pool items is bit `lane` of
+        // the wave-uniform hitmask, and one register triple (c_keep) holds the constant radiance
+        // of a pixel without items or the own-lane radiance of one with items.
         V3 acc = zero;
-        int kind = -1;            // -1 no pixel, 0 camera ray missed, 1 hit and B == 0, 2 has items
-        V3 c_const = zero;        // radiance of every frame for kinds 0 and 1
+        V3 c_keep = zero;         // no items: the radiance of every frame; items: the own-lane frame's
         V3 P1 = zero, N1 = zero;
         int id1 = 0;
+        bool items = false;       // the camera ray hit and c_numBounces > 0: the pixel's frames are pool items
         const V3 D0 = camera_dir(cam, fx, fy);   // (lanes outside the image: unused values)
         // A tile whose camera rays all leave the box's silhouette skips their TestSceneTrace: the
         // result is the reference's miss (sky_ray below), and the trace is the whole cost of such
         // a tile's phase A -- about half of all 1080p tiles are sky.
         const bool all_sky = __ballot(valid && !sky_ray(D0)) == 0;
         if (valid) {
-            const float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
-            acc = v3(px[0], px[cs], px[2 * cs]);
+            if (MULTI) {
+                const float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
+                acc = v3(px[0], px[cs], px[2 * cs]);
+            }
             const Hit h = all_sky ? Hit{PT_SUPER_FAR, -1, 0, 0}
                                   : trace<DemofoxScene, true, QV, !ENV>(s_axis, s_qv, zero, D0);   // :335 rayPos = origin
             if (COUNT) ++n_seg, ++n_prim, n_fb += (unsigned long long)h.fb, n_sky += all_sky ? 1ull : 0ull;
             if (h.best == PT_SUPER_FAR) {                                 // :305-310
-                kind = 0;
-                c_const = add(zero, miss_radiance<ENV>(job, amb, D0));
+                c_keep = add(zero, miss_radiance<ENV>(job, amb, D0));
                 if (COUNT) n_esc += (unsigned long long)S;
             } else {
                 const PtLdsPrim pr = s_prim[h.id];
@@ -678,16 +694,18 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 P1 = add(add(zero, mul(D0, h.best)), mul(n1, PT_NUDGE));  // :313
                 N1 = n1;
                 id1 = h.id;
-                kind = B == 0 ? 1 : 2;
-                c_const = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one)); // :319 (ret after bounce 0)
+                items = B != 0;
+                c_keep = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one));  // :319 (ret after bounce 0)
             }
             if (COUNT) n_samp += (unsigned long long)S;
         }
-        const uint64_t hitmask = __ballot(kind == 2);
+        const uint64_t hitmask = __ballot(items);
         const int nh = __popcll(hitmask);
-        if (kind == 2) {   // compact the pixels with items: slot = rank among them
-            const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(hitmask >> 32),
+        // compacted record slot of this lane's pixel: its rank among the pixels with items
+        const int my_slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(hitmask >> 32),
                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)hitmask, 0u));
+        if (items) {
+            const int slot = my_slot;
             s_rec[wv][slot] = make_float4(P1.x, P1.y, P1.z, __builtin_bit_cast(float, id1 | (lane << 8)));
             s_nrm[wv][0][slot] = N1.x;
             s_nrm[wv][1][slot] = N1.y;
@@ -698,7 +716,8 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         const uint32_t this_tile = tile;
         uint32_t tile_work = 1;   // trace iterations of this tile (the schedule's cost)
 
-        for (int f0 = 0; f0 < S; f0 += CH) {
+        // one chunk covers the launch's frames unless MULTI (then the loop carries acc and c_keep)
+        for (int f0 = 0; f0 < (MULTI ? S : 1); f0 += CH) {
             const int nf = S - f0 < CH ? S - f0 : CH;
             DIAG_ADD(0, t_tile);
             // ---------------- phase B: the pool of (pixel, frame) items ----------------
@@ -710,15 +729,19 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             bool has_item = false, needs_dir = false;
             int it_lane = 0, it_f = 0;
             V3 P = zero, D = zero, T = zero, ret = zero, n = zero;
-            V3 c_last = zero;   // own: the radiance of this pixel's last frame
             uint32_t rng = 0;
             int bounce = 0;
-            if (own && kind == 2) {   // start with this pixel's own last-frame sample (bounce 0 done)
-                const PtLdsPrim pr = s_prim[id1];
-                rng = seed_int((uint32_t)(job.col0 + lc), (uint32_t)(job.height - 1 - (job.row_start + lr * job.row_stride)),
+            const bool mine = (hitmask >> lane) & 1u;   // this lane's pixel has pool items
+            if (own && mine) {   // start with this pixel's own last-frame sample (bounce 0 done)
+                // its bounce-0 record from LDS (P1 / N1 / id1 are not kept across the pool)
+                const float4 a0 = s_rec[wv][my_slot];
+                const int sId = __builtin_bit_cast(int, a0.w) & 0xff;
+                const PtLdsPrim pr = s_prim[sId];
+                const int olc = txi * 8 + (lane & 7), olr = tyi * 8 + (lane >> 3);
+                rng = seed_int((uint32_t)(job.col0 + olc), (uint32_t)(job.height - 1 - (job.row_start + olr * job.row_stride)),
                                job.frame_first + (uint32_t)(f0 + nf - 1));   // :332
-                P = P1;
-                n = N1;
+                P = v3(a0.x, a0.y, a0.z);
+                n = v3(s_nrm[wv][0][my_slot], s_nrm[wv][1][my_slot], s_nrm[wv][2][my_slot]);
                 ret = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one));             // :319
                 T = mulv(one, v3(pr.ar, pr.ag, pr.ab));                          // :322
                 bounce = 1;
@@ -813,7 +836,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                     }
                     if (done) {
                         if (own && it_f == nf - 1) {   // own item: it_lane == lane
-                            c_last = ret;
+                            c_keep = ret;
                         } else {
                             lds_f32* c = col_lds + (it_lane * CHS + it_f) * 3;
                             c[0] = ret.x;
@@ -839,15 +862,21 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 }
             }
             if (DEFER && qn > 0) drain(0, qn);
-            if (f0 + CH >= S && lane == 0) next_tile = tq.next();   // the last chunk's pool is done
+            if (f0 + CH >= S) next_tile = tq.next();   // the last chunk's pool is done
             // ---------------- phase C: progressive lerp in frame order ----------------
             DIAG_MARK(t_c);
-            if (kind >= 0) {
+            const int clc = txi * 8 + (lane & 7), clr = tyi * 8 + (lane >> 3);
+            const bool cvalid = clc < job.ncols && clr < job.nrows;
+            if (cvalid) {
+                if (!MULTI) {   // the accumulator, read once (24 B per pixel per launch with the store)
+                    const float* px = job.buf + out_index<LAYOUT>(job, clc, clr);
+                    acc = v3(px[0], px[cs], px[2 * cs]);
+                }
                 for (int fi = 0; fi < nf; ++fi) {
-                    V3 c = c_const;
-                    if (kind == 2) {
+                    V3 c = c_keep;   // a pixel without items: the same radiance every frame
+                    if (mine) {
                         if (own && fi == nf - 1) {
-                            c = c_last;
+                            c = c_keep;
                         } else {
                             const lds_f32* cp = col_lds + (lane * CHS + fi) * 3;
                             c = v3(cp[0], cp[1], cp[2]);
@@ -862,14 +891,14 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             }
             DIAG_ADD(5, t_c);
         }
-        if (valid) {
-            float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
+        if (txi * 8 + (lane & 7) < job.ncols && tyi * 8 + (lane >> 3) < job.nrows) {
+            float* px = job.buf + out_index<LAYOUT>(job, txi * 8 + (lane & 7), tyi * 8 + (lane >> 3));
             px[0] = acc.x;
             px[cs] = acc.y;
             px[2 * cs] = acc.z;
         }
         if (job.cost && lane == 0) job.cost[this_tile] = tile_work;
-        if (S <= 0 && lane == 0) next_tile = tq.next();   // no chunk ran (nframes 0)
+        if (S <= 0) next_tile = tq.next();   // no chunk ran (nframes 0)
         tile = __builtin_amdgcn_readfirstlane(next_tile);
 #if PT_DIAG && !PT_DIAG_WAVES_ONLY
         if (job.counters && lane == 0 && n_tiles_diag <= 32) {
@@ -929,39 +958,47 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 #ifndef PT_AMBIENT_WAVES
 #define PT_AMBIENT_WAVES 5
 #endif
-template <int LAYOUT, bool COUNT>
+// MULTI: the launch accumulates more frames than one LDS chunk holds (nframes > kChunk).
+template <int LAYOUT, bool COUNT, bool MULTI>
 __global__ __launch_bounds__(64 * waves_per_block<false>()) __attribute__((amdgpu_waves_per_eu(PT_AMBIENT_WAVES, PT_AMBIENT_WAVES))) void
 pt_render_kernel(PtJob job)
 {
-    render_body<LAYOUT, false, COUNT>(job);
+    render_body<LAYOUT, false, COUNT, MULTI>(job);
 }
 
-template <int LAYOUT, bool COUNT>
+template <int LAYOUT, bool COUNT, bool MULTI>
 __global__ __launch_bounds__(64 * waves_per_block<true>()) void pt_render_env_kernel(PtJob job)
 {
-    render_body<LAYOUT, true, COUNT>(job);
+    render_body<LAYOUT, true, COUNT, MULTI>(job);
 }
 
-template <int LAYOUT, bool ENV, bool COUNT>
+template <int LAYOUT, bool ENV, bool COUNT, bool MULTI>
 constexpr auto kernel_of()
 {
-    if constexpr (ENV) return pt_render_env_kernel<LAYOUT, COUNT>;
-    else return pt_render_kernel<LAYOUT, COUNT>;
+    if constexpr (ENV) return pt_render_env_kernel<LAYOUT, COUNT, MULTI>;
+    else return pt_render_kernel<LAYOUT, COUNT, MULTI>;
+}
+
+template <int LAYOUT, bool ENV, bool COUNT, bool MULTI>
+void launch_k(const PtJob& job, hipStream_t st, unsigned tiles)
+{
+    constexpr int wpb = waves_per_block<ENV>();
+    auto k = kernel_of<LAYOUT, ENV, COUNT, MULTI>();
+    const unsigned blocks = (unsigned)std::min<long>(pt_resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
 }
 
 template <int LAYOUT, bool ENV>
 hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 {
-    constexpr int wpb = waves_per_block<ENV>();
     const unsigned tiles = (unsigned)((job.ncols + 7) / 8) * (unsigned)((job.nrows + 7) / 8);
+    const bool multi = job.nframes > kChunk;
     if (count) {
-        auto k = kernel_of<LAYOUT, ENV, true>();
-        const unsigned blocks = (unsigned)std::min<long>(pt_resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
-        hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
+        if (multi) launch_k<LAYOUT, ENV, true, true>(job, st, tiles);
+        else launch_k<LAYOUT, ENV, true, false>(job, st, tiles);
     } else {
-        auto k = kernel_of<LAYOUT, ENV, false>();
-        const unsigned blocks = (unsigned)std::min<long>(pt_resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
-        hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
+        if (multi) launch_k<LAYOUT, ENV, false, true>(job, st, tiles);
+        else launch_k<LAYOUT, ENV, false, false>(job, st, tiles);
     }
     return hipGetLastError();
 }

@@ -160,19 +160,88 @@ PTQC_HD float med3(float a, float b, float c)
 #endif
 }
 
-// Outcome of the classification: lb1/W = the smallest candidate lower bound and its quad, lb2 =
-// the second smallest (kInf if none), unc = a quad's status could not be decided.
+// Outcome of the classification.  Each candidate's lower bound lb is kept as a signed-integer key
+// (bits(lb) & ~7) | q: its float bits with the quad index in the low three bits.  For lb >= 0 the
+// integer order is the float order, and clearing the three low bits only lowers the bound; every
+// negative lb orders below every non-negative one (the order among negatives is irrelevant: any
+// accepted distance exceeds 0.01, so a negative bound never certifies, whichever quad is W).  Ties
+// go to the lower index.  So one min and one median per quad track the smallest key k1 (W = its
+// low bits) and the second smallest k2, with no compare / select for W.  Non-candidates have the
+// key of +inf (>= kNoKey).  unc = a quad's status could not be decided.
 struct Cull {
-    float lb1, lb2;
-    int W;
+    int32_t k1, k2;
     bool unc;
 };
+constexpr int32_t kNoKey = 0x7f800000;   // bits(+inf): the keys of non-candidates are >= it
+PTQC_HD int32_t fbits(float x) { return __builtin_bit_cast(int32_t, x); }
+PTQC_HD int32_t imin(int32_t a, int32_t b) { return a < b ? a : b; }
+PTQC_HD int32_t imax(int32_t a, int32_t b) { return a < b ? b : a; }
+PTQC_HD int32_t imed3(int32_t a, int32_t b, int32_t c) { return imax(imin(a, b), imin(imax(a, b), c)); }
+// W: the quad to test exactly (-1: no candidate)
+PTQC_HD int cull_W(const Cull& c) { return c.k1 < kNoKey ? (c.k1 & 7) : -1; }
+// W's exact distance dist (> 0.01) is certified closest: every other candidate's bound exceeds it
+PTQC_HD bool cull_beyond(const Cull& c, float dist) { return (c.k2 & ~7) > fbits(dist); }
 
 // Per-quad classification, recorded only by the host check (tests/native/check_quadcull.cpp).
 struct CullTrace {
     bool out[PT_NQUADS], cand[PT_NQUADS];
     float s[PT_NQUADS], dl[PT_NQUADS];
 };
+
+// Opposite walls (left / right on x, floor / ceiling on y) are congruent rectangles on parallel
+// planes (static_asserts below).  Of such a pair only the wall the line runs towards -- the plane
+// c = +-12.5 in the direction of pq_j -- can be met ahead of the origin when the origin lies between
+// the planes; the other one is classified by its distance test alone: it is no candidate when
+// s + delta <= c_minimumRayHitTime (exactly the rule below, whatever its OUT status), and when that
+// test does not hold (an origin outside the slab, a loose bound) the ray is flagged uncertain and
+// takes the six exact tests.  A ray nearly parallel to the pair (|pq_j| < kTiny: (4) does not hold,
+// ~0.1% of the rays per axis) classifies the far wall as a rectangle too, in a branch.  So the
+// classification computes four rectangles and two distance tests instead of six rectangles; every
+// certified result is certified by the same rules.
+struct Pair {
+    int q_lo, q_hi;   // the quads at the lower / higher plane
+};
+constexpr Pair kPairX{3, 4}, kPairY{1, 2};
+constexpr bool pair_ok(Pair p)
+{
+    const Rect a = kRect[p.q_lo], b = kRect[p.q_hi];
+    return a.j == b.j && a.k1 == b.k1 && a.k2 == b.k2 && a.c1 == b.c1 && a.c2 == b.c2 && a.h1 == b.h1 && a.h2 == b.h2 &&
+           a.c < b.c;
+}
+static_assert(pair_ok(kPairX) && pair_ok(kPairY), "opposite walls must be congruent rectangles on parallel planes");
+
+// The rectangle classification of quad q with plane constant c (q's or its pair partner's; the
+// other Rect fields are q's) into the running keys (k1, k2).
+template <bool CAMERA>
+PTQC_HD void classify(Cull& o, int q, Rect R, float c, int qi, F3 P, F3 pq, F3 Pc, const float* r, const float* mu,
+                      const bool* tiny, float rho, const float* d0, CullTrace* tr)
+{
+    const float s = (c - comp(P, R.j)) * r[R.j];                     // plane distance along pq
+    const float Y1 = PTQC_FMA(s, comp(pq, R.k1), comp(Pc, R.k1));    // centred in-plane coords
+    const float Y2 = PTQC_FMA(s, comp(pq, R.k2), comp(Pc, R.k2));
+    const float h1h2 = R.h1 * R.h2;
+    bool out = PTQC_FMA(R.h2, __builtin_fabsf(Y1), -h1h2) > mu[R.j] || PTQC_FMA(R.h1, __builtin_fabsf(Y2), -h1h2) > mu[R.j];
+    if (CAMERA) out = out || (comp(pq, R.j) == 0.0f && __builtin_fabsf(c - comp(P, R.j)) > 1e-3f);   // (5)
+    const float dl = PTQC_FMA(__builtin_fabsf(s), rho, d0[R.j]);
+    // a non-OUT quad whose distance bound (4) does not hold (tiny |pq_j|) gets the lower bound
+    // -inf: it becomes W and is tested exactly, and a second such quad fails the certification
+    const bool cand = !out && (tiny[R.j] || s + dl > kMinHitLo);
+    if (tr) tr->out[q] = out, tr->cand[q] = cand, tr->s[q] = s, tr->dl[q] = tiny[R.j] ? kInf : dl;
+    const float lb = cand ? (tiny[R.j] ? -kInf : s - dl) : kInf;
+    const int32_t key = (fbits(lb) & ~7) | qi;
+    o.k2 = imed3(o.k1, o.k2, key);   // second smallest (k1 <= k2 holds throughout)
+    o.k1 = imin(o.k1, key);
+}
+
+// The distance test alone of quad q at plane c: true when q is certainly no candidate.
+PTQC_HD bool behind(int q, Rect R, float c, F3 P, const float* r, float rho, const float* d0, CullTrace* tr)
+{
+    const float s = (c - comp(P, R.j)) * r[R.j];
+    const float dl = PTQC_FMA(__builtin_fabsf(s), rho, d0[R.j]);
+    const bool ok = !(s + dl > kMinHitLo);
+    if (tr) tr->out[q] = false, tr->cand[q] = !ok, tr->s[q] = s, tr->dl[q] = dl;
+    return ok;
+}
 
 // Classify the six quads for the ray (P, D) with the reference's line direction pq; k = the lane's
 // distance axis (:121-133), dP = P_k, yD = RN(1/D_k).  CAMERA: P is the camera origin (0, 0, 0).
@@ -193,28 +262,39 @@ PTQC_HD Cull cull(F3 P, F3 pq, float dP, float yD, CullTrace* tr = nullptr)
     bool unc = false;   // the origin is outside the domain of (1)
     if (!CAMERA)
         unc = !(__builtin_fabsf(P.x) <= kDomXY && __builtin_fabsf(P.y) <= kDomXY && __builtin_fabsf(Pc.z) <= kDomZ);
-    Cull o{kInf, kInf, -1, false};
-#pragma unroll
-    for (int q = 0; q < PT_NQUADS; ++q) {
-        const Rect R = kRect[q];
-        const float s = (R.c - comp(P, R.j)) * r[R.j];                 // plane distance along pq
-        const float Y1 = PTQC_FMA(s, comp(pq, R.k1), comp(Pc, R.k1));  // centred in-plane coords
-        const float Y2 = PTQC_FMA(s, comp(pq, R.k2), comp(Pc, R.k2));
-        const float h1h2 = R.h1 * R.h2;
-        bool out = PTQC_FMA(R.h2, __builtin_fabsf(Y1), -h1h2) > mu[R.j] ||
-                   PTQC_FMA(R.h1, __builtin_fabsf(Y2), -h1h2) > mu[R.j];
-        if (CAMERA) out = out || (comp(pq, R.j) == 0.0f && __builtin_fabsf(R.c - comp(P, R.j)) > 1e-3f);   // (5)
-        const float dl = PTQC_FMA(__builtin_fabsf(s), rho, d0[R.j]);
-        // a non-OUT quad whose distance bound (4) does not hold (tiny |pq_j|) gets the lower bound
-        // -inf: it becomes W and is tested exactly, and a second such quad fails the certification
-        const bool cand = !out && (tiny[R.j] || s + dl > kMinHitLo);
-        if (tr) tr->out[q] = out, tr->cand[q] = cand, tr->s[q] = s, tr->dl[q] = tiny[R.j] ? kInf : dl;
-        const float lb = cand ? (tiny[R.j] ? -kInf : s - dl) : kInf;
-        const bool nw = lb < o.lb1;
-        o.lb2 = med3(o.lb1, o.lb2, lb);   // second smallest (lb1 <= lb2 holds throughout)
-        o.lb1 = __builtin_fminf(o.lb1, lb);
-        o.W = nw ? q : o.W;
+    Cull o{0x7fffffff, 0x7fffffff, false};
+    // the reference's order: back (0), floor (1), ceiling (2), left (3), right (4), light (5); the
+    // classification's result does not depend on the order (ties in lb: W = the lower index)
+    classify<CAMERA>(o, 0, kRect[0], kRect[0].c, 0, P, pq, Pc, r, mu, tiny, rho, d0, tr);
+    {   // floor / ceiling: the one pq.y runs towards, the other by its distance
+        const bool up = r1 > 0.0f;
+        const int qa = up ? kPairY.q_hi : kPairY.q_lo, qb = up ? kPairY.q_lo : kPairY.q_hi;
+        const float ca = up ? kRect[kPairY.q_hi].c : kRect[kPairY.q_lo].c, cb = up ? kRect[kPairY.q_lo].c : kRect[kPairY.q_hi].c;
+        if (tr) {   // (host check: record under the real quad indices)
+            classify<CAMERA>(o, qa, kRect[qa], ca, qa, P, pq, Pc, r, mu, tiny, rho, d0, tr);
+            if (tiny[1]) classify<CAMERA>(o, qb, kRect[qb], cb, qb, P, pq, Pc, r, mu, tiny, rho, d0, tr);
+            else unc = !behind(qb, kRect[qb], cb, P, r, rho, d0, tr) || unc;
+        } else {
+            classify<CAMERA>(o, kPairY.q_lo, kRect[kPairY.q_lo], ca, qa, P, pq, Pc, r, mu, tiny, rho, d0, nullptr);
+            if (tiny[1]) classify<CAMERA>(o, kPairY.q_lo, kRect[kPairY.q_lo], cb, qb, P, pq, Pc, r, mu, tiny, rho, d0, nullptr);
+            else unc = !behind(kPairY.q_lo, kRect[kPairY.q_lo], cb, P, r, rho, d0, nullptr) || unc;
+        }
     }
+    {   // left / right walls
+        const bool right = r0 > 0.0f;
+        const int qa = right ? kPairX.q_hi : kPairX.q_lo, qb = right ? kPairX.q_lo : kPairX.q_hi;
+        const float ca = right ? kRect[kPairX.q_hi].c : kRect[kPairX.q_lo].c, cb = right ? kRect[kPairX.q_lo].c : kRect[kPairX.q_hi].c;
+        if (tr) {
+            classify<CAMERA>(o, qa, kRect[qa], ca, qa, P, pq, Pc, r, mu, tiny, rho, d0, tr);
+            if (tiny[0]) classify<CAMERA>(o, qb, kRect[qb], cb, qb, P, pq, Pc, r, mu, tiny, rho, d0, tr);
+            else unc = !behind(qb, kRect[qb], cb, P, r, rho, d0, tr) || unc;
+        } else {
+            classify<CAMERA>(o, kPairX.q_lo, kRect[kPairX.q_lo], ca, qa, P, pq, Pc, r, mu, tiny, rho, d0, nullptr);
+            if (tiny[0]) classify<CAMERA>(o, kPairX.q_lo, kRect[kPairX.q_lo], cb, qb, P, pq, Pc, r, mu, tiny, rho, d0, nullptr);
+            else unc = !behind(kPairX.q_lo, kRect[kPairX.q_lo], cb, P, r, rho, d0, nullptr) || unc;
+        }
+    }
+    classify<CAMERA>(o, 5, kRect[5], kRect[5].c, 5, P, pq, Pc, r, mu, tiny, rho, d0, tr);
     o.unc = unc;
     return o;
 }

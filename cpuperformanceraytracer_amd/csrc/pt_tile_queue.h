@@ -23,8 +23,11 @@
 // only grows, so a load that shows it used up is right; without the screening the tail's atomics
 // tripled the launch time).  Victims are visited in a per-wave rotation.
 //
-// All state is lane 0's (the kernels broadcast the tile with readfirstlane); the kernels are built
-// with the atomic optimizer off, so a single-lane atomic needs no wave reduction.
+// The whole wave runs the queue code (uniform control flow): every value is wave-uniform and lives
+// in scalar registers -- held by lane 0 alone they took vector registers across the whole pool
+// loop, which the 96-VGPR budget of the ambient kernel spilled.  Only the counter atomics are
+// issued by one lane (the first active one) and broadcast with readfirstlane; the kernels are
+// built with the atomic optimizer off, so that single-lane atomic needs no wave reduction.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -46,7 +49,7 @@ struct PtTileQueue {
                            const uint32_t* nunits_, uint32_t total_tiles, int wv)
         : base(queue), order(order_), units(units_)
     {
-        nunits = units ? *nunits_ : total_tiles;
+        nunits = units ? __builtin_amdgcn_readfirstlane(*nunits_) : total_tiles;
         ntiles = total_tiles;
         ngroups = gridDim.x < PT_NQUEUES ? gridDim.x : PT_NQUEUES;   // small grids: fewer groups
         qg = blockIdx.x % ngroups;
@@ -61,26 +64,38 @@ struct PtTileQueue {
         const uint32_t slot = g + ngroups * (group_waves(g) + c);
         return slot < nunits ? slot : kNone;
     }
-    __device__ uint32_t unit_lo(uint32_t u) const { return units ? units[u] : u; }
-    __device__ uint32_t unit_hi(uint32_t u) const { return units ? units[u + 1] : u + 1; }
+    __device__ uint32_t unit_lo(uint32_t u) const { return units ? __builtin_amdgcn_readfirstlane(units[u]) : u; }
+    __device__ uint32_t unit_hi(uint32_t u) const { return units ? __builtin_amdgcn_readfirstlane(units[u + 1]) : u + 1; }
     // (defensive: a schedule entry outside the launch's tiles ends the wave instead of faulting)
     __device__ uint32_t tile_at(uint32_t i) const
     {
-        const uint32_t tile = order ? order[i] : i;
+        const uint32_t tile = order ? __builtin_amdgcn_readfirstlane(order[i]) : i;
         return tile < ntiles ? tile : kNone;
     }
 
+    // one returning atomic for the wave (its first active lane), the result broadcast
+    __device__ static uint32_t wave_atomic_add(unsigned int* c)
+    {
+        const uint32_t me = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        uint32_t r = 0;
+        if (me == (uint32_t)__builtin_amdgcn_readfirstlane(me)) r = atomicAdd(c, 1u);
+        return __builtin_amdgcn_readfirstlane(r);
+    }
+    __device__ static uint32_t wave_load(const unsigned int* c)
+    {
+        return __builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
     __device__ uint32_t steal()
     {
         for (uint32_t k = 1; k < ngroups; ++k) {
             const uint32_t g = (qg + 1 + (wave + k - 1) % (ngroups - 1)) % ngroups;
             if ((dead >> g) & 1u) continue;
             unsigned int* const c = base + g * 32u;
-            if (slot_of(g, __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == kNone) {
+            if (slot_of(g, wave_load(c)) == kNone) {
                 dead |= 1u << g;
                 continue;
             }
-            const uint32_t slot = slot_of(g, atomicAdd(c, 1u));
+            const uint32_t slot = slot_of(g, wave_atomic_add(c));
             if (slot != kNone) return slot;
             dead |= 1u << g;
         }
@@ -100,7 +115,7 @@ struct PtTileQueue {
     __device__ uint32_t next()
     {
         if (c_pos >= c_end) {
-            uint32_t u = ((dead >> qg) & 1u) ? kNone : slot_of(qg, atomicAdd(base + qg * 32u, 1u));
+            uint32_t u = ((dead >> qg) & 1u) ? kNone : slot_of(qg, wave_atomic_add(base + qg * 32u));
             if (u == kNone) {
                 dead |= 1u << qg;
                 u = steal();

@@ -583,7 +583,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     constexpr uint32_t kNone = PtTileQueue<kWaves>::kNone;
     PtTileQueue<kWaves> tq(job.queue, job.order, job.units, job.nunits, (uint32_t)ntiles, wv);
     uint32_t tile = kNone, next_tile = kNone;
-    if (lane == 0) tile = tq.first();
+    tile = tq.first();   // (the whole wave: uniform, scalar registers)
     tile = __builtin_amdgcn_readfirstlane(tile);
     while (tile != kNone) {
     const int tcol = ((int)tile % tiles_x) * 8, trow = ((int)tile / tiles_x) * 8;
@@ -867,7 +867,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
             }
         }
         if (DEFER && qn > 0) drain(qn);
-        if (c0 + kChunk >= job.nframes && lane == 0) next_tile = tq.next();   // the last pool is done
+        if (c0 + kChunk >= job.nframes) next_tile = tq.next();   // the last pool is done
         // all radiance of this chunk is in LDS (written by lanes of this wave)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -887,7 +887,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (job.nframes <= 0 && lane == 0) next_tile = tq.next();   // no chunk ran
+    if (job.nframes <= 0) next_tile = tq.next();   // no chunk ran
     if (pvalid) {
         acc_p[0] = acc.x;
         acc_p[cs] = acc.y;

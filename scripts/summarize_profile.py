@@ -27,7 +27,7 @@ src = ROOT / "gpurun_out" / "prof" / tag
 dst = ROOT / "profiles"
 dst.mkdir(exist_ok=True)
 ENV = workload.startswith("c4")
-KERNEL = "pt_render_env_kernel<0, false>" if ENV else "pt_render_kernel<0, false>"
+KERNEL = "pt_render_env_kernel<0, false, false>" if ENV else "pt_render_kernel<0, false, false>"
 if workload.startswith("v4"):
     KERNEL = "pt_v4_kernel<1, 0, false, true>"   # <EQUIRECT, INTERLEAVED, COUNT = false, default-scene literals>
 SUMMARY = "pmc_summary.json" if workload == "c2_1080p" else f"pmc_summary_{workload}.json"

@@ -119,18 +119,19 @@ static void check_ray(F3 P, F3 D, bool camera)
     bool unc = c.unc;
     float fd = PT_SUPER_FAR;
     int fid = -1, fflip = 0;
-    if (c.W >= 0) {
-        fid = c.W;
-        fd = qdist[c.W];
-        fflip = qflip[c.W];
+    const int cW = ptqc::cull_W(c);
+    if (cW >= 0) {
+        fid = cW;
+        fd = qdist[cW];
+        fflip = qflip[cW];
         auto own = [&](int q) { return std::fabs(ptqc::comp(P, ptqc::kRect[q].j) - ptqc::kRect[q].c) < 0.02f; };
-        if (!c.unc && qcode[c.W] != ptqc::kAccepted) ++n_r_wrej, n_r_wrej_own += own(c.W);
-        else if (!c.unc && !(c.lb2 > fd)) {
+        if (!c.unc && qcode[cW] != ptqc::kAccepted) ++n_r_wrej, n_r_wrej_own += own(cW);
+        else if (!c.unc && !ptqc::cull_beyond(c, fd)) {
             ++n_r_block;
             for (int q = 0; q < PT_NQUADS; ++q)
-                if (q != c.W && tr.cand[q] && own(q)) { ++n_r_block_own; break; }
+                if (q != cW && tr.cand[q] && own(q)) { ++n_r_block_own; break; }
         }
-        if (qcode[c.W] != ptqc::kAccepted || !(c.lb2 > fd)) unc = true;
+        if (qcode[cW] != ptqc::kAccepted || !ptqc::cull_beyond(c, fd)) unc = true;
     } else {
         ++n_nocand;
     }
