@@ -234,23 +234,43 @@ static_assert(scene_spheres_disjoint(), "the closest-sphere stage needs pairwise
 #define PT_SPHERE_FORCE_SEQ 0   // test builds: every candidate ray takes the sequential fallback
 #endif
 
+// Which candidate has the largest b, without comparing b's: the spheres' centres lie on one line
+// parallel to x in ascending x (static_assert below), so for two candidates i < j the exact
+// b_i - b_j = (C_j - C_i).D = (x_j - x_i) D.x, and the chords (or the closest approaches, for a
+// candidate the rounded discriminant admits at a tangent) are >= 3 - 1e-4 apart along the ray,
+// far beyond the ~1e-5 rounding of the computed b's: for D.x > 0 the first candidate in index
+// order has the largest b, for D.x < 0 the last one; D.x == 0 admits at most one candidate.
+constexpr bool scene_spheres_on_x_line()
+{
+    for (int i = 1; i < PT_NSPHERES; ++i)
+        if (!(DemofoxScene::sph[i][1] == DemofoxScene::sph[0][1] && DemofoxScene::sph[i][2] == DemofoxScene::sph[0][2] &&
+              DemofoxScene::sph[i][0] > DemofoxScene::sph[i - 1][0]))
+            return false;
+    return true;
+}
+static_assert(scene_spheres_on_x_line(), "the closest-sphere order rule needs collinear spheres in ascending x");
+
 template <class SC>
 __device__ __forceinline__ void spheres_closest(V3 P, V3 D, float& best, int& id, int& flag)
 {
-    float bmax = -__builtin_huge_valf(), dsel = 0.0f;
+    float bsel = 0.0f, dsel = 0.0f;
     int ksel = -1;
+    const bool first = D.x > 0.0f;   // take the first candidate (else the last)
+    bool found = false;
 #pragma unroll
     for (int s = 0; s < PT_NSPHERES; ++s) {   // :150-164 exactly
         const V3 m = sub(P, v3(SC::sph[s][0], SC::sph[s][1], SC::sph[s][2]));
         const float b = dot(m, D);
         const float c = dot(m, m) - SC::sph_r2[s];
         const float discr = b * b - c;
-        const bool early = (c > 0.0f && b > 0.0f) || discr < 0.0f;
-        const bool take = !early && b > bmax;
-        bmax = take ? b : bmax;
+        const bool cand = !((c > 0.0f && b > 0.0f) || discr < 0.0f);
+        const bool take = cand && !(found && first);
+        found = found || cand;
+        bsel = take ? b : bsel;
         dsel = take ? discr : dsel;
         ksel = take ? s : ksel;
     }
+    const float bmax = bsel;
     bool seq = false;
     if (ksel >= 0) {
         const float sq = sqrt_x(dsel);
@@ -462,7 +482,9 @@ __device__ __forceinline__ V3 hit_normal(const PtLdsPrim& pr, const Hit& h, V3 P
         return h.flag ? mul(n, -1.0f) : n;                              // :71
     }
     const V3 c = sub(add(P, mul(D, h.best)), v3(pr.nx, pr.ny, pr.nz));  // :179
-    return mul(normalize(c), h.flag ? -1.0f : 1.0f);
+    // normalize(c) * (inside ? -1 : 1): (c_i * g) * -1 == c_i * -g exactly, so the sign goes on g
+    const float g = rcp_x(sqrt_x(dot(c, c)));
+    return mul(c, h.flag ? -g : g);
 }
 
 // Miss radiance of the textured variant: EquirectangularTextureSample (texture.cpp:101-139), the

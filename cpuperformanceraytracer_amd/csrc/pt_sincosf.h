@@ -11,8 +11,9 @@
 //
 // Verified exhaustively on every f32 in [0, 2*pi*1.0001] against the host libm in
 // tests/test_sincosf.py (tests/native/check_sincosf.cpp compiles THIS header for the host).
-// Domain: |y| < 120 (the reference's argument never leaves [0, 2*pi]; larger |y| is rejected by
-// the caller's construction, not handled here).
+// Domain: |y| < 120, y != -0 (the reference's argument never leaves [+0, 2*pi]; larger |y| is
+// excluded by the caller's construction, not handled here, and for -0 glibc's sinf returns -0,
+// the straight-line form below +0).
 #pragma once
 #include <stdint.h>
 
@@ -51,21 +52,19 @@ PT_HD uint32_t f32_bits(float f)
 }
 
 // Both results of one argument (the reduction is shared; each output equals the separate call).
+// Straight-line form of glibc's sincosf for |y| < 120 (same results, no branches):
+//  * |y| < 2^-12 (glibc: sinf = y, cosf = 1) and 2^-12 <= |y| < 0.75 (glibc: no reduction) run
+//    the reduction and polynomials too: below 0.75 the reduction yields n = 0 and x = y exactly,
+//    and below 2^-12 the polynomials round to y and 1 (|y^3/6| and y^2/2 stay below half an ulp);
+//  * the sine polynomial of glibc's x * sign[n & 3] is evaluated on x and its f32 result negated:
+//    every term of the odd polynomial changes sign exactly (round-to-nearest is sign-symmetric).
+// Checked exhaustively against the host libm (tests/test_sincosf.py).
 PT_HD void sincosf_glibc(float y, float* s_out, float* c_out)
 {
-    const uint32_t top = (f32_bits(y) >> 20) & 0x7ffu;   // abstop12
-    if (top < 0x398u) {                                   // |y| < 2^-12: sinf = y, cosf = 1
-        *s_out = y;
-        *c_out = 1.0f;
-        return;
-    }
     double x = (double)y;
-    int n = 0;
-    if (top >= 0x3f4u) {                                  // |y| >= 0.75 (abstop12(pio4f)): reduce
-        const double r = x * kHpiInv;
-        n = ((int32_t)r + 0x800000) >> 24;
-        x = __builtin_fma(-(double)n, kHpi, x);
-    }
+    const double r = x * kHpiInv;
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    x = __builtin_fma(-(double)n, kHpi, x);
     // The two polynomial constants that end up as fma addends must sit in VGPRs; writing them with
     // inline v_mov makes the device code materialise them here (two v_mov each) instead of
     // hoisting them out of the caller's loop, where the register allocator spilled them to scratch.
@@ -80,31 +79,31 @@ PT_HD void sincosf_glibc(float y, float* s_out, float* c_out)
 #else
     const double s2 = kS2, c3 = kC3;
 #endif
-    const double sg = ((n + 1) & 2) ? -1.0 : 1.0;        // sign[n & 3] = {1,-1,-1,1}
-    const double xs = x * sg;
     const double x2 = x * x;
-    // sine polynomial (sinf_poly, even n)
-    const double x3 = xs * x2;
+    // sine polynomial (sinf_poly, even n), on x; its sign sign[n & 3] = {1,-1,-1,1} applied below
+    const double x3 = x * x2;
     const double s1 = __builtin_fma(x2, kS3, s2);
     const double x7 = x3 * x2;
-    const double ss = __builtin_fma(x3, kS1, xs);
+    const double ss = __builtin_fma(x3, kS1, x);
     const float sp = (float)__builtin_fma(x7, s1, ss);
-    // cosine polynomial (sinf_poly, odd n), table selected by n & 2
+    // cosine polynomial (sinf_poly, odd n), table selected by n & 2 (negated)
     const double x4 = x2 * x2;
     const double c2 = __builtin_fma(x2, kC4, c3);
     const double c1 = __builtin_fma(x2, kC1, kC0);
     const double x6 = x4 * x2;
     const double cc = __builtin_fma(x4, kC2, c1);
-    float cp = (float)__builtin_fma(x6, c2, cc);
-    if (n & 2) cp = -cp;
+    const float cp = (float)__builtin_fma(x6, c2, cc);
+    const uint32_t sps = f32_bits(sp) ^ ((uint32_t)((n + 1) & 2) << 30);
+    const uint32_t cps = f32_bits(cp) ^ ((uint32_t)(n & 2) << 30);
     // sinf uses poly(n), cosf uses poly(n ^ 1)
-    if (n & 1) {
-        *s_out = cp;
-        *c_out = sp;
-    } else {
-        *s_out = sp;
-        *c_out = cp;
-    }
+    const uint32_t sb = (n & 1) ? cps : sps, cb = (n & 1) ? sps : cps;
+#if defined(__HIPCC__)
+    *s_out = __builtin_bit_cast(float, sb);
+    *c_out = __builtin_bit_cast(float, cb);
+#else
+    __builtin_memcpy(s_out, &sb, 4);
+    __builtin_memcpy(c_out, &cb, 4);
+#endif
 }
 
 }  // namespace pt

@@ -542,9 +542,15 @@ __device__ __forceinline__ size_t out_index(const PtV4Job& j, int x, int r)   //
 #ifdef PT_V4_WAVES   // A/B builds: force the occupancy (waves per SIMD)
 #define PT_V4_OCC __attribute__((amdgpu_waves_per_eu(PT_V4_WAVES, PT_V4_WAVES)))
 #else
-#define PT_V4_OCC
+// render instances: at least 5 waves per SIMD (<= 96 VGPRs; the exact-exp instance needs 97
+// otherwise and compiles spill-free at 96); the diagnostic COUNT instances are left unconstrained
+#define PT_V4_OCC __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : 5)))
 #endif
-template <int ENV, int LAYOUT, bool COUNT, bool DEF>
+// FEXP: USE_FAST_APPROXIMATE_EXP as a compile-time switch (1 fast, 0 exact) for the render
+// instances -- the exact expf's registers in the Beer branch would otherwise raise the kernel from
+// 93 to 97 VGPRs, i.e. from 5 to 4 waves per SIMD (0.410 -> 0.451 ms at 1080p equirect) -- and as
+// the runtime flag (2) for the diagnostic COUNT instances.
+template <int ENV, int LAYOUT, bool COUNT, bool DEF, int FEXP>
 __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
 {
     __shared__ float s_col[kWaves][kChunk * 64 * 3];
@@ -700,7 +706,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                     }
                     const PtV4Mat& M = s_mat[h.mat];
                     if (h.inside) {   // :797, Beer's law
-                        if (job.fast_exp)   // USE_FAST_APPROXIMATE_EXP 1 (:783-784)
+                        if (FEXP == 2 ? job.fast_exp != 0 : FEXP == 1)   // USE_FAST_APPROXIMATE_EXP 1 (:783-784)
                             T = mul(T, v3(approx_exp(-M.refr_color[0] * h.dist), approx_exp(-M.refr_color[1] * h.dist),
                                           approx_exp(-M.refr_color[2] * h.dist)));
                         else                // 0 (:785-787): exp_ps -> glibc-exact expf (pt_libmf.h)
@@ -924,11 +930,13 @@ hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool 
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), block, 0, st, j, sc);
     };
     if (j.default_scene) {
-        if (count) go(pt_v4_kernel<ENV, LAYOUT, true, true>);
-        else go(pt_v4_kernel<ENV, LAYOUT, false, true>);
+        if (count) go(pt_v4_kernel<ENV, LAYOUT, true, true, 2>);
+        else if (j.fast_exp) go(pt_v4_kernel<ENV, LAYOUT, false, true, 1>);
+        else go(pt_v4_kernel<ENV, LAYOUT, false, true, 0>);
     } else {
-        if (count) go(pt_v4_kernel<ENV, LAYOUT, true, false>);
-        else go(pt_v4_kernel<ENV, LAYOUT, false, false>);
+        if (count) go(pt_v4_kernel<ENV, LAYOUT, true, false, 2>);
+        else if (j.fast_exp) go(pt_v4_kernel<ENV, LAYOUT, false, false, 1>);
+        else go(pt_v4_kernel<ENV, LAYOUT, false, false, 0>);
     }
     return hipGetLastError();
 }

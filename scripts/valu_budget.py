@@ -31,12 +31,12 @@ FOUR = re.compile(r"^v_(cmp|cmpx|cndmask|max|min|med3|bfi|mul_lo_u32|mul_hi|cvt|
 TRANS = re.compile(r"^v_(rcp|rsq|sqrt|sin|cos|exp|log)")
 
 
-def build(defines) -> Path:
+def build(defines, src="pt_kernel.hip") -> Path:
     obj, co = Path("/tmp/_vb.o"), Path("/tmp/_vb.co")
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
            "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero", "-mllvm",
            "-amdgpu-atomic-optimizer-strategy=None", "-fno-slp-vectorize", f"-I{ROOT / 'include'}", f"-I{CSRC}",
-           "--cuda-device-only", "-c", "-g", *[f"-D{d}" for d in defines], str(CSRC / "pt_kernel.hip"), "-o", str(obj)]
+           "--cuda-device-only", "-c", "-g", *[f"-D{d}" for d in defines], str(CSRC / src), "-o", str(obj)]
     subprocess.run(cmd, check=True, capture_output=True)
     subprocess.run([str(LLVM / "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={obj}",
                     "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
@@ -71,9 +71,13 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", default="_ZN12_GLOBAL__N_116pt_render_kernelILi0ELb0ELb0EEEv5PtJob")
     ap.add_argument("--defines", nargs="*", default=[])
+    ap.add_argument("--src", default="pt_kernel.hip")
+    ap.add_argument("--body", default="render_body", help="the function whose callees are the phases")
+    ap.add_argument("--need", nargs="*", default=["trace<*, false,", "random_unit_vector"],
+                    help="function-name prefixes the pool loop must hold ('*' = anything)")
     ap.add_argument("--dump", default=None, help="print the instructions of the phases starting with this")
     a = ap.parse_args()
-    co = build(a.defines)
+    co = build(a.defines, a.src)
     dis = subprocess.run([str(LLVM / "llvm-objdump"), "-d", str(co), f"--disassemble-symbols={a.kernel}"],
                          capture_output=True, text=True, check=True).stdout
     ins = []   # (addr, op, text, branch target)
@@ -106,21 +110,28 @@ def main() -> None:
         return any(any(pred(f) for f, _ in frames[j]) for j in range(lo, hi + 1))
 
     # the pool iteration: the smallest loop holding phase B's trace AND the new direction
-    pool = min((l for l in loops if holds(*l, lambda f: f.startswith("trace<") and ", false," in f)
-                and holds(*l, lambda f: f.startswith("random_unit_vector"))), key=lambda l: l[1] - l[0])
+    pats = [re.compile(re.escape(n).replace(r"\*", ".*")) for n in a.need]
+    pool = min((l for l in loops if all(holds(*l, lambda f, r=r: r.match(f) is not None) for r in pats)),
+               key=lambda l: l[1] - l[0])
+    # rarely taken sub-paths, marked "(fallback)": the sequential sphere tests, the six exact quad
+    # tests, and the cull's far-wall rectangle for rays nearly parallel to a wall pair
+    qc = (CSRC / "pt_quadcull.h").read_text().splitlines()
+    tiny_lines = {str(i + 1) for i, l in enumerate(qc) if "if (tiny[" in l and "classify" in l}
     counts = collections.defaultdict(collections.Counter)
     for j in range(pool[0], pool[1] + 1):
         fr = frames[j]
         names = [f for f, _ in fr]
-        k = next((i for i, f in enumerate(names) if f.startswith("render_body")), len(names))
+        k = next((i for i, f in enumerate(names) if f.startswith(a.body)), len(names))
         if k == 0:
-            ph = "render_body:" + fr[0][1].rsplit(":", 2)[-2]   # its own line
+            ph = a.body + ":" + fr[0][1].rsplit(":", 2)[-2]   # its own line
         else:
             ph = short(names[k - 1])
             if ph in ("trace", "random_unit_vector") and k >= 2:
                 ph += "/" + short(names[k - 2])
-            if ph == "trace/quads_exact" or ph == "trace/sphere_test":
-                ph += " (fallback)"
+            if ph == "trace/quads_exact" or ph == "trace/sphere_test" or "sphere_test" in names[:k]:
+                ph = ph + " (fallback)" if ph.endswith("sphere_test") or ph.endswith("quads_exact") else "trace/sphere_test (fallback)"
+            if ph == "trace/cull" and any(f.startswith("cull") and ln.rsplit(":", 2)[-2] in tiny_lines for f, ln in fr):
+                ph = "trace/cull (tiny-pq branch)"
         counts[ph][classify(ins[j][1])] += 1
         if a.dump and ph.startswith(a.dump):
             print(f"{ph[:28]:28s} {ins[j][2].split('//')[0]}")

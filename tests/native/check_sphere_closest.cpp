@@ -11,7 +11,9 @@
 //            cc = fma(-r, r, dot(m, m)), discr = fma(b, b, -cc), the v4 InitializeScene spheres.
 // For every ray the sequential tests (in order, strict '<' against a running best that starts at a
 // random "quad" distance) and the closest-sphere stage must agree on (distance bits, sphere,
-// inside) whenever the stage does not fall back.  Ray families: random origins and directions,
+// inside) whenever the stage does not fall back, and the candidate with the largest b must be the
+// first (D.x > 0) or last (else) candidate in index order -- the rule both kernels use instead of
+// comparing b's (the spheres of both scenes lie on one x line).  Ray families: random origins and directions,
 // rays aimed between two neighbouring spheres (grazing both), origins just off a sphere surface
 // (either side), origins inside a sphere.
 //
@@ -148,7 +150,7 @@ void check(F3 P, F3 D, const float (*sph)[4], int n)
         cands += sphere_pre<V4>(P, D, sph[k], b, discr);
     }
     n_multi += cands > 1;
-    if (V4) {   // pt_v4.hip PT_V4_SPHERE_ORDER: the argmax of b is the first / last candidate by sign(D.x)
+    {   // both kernels: the argmax of b is the first / last candidate by sign(D.x) (collinear spheres)
         float bmax = -INFINITY;
         int karg = -1;
         uint32_t cand = 0;
