@@ -267,8 +267,10 @@ PTQC_HD Cull cull(F3 P, F3 pq, float dP, float yD, CullTrace* tr = nullptr)
     // classification's result does not depend on the order (ties in lb: W = the lower index)
     classify<CAMERA>(o, 0, kRect[0], kRect[0].c, 0, P, pq, Pc, r, mu, tiny, rho, d0, tr);
     {   // floor / ceiling: the one pq.y runs towards, the other by its distance
-        const bool up = r1 > 0.0f;
-        const int qa = up ? kPairY.q_hi : kPairY.q_lo, qb = up ? kPairY.q_lo : kPairY.q_hi;
+        static_assert(kPairY.q_hi == kPairY.q_lo + 1, "y pair");
+        const uint32_t neg = (uint32_t)fbits(r1) >> 31;   // pq.y < 0
+        const bool up = neg == 0;
+        const int qa = kPairY.q_hi - (int)neg, qb = kPairY.q_lo + (int)neg;
         const float ca = up ? kRect[kPairY.q_hi].c : kRect[kPairY.q_lo].c, cb = up ? kRect[kPairY.q_lo].c : kRect[kPairY.q_hi].c;
         if (tr) {   // (host check: record under the real quad indices)
             classify<CAMERA>(o, qa, kRect[qa], ca, qa, P, pq, Pc, r, mu, tiny, rho, d0, tr);
@@ -280,10 +282,11 @@ PTQC_HD Cull cull(F3 P, F3 pq, float dP, float yD, CullTrace* tr = nullptr)
             else unc = !behind(kPairY.q_lo, kRect[kPairY.q_lo], cb, P, r, rho, d0, nullptr) || unc;
         }
     }
-    {   // left / right walls
-        const bool right = r0 > 0.0f;
-        const int qa = right ? kPairX.q_hi : kPairX.q_lo, qb = right ? kPairX.q_lo : kPairX.q_hi;
-        const float ca = right ? kRect[kPairX.q_hi].c : kRect[kPairX.q_lo].c, cb = right ? kRect[kPairX.q_lo].c : kRect[kPairX.q_hi].c;
+    {   // left / right walls (planes x = -+12.5: the forward one is copysign(12.5, pq.x), by bits)
+        static_assert(kRect[kPairX.q_lo].c == -kRect[kPairX.q_hi].c && kPairX.q_hi == kPairX.q_lo + 1, "x pair");
+        const uint32_t neg = (uint32_t)fbits(r0) >> 31;   // pq.x < 0 (r0 = +-inf for pq.x = +-0)
+        const int qa = kPairX.q_hi - (int)neg, qb = kPairX.q_lo + (int)neg;
+        const float ca = __builtin_bit_cast(float, fbits(kRect[kPairX.q_hi].c) | (int32_t)(neg << 31)), cb = -ca;
         if (tr) {
             classify<CAMERA>(o, qa, kRect[qa], ca, qa, P, pq, Pc, r, mu, tiny, rho, d0, tr);
             if (tiny[0]) classify<CAMERA>(o, qb, kRect[qb], cb, qb, P, pq, Pc, r, mu, tiny, rho, d0, tr);
@@ -309,13 +312,14 @@ PTQC_HD int quad_exact(F3 P, F3 pq, F3 a, F3 b, F3 c, F3 d, float ak, float bk, 
 {
     // straight-line: every lane evaluates every step (a rejected lane's later values are unused;
     // its weight sum is replaced by 1 so the reciprocal stays on its fast path)
-    const F3 pa = sub(a, P), pb = sub(b, P), pc = sub(c, P), pd = sub(d, P);
+    const F3 pa = sub(a, P), pc = sub(c, P);
     const F3 m = cross(pc, pq);                        // :90
     float v = dot(pa, m);                              // :91
     const bool t1 = v >= 0.0f;                         // :93 triangle a,b,c (else a,c,d)
-    const float tu = dot(sel(t1, pb, pd), m);          // :96 -dot(pb, m) | :109 dot(pd, m)
+    const F3 pe = sub(sel(t1, b, d), P);               // pb | pd (the same subtraction)
+    const float tu = dot(pe, m);                       // :96 -dot(pb, m) | :109 dot(pd, m)
     const float u = t1 ? -tu : tu;
-    const float w = dot(cross(pq, sel(t1, pb, pa)), sel(t1, pa, pd));   // :98 | :111 ScalarTriple
+    const float w = dot(cross(pq, sel(t1, pe, pa)), sel(t1, pa, pe));   // :98 | :111 ScalarTriple
     v = t1 ? v : -v;                                   // :113
     const bool inside = !(u < 0.0f || w < 0.0f);       // :97,99,110,112
     const float denom = PTQC_RCP_EXACT(inside ? (u + v) + w : 1.0f);   // :100 / :114

@@ -31,12 +31,13 @@ FOUR = re.compile(r"^v_(cmp|cmpx|cndmask|max|min|med3|bfi|mul_lo_u32|mul_hi|cvt|
 TRANS = re.compile(r"^v_(rcp|rsq|sqrt|sin|cos|exp|log)")
 
 
-def build(defines, src="pt_kernel.hip") -> Path:
+def build(defines, src="pt_kernel.hip", csrc=None) -> Path:
+    csrc = Path(csrc) if csrc else CSRC
     obj, co = Path("/tmp/_vb.o"), Path("/tmp/_vb.co")
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
            "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero", "-mllvm",
-           "-amdgpu-atomic-optimizer-strategy=None", "-fno-slp-vectorize", f"-I{ROOT / 'include'}", f"-I{CSRC}",
-           "--cuda-device-only", "-c", "-g", *[f"-D{d}" for d in defines], str(CSRC / src), "-o", str(obj)]
+           "-amdgpu-atomic-optimizer-strategy=None", "-fno-slp-vectorize", f"-I{csrc.parents[1] / 'include'}", f"-I{csrc}",
+           "--cuda-device-only", "-c", "-g", *[f"-D{d}" for d in defines], str(csrc / src), "-o", str(obj)]
     subprocess.run(cmd, check=True, capture_output=True)
     subprocess.run([str(LLVM / "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={obj}",
                     "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
@@ -72,12 +73,14 @@ def main() -> None:
     ap.add_argument("--kernel", default="_ZN12_GLOBAL__N_116pt_render_kernelILi0ELb0ELb0EEEv5PtJob")
     ap.add_argument("--defines", nargs="*", default=[])
     ap.add_argument("--src", default="pt_kernel.hip")
+    ap.add_argument("--csrc", default=None, help="another tree's csrc/ (e.g. a git worktree of an earlier round)")
     ap.add_argument("--body", default="render_body", help="the function whose callees are the phases")
     ap.add_argument("--need", nargs="*", default=["trace<*, false,", "random_unit_vector"],
                     help="function-name prefixes the pool loop must hold ('*' = anything)")
+    ap.add_argument("--groups", action="store_true", help="also print the grouped markdown table (DESIGN.md §3)")
     ap.add_argument("--dump", default=None, help="print the instructions of the phases starting with this")
     a = ap.parse_args()
-    co = build(a.defines, a.src)
+    co = build(a.defines, a.src, a.csrc)
     dis = subprocess.run([str(LLVM / "llvm-objdump"), "-d", str(co), f"--disassemble-symbols={a.kernel}"],
                          capture_output=True, text=True, check=True).stdout
     ins = []   # (addr, op, text, branch target)
@@ -115,9 +118,11 @@ def main() -> None:
                key=lambda l: l[1] - l[0])
     # rarely taken sub-paths, marked "(fallback)": the sequential sphere tests, the six exact quad
     # tests, and the cull's far-wall rectangle for rays nearly parallel to a wall pair
-    qc = (CSRC / "pt_quadcull.h").read_text().splitlines()
+    qcp = (Path(a.csrc) if a.csrc else CSRC) / "pt_quadcull.h"
+    qc = qcp.read_text().splitlines() if qcp.exists() else []
     tiny_lines = {str(i + 1) for i, l in enumerate(qc) if "if (tiny[" in l and "classify" in l}
     counts = collections.defaultdict(collections.Counter)
+    cross = collections.defaultdict(collections.Counter)   # cross-cutting: exact-math sequences, f64
     for j in range(pool[0], pool[1] + 1):
         fr = frames[j]
         names = [f for f, _ in fr]
@@ -133,6 +138,12 @@ def main() -> None:
             if ph == "trace/cull" and any(f.startswith("cull") and ln.rsplit(":", 2)[-2] in tiny_lines for f, ln in fr):
                 ph = "trace/cull (tiny-pq branch)"
         counts[ph][classify(ins[j][1])] += 1
+        if "(fallback)" not in ph and "branch)" not in ph:
+            if any(short(f) in ("rcp_x", "sqrt_x", "div_x", "rcp_rn", "sqrt_rn", "div_rn", "sqrt_guarded", "rcp_guarded",
+                                "div_guarded") for f in names):
+                cross["exact rcp / sqrt / div sequences (pt_exactmath.h)"][classify(ins[j][1])] += 1
+            if "_f64" in ins[j][1] or ins[j][1].startswith("v_cvt_f32_f64") or ins[j][1].startswith("v_cvt_f64"):
+                cross["f64 instructions (all in sincosf_glibc)"][classify(ins[j][1])] += 1
         if a.dump and ph.startswith(a.dump):
             print(f"{ph[:28]:28s} {ins[j][2].split('//')[0]}")
     # fold render_body's own lines into one bucket per source line range
@@ -152,6 +163,44 @@ def main() -> None:
         tot.update(c)
         print(f"{ph[:34]:34s}" + "".join(f"{c[k]:10d}" for k in cols) + f"{valu(c):7d}{cyc(c):7d}")
     print(f"{'total':34s}" + "".join(f"{tot[k]:10d}" for k in cols) + f"{valu(tot):7d}{cyc(tot):7d}")
+    if not a.groups:
+        return
+    groups = [
+        ("cull classification (pt_quadcull.h)", lambda p: p == "trace/cull"),
+        ("exact TestQuadTrace of the cull's W", lambda p: p == "trace/quad_exact"),
+        ("closest-sphere stage", lambda p: p == "trace/spheres_closest"),
+        ("trace glue (distance axis, W's vertex rows, result)", lambda p: p.startswith("trace") and "(" not in p
+         and p not in ("trace/cull", "trace/quad_exact", "trace/spheres_closest")),
+        ("glibc-exact sincosf (f64)", lambda p: p == "random_unit_vector/sincosf_glibc"),
+        ("RNG (wang_hash, Randomf3201, seed)", lambda p: p in ("random_unit_vector/randomf", "seed_int")),
+        ("unit vector + new direction (sqrt, normalize)", lambda p: p in ("random_unit_vector", "random_unit_vector/sqrt_x",
+                                                                          "normalize", "add")),
+        ("shading (hit normal, emissive, albedo, origin)", lambda p: p in ("hit_normal", "mulv", "mul")),
+        ("pool bookkeeping (refill, slots, ballots)", lambda p: p.startswith(a.body) or p.startswith("__")),
+    ]
+    main = collections.Counter()
+    print("\n| phase | VALU | of which 4-cycle | transcendental | issue cycles |\n|---|---|---|---|---|")
+    seen = set()
+    for name, pred in groups:
+        c = collections.Counter()
+        for ph in counts:
+            if pred(ph) and "(fallback)" not in ph and "branch)" not in ph:
+                c.update(counts[ph]); seen.add(ph)
+        main.update(c)
+        print(f"| {name} | {valu(c)} | {c['valu_4cyc']} | {c['valu_trans']} | {cyc(c)} |")
+    rest = collections.Counter()
+    for ph in counts:
+        if ph not in seen and "(fallback)" not in ph and "branch)" not in ph:
+            rest.update(counts[ph])
+    if valu(rest):
+        print(f"| other | {valu(rest)} | {rest['valu_4cyc']} | {rest['valu_trans']} | {cyc(rest)} |")
+    main.update(rest)
+    print(f"| **main path per iteration** | **{valu(main)}** | **{main['valu_4cyc']}** | **{main['valu_trans']}** | **{cyc(main)}** |")
+    for ph in sorted(p for p in counts if "(fallback)" in p or "branch)" in p):
+        c = counts[ph]
+        print(f"| rare: {ph} | {valu(c)} | {c['valu_4cyc']} | {c['valu_trans']} | {cyc(c)} |")
+    for name, c in cross.items():
+        print(f"| cross-cut: {name} | {valu(c)} | {c['valu_4cyc']} | {c['valu_trans']} | {cyc(c)} |")
 
 
 if __name__ == "__main__":
