@@ -27,14 +27,21 @@ src = ROOT / "gpurun_out" / "prof" / tag
 dst = ROOT / "profiles"
 dst.mkdir(exist_ok=True)
 ENV = workload.startswith("c4")
-KERNEL = "pt_render_env_kernel<0, false, false>" if ENV else "pt_render_kernel<0, false, false>"
+# Family prefix of the timed (COUNT = false) instance; the remaining template arguments (MULTI for
+# launches that chain chunks, v4's exp switch) are resolved below to the instance with the most
+# kernel-trace time.
+KERNEL = "pt_render_env_kernel<0, false," if ENV else "pt_render_kernel<0, false,"
 if workload.startswith("v4"):
-    KERNEL = "pt_v4_kernel<1, 0, false, true>"   # <EQUIRECT, INTERLEAVED, COUNT = false, default-scene literals>
+    KERNEL = "pt_v4_kernel<1, 0, false, true,"   # <EQUIRECT, INTERLEAVED, COUNT = false, default-scene literals, FEXP>
 SUMMARY = "pmc_summary.json" if workload == "c2_1080p" else f"pmc_summary_{workload}.json"
 
 stats = glob.glob(str(src / "trace" / "**" / "*kernel_stats.csv"), recursive=True)
 if stats:
     shutil.copy(stats[0], dst / f"{tag}_kernel_stats.csv")
+    rows = [r for r in csv.DictReader(open(stats[0])) if KERNEL in r["Name"]]
+    if rows:
+        best = max(rows, key=lambda r: float(r["TotalDurationNs"]))["Name"]
+        KERNEL = best[best.index(KERNEL):best.index(">", best.index(KERNEL)) + 1]
 agg = collections.defaultdict(list)
 for f in glob.glob(str(src / "**" / "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
