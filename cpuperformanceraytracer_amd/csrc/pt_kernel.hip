@@ -41,6 +41,7 @@
 #define PT_IT_SQRT(x) pt::sqrt_guarded(x)
 #include "pt_invtrig.h"
 #include "pt_tile_queue.h"
+#include "pt_wave.h"
 #include <math.h>
 #include <algorithm>
 
@@ -72,6 +73,14 @@ __device__ __forceinline__ float rcp_x(float x)
     if (__builtin_expect(!(ax >= 0x1p-125f && ax <= 0x1p125f), 0)) r = 1.0f / x;
     return r;
 }
+// RN(1/x) for an x that is >= 0 (or NaN) and provably <= 2^125: only the lower end of rcp_rn's range
+// can fail (0, denormals), so one compare guards it.
+__device__ __forceinline__ float rcp_x_nonneg(float x)
+{
+    float r = pt::rcp_rn(x);
+    if (__builtin_expect(!(x >= 0x1p-125f), 0)) r = 1.0f / x;
+    return r;
+}
 // a / b with y = rcp_x(b) and b normal in [2^-125, 2^125]: exact whenever a/b is normal and
 // |a| < 2^124; callers only use it where any other quotient is discarded by the reference's
 // comparisons (see quad_test) or cannot occur (camera: 0 <= a <= 2^24).
@@ -80,14 +89,15 @@ __device__ __forceinline__ float div_x(float a, float b, float y) { return pt::d
 }  // namespace
 #define PTQC_HD __device__ __forceinline__
 #define PTQC_RCP_APPROX(x) pt::rcp_approx(x)
-#define PTQC_RCP_EXACT(x) rcp_x(x)
+#define PTQC_RCP_EXACT(x) rcp_x_nonneg(x)   // quad_exact's weight sum: >= 0 and <= 3 x 9.2e3 (pt_quadcull.h)
 #define PTQC_DIV_EXACT(a, b, y) div_x((a), (b), (y))
 #define PTQC_FMA(a, b, c) __builtin_fmaf((a), (b), (c))
 #include "pt_quadcull.h"
 namespace {
 
-// mathlib.h:750   normalize = v * (1 / sqrt(dot(v, v)))
-__device__ __forceinline__ V3 normalize(V3 v) { return mul(v, rcp_x(sqrt_x(dot(v, v)))); }
+// mathlib.h:750   normalize = v * (1 / sqrt(dot(v, v))).  Its arguments here are n + u (unit normal +
+// unit vector: |v| <= 2) and the camera's (tx, ty, cam_dist): sqrt(dot) <= 2^125, and >= 0.
+__device__ __forceinline__ V3 normalize(V3 v) { return mul(v, rcp_x_nonneg(sqrt_x(dot(v, v)))); }
 
 // scalar.cpp:27-35 (logical shifts, wrapping u32)
 __device__ __forceinline__ uint32_t wang_hash(uint32_t& s)
@@ -287,11 +297,11 @@ __device__ __forceinline__ void spheres_closest(V3 P, V3 D, float& best, int& id
             seq = true;
         }
     }
-    if (__builtin_expect(__any(seq), 0)) {
-        if (seq) {
+    // (a divergent branch: s_cbranch_execz skips it for the whole wave when no lane needs it, with
+    // no VALU vote)
+    if (__builtin_expect(seq, 0)) {
 #pragma unroll
-            for (int k = 0; k < PT_NSPHERES; ++k) sphere_test<SC>(k, P, D, best, id, flag);
-        }
+        for (int k = 0; k < PT_NSPHERES; ++k) sphere_test<SC>(k, P, D, best, id, flag);
     }
 }
 
@@ -415,7 +425,10 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, 
     const int axis = fabsf(D.x) > 0.1f ? 0 : (fabsf(D.y) > 0.1f ? 1 : 2);
     const float dP = axis == 0 ? P.x : (axis == 1 ? P.y : P.z);
     const float dD = axis == 0 ? D.x : (axis == 1 ? D.y : D.z);
-    const float yD = rcp_x(dD);
+    // |dD| is in [0.1, 1.0001] (or NaN), so RN(1/dD) needs no range guard: D is normalize(v) of a
+    // non-zero v (a unit vector within 1e-6; v = 0 gives NaN, and every test of a NaN ray fails as
+    // in the reference), and axis 2 is taken only when |D.x|, |D.y| <= 0.1, i.e. |D.z| > 0.98
+    const float yD = pt::rcp_rn(dD);
     Hit h{PT_SUPER_FAR, -1, 0, 0};
     // classify the six quads cheaply, test the one candidate W exactly (pt_quadcull.h); a ray whose
     // result is not certified runs the six exact tests (wave-uniform branch, rare).  Then the
@@ -459,11 +472,9 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, 
         h.id = W;
         h.flag = fl ? 1 : 0;
     }
-    if (__any(unc)) {
-        if (unc) {
-            h = Hit{PT_SUPER_FAR, -1, 0, 1};
-            quads_exact<SC, QV>(s_axis, P, D, pq, axis, dP, dD, yD, h);
-        }
+    if (__builtin_expect(unc, 0)) {   // (divergent: skipped by s_cbranch_execz when no lane needs it)
+        h = Hit{PT_SUPER_FAR, -1, 0, 1};
+        quads_exact<SC, QV>(s_axis, P, D, pq, axis, dP, dD, yD, h);
     }
     if (SPH_CLOSEST) {
         spheres_closest<SC>(P, D, h.best, h.id, h.flag);
@@ -482,8 +493,12 @@ __device__ __forceinline__ V3 hit_normal(const PtLdsPrim& pr, const Hit& h, V3 P
         return h.flag ? mul(n, -1.0f) : n;                              // :71
     }
     const V3 c = sub(add(P, mul(D, h.best)), v3(pr.nx, pr.ny, pr.nz));  // :179
-    // normalize(c) * (inside ? -1 : 1): (c_i * g) * -1 == c_i * -g exactly, so the sign goes on g
-    const float g = rcp_x(sqrt_x(dot(c, c)));
+    // normalize(c) * (inside ? -1 : 1): (c_i * g) * -1 == c_i * -g exactly, so the sign goes on g.
+    // c is the hit point minus the centre, |c| = the radius (3) up to rounding: the radicand and the
+    // divisor are far inside the fast paths' ranges, no guard
+    static_assert(DemofoxScene::sph[0][3] == 3.0f && DemofoxScene::sph[1][3] == 3.0f && DemofoxScene::sph[2][3] == 3.0f,
+                  "the unguarded sphere normal assumes radius 3");
+    const float g = pt::rcp_rn(pt::sqrt_rn(dot(c, c)));
     return mul(c, h.flag ? -g : g);
 }
 
@@ -698,7 +713,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         // A tile whose camera rays all leave the box's silhouette skips their TestSceneTrace: the
         // result is the reference's miss (sky_ray below), and the trace is the whole cost of such
         // a tile's phase A -- about half of all 1080p tiles are sky.
-        const bool all_sky = __ballot(valid && !sky_ray(D0)) == 0;
+        const bool all_sky = pt_ballot(valid && !sky_ray(D0)) == 0;
         if (valid) {
             if (MULTI) {
                 const float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
@@ -721,7 +736,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             }
             if (COUNT) n_samp += (unsigned long long)S;
         }
-        const uint64_t hitmask = __ballot(items);
+        const uint64_t hitmask = pt_ballot(items);
         const int nh = __popcll(hitmask);
         // compacted record slot of this lane's pixel: its rank among the pixels with items
         const int my_slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(hitmask >> 32),
@@ -785,9 +800,11 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                     cp[2] = cp[2] + c.z;
                 }
             };
+            const uint64_t live = pt_ballot(true);   // the wave's lanes (exec)
             while (true) {
                 DIAG_MARK(t_it);
-                const uint64_t idle = __ballot(!has_item);
+                const uint64_t idle = pt_ballot(!has_item);
+                int ntaken = 0;   // items handed out by this refill (wave-uniform)
                 if (idle != 0 && next_item < nitems) {
                     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
@@ -821,9 +838,12 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                         needs_dir = true;
                     }
                     const int npop = __popcll(idle);
-                    next_item += npop < nitems - next_item ? npop : nitems - next_item;
+                    ntaken = npop < nitems - next_item ? npop : nitems - next_item;
+                    next_item += ntaken;
                 }
-                if (!__any(has_item)) break;
+                // __any(has_item), from the masks alone (SALU): the lanes that held an item before the
+                // refill, or any lane that took one
+                if ((live & ~idle) == 0 && ntaken == 0) break;
                 ++tile_work;
                 DIAG_ADD(1, t_it);
                 DIAG_MARK(t_dir);
@@ -870,7 +890,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                     DIAG_ADD(4, t_sh);
                 }
                 if (DEFER) {
-                    const uint64_t qm = __ballot(queued);
+                    const uint64_t qm = pt_ballot(queued);
                     if (queued) {
                         const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32),
                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));

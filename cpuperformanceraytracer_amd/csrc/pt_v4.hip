@@ -29,6 +29,7 @@
 #include "pt_invtrig.h"
 #include "pt_v4_default_scene.h"
 #include "pt_tile_queue.h"
+#include "pt_wave.h"
 #include <algorithm>
 
 namespace {
@@ -504,7 +505,7 @@ __device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir, const 
                     seq = true;
                 }
             }
-            if (__builtin_expect(__any(seq), 0)) {   // wave-uniform, rare
+            if (__builtin_expect(pt_any(seq), 0)) {   // wave-uniform, rare
                 if (seq) {
                     fb = 1;
 #pragma unroll 1
@@ -638,7 +639,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
         for (;;) {
             // hand out items to idle lanes, in lane order
             const bool need = item < 0;
-            const unsigned long long m = __ballot(need);
+            const unsigned long long m = pt_ballot(need);
             if (need) {
                 const int it = next + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -669,7 +670,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                 }
             }
             next += __builtin_popcountll(m);
-            if (__ballot(item >= 0) == 0ull) break;
+            if (pt_ballot(item >= 0) == 0ull) break;
             ++tile_work;
             if (COUNT) n_slots += 64;
             bool queued = false;   // DEFER: this lane's item missed and goes to the queue
@@ -679,8 +680,8 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
             // (the slope test runs only in iterations where every busy lane is at bounce 0: a wave-
             // uniform branch, instead of the test on every lane in every iteration)
             bool all_sky = false;
-            if (DEF && __ballot(item >= 0 && bounce != 0) == 0)
-                all_sky = __ballot(item >= 0 && !sky_ray_v4(dir)) == 0;
+            if (DEF && pt_ballot(item >= 0 && bounce != 0) == 0)
+                all_sky = pt_ballot(item >= 0 && !sky_ray_v4(dir)) == 0;
             if (item >= 0) {
                 // one iteration of GetColorForRay's bounce loop (:733-909)
                 int fb = 0;
@@ -852,7 +853,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                 }
             }
             if (DEFER) {
-                const unsigned long long qm = __ballot(queued);
+                const unsigned long long qm = pt_ballot(queued);
                 const int nq = __builtin_popcountll(qm);
                 const V3 ed = ENV == PT_V4_ENV_EQUIRECT_ ? v3(-dir.x, dir.y, -dir.z) : dir;
                 if (qn + nq > kEnvQ && nq >= qn) {   // overflow, the new misses the larger batch: now

@@ -144,7 +144,7 @@ def main() -> None:
                 cross["exact rcp / sqrt / div sequences (pt_exactmath.h)"][classify(ins[j][1])] += 1
             if "_f64" in ins[j][1] or ins[j][1].startswith("v_cvt_f32_f64") or ins[j][1].startswith("v_cvt_f64"):
                 cross["f64 instructions (all in sincosf_glibc)"][classify(ins[j][1])] += 1
-        if a.dump and ph.startswith(a.dump):
+        if a.dump is not None and ph.startswith(a.dump):
             print(f"{ph[:28]:28s} {ins[j][2].split('//')[0]}")
     # fold render_body's own lines into one bucket per source line range
     cols = ["valu_2cyc", "valu_4cyc", "valu_trans", "salu", "lds", "vmem", "scratch", "branch", "other"]
