@@ -27,6 +27,17 @@ __device__ __forceinline__ float rcp_rn(float x)
     return r;
 }
 
+// RN(1/x) for |x| < 2^-125 (zero, denormals, the lowest normals) and NaN: 1/+-0 = +-inf, else x 2^24 is
+// exact and inside rcp_rn's range, and scaling its correctly rounded reciprocal back by 2^24 is exact
+// (the same relative rounding; a result that rounds to 2^128 overflows to inf, as RN(1/x) does).
+// The slow path of a range guard: a few VALU instead of the compiler's IEEE division sequence
+// (tests/native/exactmath_probe.hip checks every such x).
+__device__ __forceinline__ float rcp_tiny_rn(float x)
+{
+    const float r = rcp_rn(x * 0x1p24f) * 0x1p24f;
+    return x == 0.0f ? __builtin_copysignf(__builtin_huge_valf(), x) : r;
+}
+
 // RN(a/b) given y = RN(1/b) (Markstein: with y the correctly rounded reciprocal and a faithful
 // first quotient, the exact-remainder correction yields the correctly rounded quotient).  Two
 // corrections: the first makes the quotient faithful, the second rounds it correctly.  Valid when

@@ -64,24 +64,20 @@ __device__ __forceinline__ V3 cross(V3 u, V3 v)
     return v3(u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x);
 }
 
-// ---- correctly rounded '/' and sqrt (pt_exactmath.h), IEEE fallback outside the fast range ----
+// ---- correctly rounded '/' and sqrt (pt_exactmath.h), an exact slow path outside the fast range ----
+// Every reciprocal of the kernel has a proven operand range: unguarded rcp_rn where it is inside
+// [2^-125, 2^125] (1/dD, the sphere normal, the lerp weights), rcp_x_nonneg where only the lower
+// end can fail.
 __device__ __forceinline__ float sqrt_x(float x) { return pt::sqrt_guarded(x); }
-__device__ __forceinline__ float rcp_x(float x)
-{
-    float r = pt::rcp_rn(x);
-    const float ax = __builtin_fabsf(x);
-    if (__builtin_expect(!(ax >= 0x1p-125f && ax <= 0x1p125f), 0)) r = 1.0f / x;
-    return r;
-}
 // RN(1/x) for an x that is >= 0 (or NaN) and provably <= 2^125: only the lower end of rcp_rn's range
 // can fail (0, denormals), so one compare guards it.
 __device__ __forceinline__ float rcp_x_nonneg(float x)
 {
     float r = pt::rcp_rn(x);
-    if (__builtin_expect(!(x >= 0x1p-125f), 0)) r = 1.0f / x;
+    if (__builtin_expect(!(x >= 0x1p-125f), 0)) r = pt::rcp_tiny_rn(x);   // 0, denormals, NaN
     return r;
 }
-// a / b with y = rcp_x(b) and b normal in [2^-125, 2^125]: exact whenever a/b is normal and
+// a / b with y = RN(1/b) and b normal in [2^-125, 2^125]: exact whenever a/b is normal and
 // |a| < 2^124; callers only use it where any other quotient is discarded by the reference's
 // comparisons (see quad_test) or cannot occur (camera: 0 <= a <= 2^24).
 __device__ __forceinline__ float div_x(float a, float b, float y) { return pt::div_rn(a, b, y); }
@@ -178,8 +174,8 @@ __device__ __forceinline__ void quad_test(int q, V3 P, V3 D, V3 pq, float dP, fl
     const float ck = flip ? ax.b : ax.c;
     const float ek = t1 ? (flip ? ax.c : ax.b) : (flip ? ax.a : ax.d);
     if (u < 0.0f || w < 0.0f) return;                         // :97,99,110,112
-    // :100-103 / :114-117
-    const float denom = rcp_x((u + v) + w);
+    // :100-103 / :114-117 (u, w >= 0 here and v >= 0 by the triangle choice: a sum >= 0, <= 3 x 9.2e3)
+    const float denom = rcp_x_nonneg((u + v) + w);
     u *= denom;
     v *= denom;
     w *= denom;
@@ -502,6 +498,18 @@ __device__ __forceinline__ V3 hit_normal(const PtLdsPrim& pr, const Hit& h, V3 P
     return mul(c, h.flag ? -g : g);
 }
 
+// s_prim[id] (id < PT_NPRIMS): the byte offset as a 24-bit multiply (v_mul_u32_u24, full rate)
+// instead of the quarter-rate v_mul_lo_u32 the compiler emits for a 32-bit index times 48
+__device__ __forceinline__ PtLdsPrim prim_at(const PtLdsPrim* s_prim, int id)
+{
+    return *(const PtLdsPrim*)((const char*)s_prim + __umul24((uint32_t)id, (uint32_t)sizeof(PtLdsPrim)));
+}
+
+// ret after bounce 0 (scalar.cpp:319): 0 + emissive * (1, 1, 1).  e * 1 == e, and 0 + e == e for
+// every e but -0; the scene's emissive values are +0 or positive (pt_build_demofox_scene: memset, then
+// the light's 20 x (1, 0.9, 0.7)), so the sum is the emissive value itself
+__device__ __forceinline__ V3 emissive0(const PtLdsPrim& pr) { return v3(pr.er, pr.eg, pr.eb); }
+
 // Miss radiance of the textured variant: EquirectangularTextureSample (texture.cpp:101-139), the
 // per-lane nearest lookup demofox_path_tracing_simt_textured.cpp:408 adds (unweighted) on a miss.
 // atan2f/asinf are the glibc algorithms (pt_invtrig.h); the texture is H x W x 3 f32, row 0 the
@@ -638,7 +646,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             s_qv[t - 128] = make_float4(e[0], e[1], e[2], e[3]);
         }
         if (t < kMaxWeights && t < job.nframes)   // :812 1/(iFrame + 1), iFrame exact below 2^24
-            s_w[t] = rcp_x((float)(job.frame_first + (uint32_t)t) + 1.0f);
+            s_w[t] = pt::rcp_rn((float)(job.frame_first + (uint32_t)t) + 1.0f);   // in [1, 2^24 + 1]: no guard
     }
     __syncthreads();
 
@@ -726,7 +734,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 c_keep = add(zero, miss_radiance<ENV>(job, amb, D0));
                 if (COUNT) n_esc += (unsigned long long)S;
             } else {
-                const PtLdsPrim pr = s_prim[h.id];
+                const PtLdsPrim pr = prim_at(s_prim, h.id);
                 const V3 n1 = hit_normal(pr, h, zero, D0);
                 P1 = add(add(zero, mul(D0, h.best)), mul(n1, PT_NUDGE));  // :313
                 N1 = n1;
@@ -763,29 +771,26 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             const int nitems = nh * npf;                  // pooled items
             const uint32_t div_m = (65536u + (uint32_t)npf - 1u) / (uint32_t)npf;   // see the take
             int next_item = 0;
-            bool has_item = false, needs_dir = false;
             int it_lane = 0, it_f = 0;
             V3 P = zero, D = zero, T = zero, ret = zero, n = zero;
             uint32_t rng = 0;
-            int bounce = 0;
+            int bounce = 0;   // 0: no item (a lane holds an item iff bounce != 0)
             const bool mine = (hitmask >> lane) & 1u;   // this lane's pixel has pool items
             if (own && mine) {   // start with this pixel's own last-frame sample (bounce 0 done)
                 // its bounce-0 record from LDS (P1 / N1 / id1 are not kept across the pool)
                 const float4 a0 = s_rec[wv][my_slot];
                 const int sId = __builtin_bit_cast(int, a0.w) & 0xff;
-                const PtLdsPrim pr = s_prim[sId];
+                const PtLdsPrim pr = prim_at(s_prim, sId);
                 const int olc = txi * 8 + (lane & 7), olr = tyi * 8 + (lane >> 3);
                 rng = seed_int((uint32_t)(job.col0 + olc), (uint32_t)(job.height - 1 - (job.row_start + olr * job.row_stride)),
                                job.frame_first + (uint32_t)(f0 + nf - 1));   // :332
                 P = v3(a0.x, a0.y, a0.z);
                 n = v3(s_nrm[wv][0][my_slot], s_nrm[wv][1][my_slot], s_nrm[wv][2][my_slot]);
-                ret = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one));             // :319
+                ret = emissive0(pr);                                             // :319
                 T = mulv(one, v3(pr.ar, pr.ag, pr.ab));                          // :322
                 bounce = 1;
                 it_lane = lane;
                 it_f = nf - 1;
-                has_item = true;
-                needs_dir = true;
             }
             int qn = 0;   // queued misses (DEFER), wave-uniform
             float4* const envq = s_envq[DEFER ? wv : 0];
@@ -803,13 +808,16 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             const uint64_t live = pt_ballot(true);   // the wave's lanes (exec)
             while (true) {
                 DIAG_MARK(t_it);
-                const uint64_t idle = pt_ballot(!has_item);
+                const bool had = bounce != 0;   // this lane holds an item (lane mask, before the refill)
+                const uint64_t idle = pt_ballot(!had);
+                bool took = false;              // this lane takes an item now (lane mask)
                 int ntaken = 0;   // items handed out by this refill (wave-uniform)
                 if (idle != 0 && next_item < nitems) {
                     const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                     const int k = next_item + rank;
-                    const bool take = !has_item && k < nitems;
+                    const bool take = !had && k < nitems;
+                    took = take;
                     // pixel-major: consecutive items are the frames of one pixel (shared ray
                     // origin; 1-1.3 % faster than frame-major).  k / npf as (k * ceil(2^16 / npf)) >>
                     // 16: exact for k < 64 npf, npf < 32 (the error k (M - 2^16 / npf) / 2^16 <
@@ -823,25 +831,23 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                         const int sId = packed & 0xff;
                         const int src = packed >> 8;                  // lane owning the pixel
                         const int slc = txi * 8 + (src & 7), slr = tyi * 8 + (src >> 3);
-                        const PtLdsPrim pr = s_prim[sId];
+                        const PtLdsPrim pr = prim_at(s_prim, sId);
                         rng = seed_int((uint32_t)(job.col0 + slc),
-                                       (uint32_t)(job.height - 1 - (job.row_start + slr * job.row_stride)),
+                                       (uint32_t)(job.height - 1 - (job.row_start + (int)__umul24((uint32_t)slr, (uint32_t)job.row_stride))),
                                        job.frame_first + (uint32_t)(f0 + fi));                    // :332
                         P = v3(a0.x, a0.y, a0.z);                                            // :313 (bounce 0)
                         n = v3(s_nrm[wv][0][slot], s_nrm[wv][1][slot], s_nrm[wv][2][slot]);
-                        ret = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one));                 // :319
+                        ret = emissive0(pr);                                                 // :319
                         T = mulv(one, v3(pr.ar, pr.ag, pr.ab));                              // :322
                         bounce = 1;
                         it_lane = src;
                         it_f = fi;
-                        has_item = true;
-                        needs_dir = true;
                     }
                     const int npop = __popcll(idle);
                     ntaken = npop < nitems - next_item ? npop : nitems - next_item;
                     next_item += ntaken;
                 }
-                // __any(has_item), from the masks alone (SALU): the lanes that held an item before the
+                // __any(a lane holds an item), from the masks alone (SALU): the lanes that held an item before the
                 // refill, or any lane that took one
                 if ((live & ~idle) == 0 && ntaken == 0) break;
                 ++tile_work;
@@ -849,11 +855,12 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 DIAG_MARK(t_dir);
                 if (COUNT) ++n_iter;
                 bool queued = false;   // DEFER: this lane's item missed, (D, slot) to be queued
-                if (has_item) {
-                    if (needs_dir) {                                                  // :316
-                        D = normalize(add(n, random_unit_vector(rng)));
-                        needs_dir = false;
-                    }
+                if (had || took) {   // (bounce != 0, from the two lane masks: no compare)
+                    // :316.  Every lane that holds an item at the start of an iteration needs a new
+                    // direction: a taken item starts at bounce 1, a hit that does not end the path
+                    // continues, and the direction after the last bounce is never drawn (the path
+                    // ends there; its RNG draws are unused)
+                    D = normalize(add(n, random_unit_vector(rng)));
                     DIAG_ADD(2, t_dir);
                     DIAG_MARK(t_tr);
                     const Hit h = trace<DemofoxScene, false, QV, !ENV>(s_axis, s_qv, P, D);
@@ -867,14 +874,13 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                         done = true;
                         if (COUNT) ++n_esc;
                     } else {
-                        const PtLdsPrim pr = s_prim[h.id];
+                        const PtLdsPrim pr = prim_at(s_prim, h.id);
                         n = hit_normal(pr, h, P, D);
                         P = add(add(P, mul(D, h.best)), mul(n, PT_NUDGE));            // :313
                         ret = add(ret, mulv(v3(pr.er, pr.eg, pr.eb), T));             // :319
                         T = mulv(T, v3(pr.ar, pr.ag, pr.ab));                         // :322
                         bounce += 1;
                         done = bounce > B;
-                        needs_dir = !done;       // the direction after the last bounce is never used
                     }
                     if (done) {
                         if (own && it_f == nf - 1) {   // own item: it_lane == lane
@@ -885,7 +891,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                             c[1] = ret.y;
                             c[2] = ret.z;
                         }
-                        has_item = false;
+                        bounce = 0;   // no item
                     }
                     DIAG_ADD(4, t_sh);
                 }
@@ -927,7 +933,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                     // color = 0 + c * (1/1) (:355-356); lerp(last, color, 1/(iFrame+1)) (:812)
                     const V3 colr = v3(0.0f + c.x * 1.0f, 0.0f + c.y * 1.0f, 0.0f + c.z * 1.0f);
                     const int f = f0 + fi;
-                    const float t = f < kMaxWeights ? s_w[f] : rcp_x((float)(job.frame_first + (uint32_t)f) + 1.0f);
+                    const float t = f < kMaxWeights ? s_w[f] : pt::rcp_rn((float)(job.frame_first + (uint32_t)f) + 1.0f);
                     acc = add(acc, mul(sub(colr, acc), t));
                 }
             }
@@ -1180,7 +1186,7 @@ hipError_t pt_launch_render(const PtJob& job_in, hipStream_t st, bool count)
     if (job_in.ncols <= 0 || job_in.nrows <= 0 || job_in.nframes <= 0) return hipSuccess;
     if (!job_in.scene || !job_in.buf || !job_in.queue) return hipErrorInvalidValue;
     // mainImage's frame constants (scalar.cpp:338-347): IEEE f32 '/' here (host, -ffp-contract=off)
-    // == the kernel's correctly rounded div_x / rcp_x
+    // == the kernel's correctly rounded div_x / rcp_rn
     PtJob job = job_in;
     job.cam_W = (float)job.width;
     job.cam_H = (float)job.height;

@@ -77,8 +77,18 @@ __device__ __forceinline__ float rcp(float x)   // rcp -> 1.f / x (mathlib.h:415
     if (__builtin_expect(!(ax >= 0x1p-125f && ax <= 0x1p125f), 0)) r = 1.0f / x;
     return r;
 }
+// 1.f / x for an x >= 0 (or NaN) that is provably <= 2^125: only the lower end of rcp_rn's range can
+// fail (0, denormals), one compare guards it
+__device__ __forceinline__ float rcp_nonneg(float x)
+{
+    float r = pt::rcp_rn(x);
+    if (__builtin_expect(!(x >= 0x1p-125f), 0)) r = pt::rcp_tiny_rn(x);   // 0, denormals, NaN
+    return r;
+}
 __device__ __forceinline__ float sqrt_(float x) { return pt::sqrt_guarded(x); }
 __device__ __forceinline__ V3 normalize(V3 v) { return v * rcp(sqrt_(dot(v, v))); }  // mathlib.h:759
+// normalize of a vector no longer than ~2 (unit vectors, their sums and lerps): sqrt(dot) <= 2^125
+__device__ __forceinline__ V3 normalize_small(V3 v) { return v * rcp_nonneg(sqrt_(dot(v, v))); }
 
 __device__ __forceinline__ uint32_t wang(uint32_t& s)   // mathutils.h:8-16 (logical shifts)
 {
@@ -308,12 +318,17 @@ struct Hit {
 };
 
 // TestQuadTrace :556-637 for one quad (the reference's operations; `dk` evaluates its fused dots)
-template <class DOT>
+// DEF (InitializeScene's quads): 1/rdn without the range guard.  Their normals are axis vectors and
+// their v0 components have magnitudes >= 1.5, so ron = dot(v0 - pos, n) = +-(v0_j - pos_j) is 0 or
+// >= 6e-8 in magnitude (Sterbenz, or >= |v0_j| / 2).  The reference keeps dist = ron / rdn only inside
+// (0.01, best <= 1e4), which needs |rdn| >= 6e-12 -- inside rcp_rn's range, where the values agree.
+// Outside it (|rdn| < 2^-125, 0, NaN) both quotients are 0, huge, +-inf or NaN: rejected either way.
+template <bool DEF, class DOT>
 __device__ __forceinline__ void quad_test(V3 pos, V3 dir, Hit& h, int obj, V3 v0, V3 n, const DOT& dk, int q)
 {
     const V3 off = v0 - pos;
     const float rdn = dk(dir, q, 1);   // dot(dir, normal)
-    const float dist = dk(off, q, 1) * rcp(rdn);
+    const float dist = dk(off, q, 1) * (DEF ? pt::rcp_rn(rdn) : rcp(rdn));
     // the hit needs (tri1 || tri2) && 0.01 < dist < best: the barycentric tests only run for
     // distances in range (a wave whose lanes all fail skips them)
     if (dist > kMinHit && dist < h.dist) {
@@ -426,6 +441,8 @@ constexpr bool default_spheres_on_x_line()
 }
 static_assert(default_spheres_on_x_line(),
               "the sphere-order rule needs InitializeScene's spheres on one x line, >= 0.4 apart");
+static_assert(pt_v4_default::kSphere[0][3] > 1.0f && pt_v4_default::kSphere[0][3] < 4.0f,
+              "the unguarded closest-sphere normal assumes radii of order 1 (all equal, above)");
 #ifndef PT_V4_SPHERE_FORCE_SEQ
 #define PT_V4_SPHERE_FORCE_SEQ 0   // test builds: every candidate ray takes the sequential fallback
 #endif
@@ -463,7 +480,7 @@ __device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir, const 
         };
 #pragma unroll
         for (int i = 0; i < D::kQuads; ++i)
-            quad_test(pos, dir, h, i, v3(D::kQuad[i][0], D::kQuad[i][1], D::kQuad[i][2]),
+            quad_test<true>(pos, dir, h, i, v3(D::kQuad[i][0], D::kQuad[i][1], D::kQuad[i][2]),
                       v3(D::kQuad[i][3], D::kQuad[i][4], D::kQuad[i][5]), dk, i);
         {   // closest-sphere stage
             float bmax = -__builtin_huge_valf(), dsel = 0.0f;
@@ -498,21 +515,21 @@ __device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir, const 
                         h.inside = inside;
                         h.dist = dist;
                         const V3 p = v3(fma_(dir.x, dist, m.x), fma_(dir.y, dist, m.y), fma_(dir.z, dist, m.z));
-                        h.n = normalize(p) * (inside ? -1.0f : 1.0f);
+                        // p = hit point - centre, |p| = the radius (2.8, asserted) up to rounding: the
+                        // radicand and the divisor are far inside the fast paths' ranges, no guards
+                        h.n = (p * pt::rcp_rn(pt::sqrt_rn(dot(p, p)))) * (inside ? -1.0f : 1.0f);
                         h.mat = D::kQuads + ksel;
                     }
                 } else {
                     seq = true;
                 }
             }
-            if (__builtin_expect(pt_any(seq), 0)) {   // wave-uniform, rare
-                if (seq) {
-                    fb = 1;
+            if (__builtin_expect(seq, 0)) {   // rare; s_cbranch_execz skips it when no lane needs it
+                fb = 1;
 #pragma unroll 1
-                    for (int i = 0; i < D::kSpheres; ++i) {
-                        const float4 c = s_sc[i];
-                        sphere_test(pos, dir, h, D::kQuads + i, v3(c.x, c.y, c.z), c.w);
-                    }
+                for (int i = 0; i < D::kSpheres; ++i) {
+                    const float4 c = s_sc[i];
+                    sphere_test(pos, dir, h, D::kQuads + i, v3(c.x, c.y, c.z), c.w);
                 }
             }
         }
@@ -522,7 +539,7 @@ __device__ __forceinline__ Hit trace(const PtV4Scene& sc, V3 pos, V3 dir, const 
             const PtV4Quad& q = sc.quad[i];
             const float* t = &q.v0[0];
             const auto dk = [t](V3 v, int, int k) { return dot(v, ld3(t + 3 * k)); };
-            quad_test(pos, dir, h, obj, ld3(q.v0), ld3(q.n), dk, i);
+            quad_test<false>(pos, dir, h, obj, ld3(q.v0), ld3(q.n), dk, i);
         }
         for (int i = 0; i < sc.nspheres; ++i, ++obj) sphere_test(pos, dir, h, obj, ld3(sc.sph[i]), sc.sph[i][3]);
     }
@@ -661,7 +678,9 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                         const float tx = fma_(((float)X + jx) * rW, 2.0f, -1.0f);
                         float ty = fma_(((float)fyi + jy) * rH, 2.0f, -1.0f);
                         ty = ty * (rW * H);
-                        dir = normalize(v3(tx, ty, -cam_dist) - v3(0.0f, 0.0f, 0.0f));
+                        // |(tx, ty, -1)| >= 1 and tx, ty are O(1): no range guards
+                        const V3 cv = v3(tx, ty, -cam_dist) - v3(0.0f, 0.0f, 0.0f);
+                        dir = cv * pt::rcp_rn(pt::sqrt_rn(dot(cv, cv)));
                         pos = v3(0.0f, 0.0f, 1.0f * 40.0f);   // camera.Position :1501
                         T = v3(1.0f, 1.0f, 1.0f);
                         ret = v3(0.0f, 0.0f, 0.0f);
@@ -769,7 +788,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                             const V3 u = ruv_rejection_of(h0, h1, h2);
                             const V3 sn = do_refr ? neg(h.n) : h.n;
                             const V3 a = u + sn;
-                            const V3 nb = a * rcp(sqrt_(dot(a, a)));
+                            const V3 nb = a * rcp_nonneg(sqrt_(dot(a, a)));   // |a| <= 2
                             const float vdn = dot(dir, h.n);
                             // reflect (:861-862): dir - 2 dot(dir, n) n as fma
                             const float d2 = 2.0f * vdn;
@@ -820,11 +839,11 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                             }
                             ndir = rd;
                         }
-                        ndir = normalize(ndir);
+                        ndir = normalize_small(ndir);   // a unit vector or a lerp of two
                         ret = v3(fma_(em.x, T.x, ret.x), fma_(em.y, T.y, ret.y), fma_(em.z, T.z, ret.z));
                         const V3 cf = do_spec ? ld3(M.spec_color) : ld3(M.albedo);
                         if (!do_refr) T = mul(T, cf);
-                        T = T * rcp(prob);
+                        T = T * rcp(prob);   // (prob >= 0.001; materials may set any chance)
                         {   // :891-899 (boost only; the path continues either way)
                             const float pm = max_ps(T.x, max_ps(T.y, T.z));
                             const bool term = randf(rng) > pm;

@@ -3,6 +3,7 @@
 // -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero).
 //
 //   rcp_rn(x)  == 1.0f / x   for EVERY f32 x with 2^-125 <= |x| <= 2^125           (2^32 inputs)
+//   rcp_tiny_rn(x) == 1.0f / x for EVERY f32 x with |x| < 2^-125 (zeros, denormals)  (same pass)
 //   sqrt_rn(x) == sqrtf(x)   for EVERY f32 x >= 2^-100 (finite)                       (2^31 inputs)
 //   div_rn(a, b, rcp_rn(b)) == a / b  on N pseudo-random pairs per operand class (normal results)
 //
@@ -35,6 +36,13 @@ __global__ void k_rcp(Res* r)
          u += (uint64_t)gridDim.x * blockDim.x) {
         const float x = __builtin_bit_cast(float, (uint32_t)u);
         const float ax = __builtin_fabsf(x);
+        if (ax < 0x1p-125f) {   // rcp_tiny_rn: zeros, denormals, the lowest normals
+            ++n;
+            const float want = 1.0f / x;
+            const float got = pt::rcp_tiny_rn(x);
+            if (__builtin_bit_cast(uint32_t, want) != __builtin_bit_cast(uint32_t, got)) record(r, (uint32_t)u, 1, got, want);
+            continue;
+        }
         if (!(ax >= 0x1p-125f && ax <= 0x1p125f)) continue;
         ++n;
         const float want = 1.0f / x;
