@@ -79,6 +79,8 @@ def main() -> None:
                     help="function-name prefixes the pool loop must hold ('*' = anything)")
     ap.add_argument("--groups", action="store_true", help="also print the grouped markdown table (DESIGN.md §3)")
     ap.add_argument("--dump", default=None, help="print the instructions of the phases starting with this")
+    ap.add_argument("--by-line", action="store_true",
+                    help="attribute instructions to the body function's source line (its call sites)")
     a = ap.parse_args()
     co = build(a.defines, a.src, a.csrc)
     dis = subprocess.run([str(LLVM / "llvm-objdump"), "-d", str(co), f"--disassemble-symbols={a.kernel}"],
@@ -127,7 +129,9 @@ def main() -> None:
         fr = frames[j]
         names = [f for f, _ in fr]
         k = next((i for i, f in enumerate(names) if f.startswith(a.body)), len(names))
-        if k == 0:
+        if a.by_line and k < len(names):
+            ph = a.body + ":" + fr[k][1].rsplit(":", 2)[-2]   # the body's line (own code or call site)
+        elif k == 0:
             ph = a.body + ":" + fr[0][1].rsplit(":", 2)[-2]   # its own line
         else:
             ph = short(names[k - 1])

@@ -6,6 +6,8 @@ equal the reference's scalar path (demofox_path_tracing_scalar.cpp) bit for bit.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 
@@ -16,6 +18,10 @@ from oracle import pyoracle
 pytestmark = pytest.mark.gpu
 
 import cpuperformanceraytracer_amd as pt  # noqa: E402
+
+# scripts/gpu_forced_fallback.sh: the library built with the *_SPHERE_FORCE_SEQ switches, whose
+# fallback RATES are 100 % by construction (the images must still be bit-exact)
+FORCED_FALLBACK = os.environ.get("PT_TEST_FORCED_FALLBACK") == "1"
 
 
 @pytest.fixture(autouse=True)
@@ -183,7 +189,8 @@ def test_device_counts_match_oracle_counts():
     assert cnt["lane_slots"] >= cnt["segments"]
     # the culled quad stage (pt_quadcull.h) certifies almost every segment: the six exact quad
     # tests run as a fallback only (and the image above is still bit-identical)
-    assert cnt["quad_fallbacks"] <= 2e-3 * cnt["segments"], cnt
+    if not FORCED_FALLBACK:   # (a forced-fallback build sends every candidate there)
+        assert cnt["quad_fallbacks"] <= 2e-3 * cnt["segments"], cnt
 
 
 def test_quad_cull_fallback_rate_full_hd():
@@ -193,7 +200,8 @@ def test_quad_cull_fallback_rate_full_hd():
     w, h = 1920, 1080
     buf = torch.zeros(h * w * 3, dtype=torch.float32, device="cuda")
     cnt = count_device(buf, w, h, frame_first=1, nframes=2, num_bounces=8)
-    assert 0 < cnt["quad_fallbacks"] <= 1e-3 * cnt["segments"], cnt
+    if not FORCED_FALLBACK:   # (a forced-fallback build sends every candidate there)
+        assert 0 < cnt["quad_fallbacks"] <= 1e-3 * cnt["segments"], cnt
     # sky tiles (pt_kernel.hip sky_ray) skip their camera rays' TestSceneTrace: about half the
     # pixels of this view, never more than the camera rays -- exactly the 8x8 tiles the oracle's
     # restatement of the test classifies as sky (pto_sky_skipped, the roofline's F_SKY_TRACE count)

@@ -10,6 +10,8 @@ synthetic arrays (the reference's .hdr files do not travel to the GPU box).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import pytest
 
@@ -21,6 +23,10 @@ pytestmark = pytest.mark.gpu
 
 import cpuperformanceraytracer_amd as pt  # noqa: E402
 from cpuperformanceraytracer_amd import _native as N  # noqa: E402
+
+# scripts/gpu_forced_fallback.sh: the library built with the *_SPHERE_FORCE_SEQ switches, whose
+# fallback RATES are 100 % by construction (the images must still be bit-exact)
+FORCED_FALLBACK = os.environ.get("PT_TEST_FORCED_FALLBACK") == "1"
 
 
 def _tex(h: int, w: int, seed: int) -> np.ndarray:
@@ -117,7 +123,8 @@ def test_v4_full_1080p_8spp():
     assert cnt["samples"] == 1920 * 1080 * 8
     # the closest-sphere stage (pt_v4.hip) decides almost every segment; the sequential sphere
     # tests run as a fallback only, and the image above is still bit-identical
-    assert cnt["sphere_fallbacks"] <= 1e-3 * cnt["segments"], cnt
+    if not FORCED_FALLBACK:   # (a forced-fallback build sends every candidate there)
+        assert cnt["sphere_fallbacks"] <= 1e-3 * cnt["segments"], cnt
     # all-sky iterations (pt_v4.hip sky_ray_v4) skip TestSceneTrace for their camera rays
     assert 0 < cnt["sky_skipped"] < cnt["samples"], cnt
 
