@@ -458,7 +458,7 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, 
     const float ak = QV ? ar.a : (fl ? ar.d : ar.a), bk = QV ? ar.b : (fl ? ar.c : ar.b);
     const float ck = QV ? ar.c : (fl ? ar.b : ar.c), dk = QV ? ar.d : (fl ? ar.a : ar.d);
     float dist;
-    const int code = ptqc::quad_exact(Pf, pqf, ptqc::F3{r0.x, r0.y, r0.z}, ptqc::F3{r0.w, r1.x, r1.y},
+    const int code = ptqc::quad_exact<false>(Pf, pqf, ptqc::F3{r0.x, r0.y, r0.z}, ptqc::F3{r0.w, r1.x, r1.y},
                                       ptqc::F3{r1.z, r1.w, r2.x}, ptqc::F3{r2.y, r2.z, r2.w}, ak, bk, ck, dk, dP, dD,
                                       yD, PT_SUPER_FAR, dist);
     const bool ok = code == ptqc::kAccepted && ptqc::cull_beyond(cl, dist);
@@ -930,8 +930,12 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                             c = v3(cp[0], cp[1], cp[2]);
                         }
                     }
-                    // color = 0 + c * (1/1) (:355-356); lerp(last, color, 1/(iFrame+1)) (:812)
-                    const V3 colr = v3(0.0f + c.x * 1.0f, 0.0f + c.y * 1.0f, 0.0f + c.z * 1.0f);
+                    // color = 0 + c * (1/1) (:355-356); lerp(last, color, 1/(iFrame+1)) (:812).  c * 1 == c
+                    // and 0 + c == c for every c but -0, and a sample's radiance is never -0: it is
+                    // 0 + (the miss radiance) for a missed camera ray, else the emissive value (+0 or
+                    // positive) plus products and sums of non-negative terms and, in the env kernel, the
+                    // texel added to that (x + (-0) == x) -- so color is c itself
+                    const V3 colr = c;
                     const int f = f0 + fi;
                     const float t = f < kMaxWeights ? s_w[f] : pt::rcp_rn((float)(job.frame_first + (uint32_t)f) + 1.0f);
                     acc = add(acc, mul(sub(colr, acc), t));

@@ -306,7 +306,12 @@ PTQC_HD Cull cull(F3 P, F3 pq, float dP, float yD, CullTrace* tr = nullptr)
 // reference's order after its facing flip, with (ak, bk, ck, dk) their components on the lane's
 // distance axis.  Returns kAccepted when the reference accepts (u, w >= 0 and 0.01 < dist < limit),
 // kOutside when its inside test fails, kRejected when the distance test does.
+// LIMIT = false: the caller's limit is c_superFar and the ray's |dD| >= 0.1 (pt_kernel.hip's axis
+// rule on a unit direction), so an accepted distance is finite and < 10^4 anyway: |ip_k - dP| <= 70
+// (ip_k a weighted mean of the vertices' k components, |.| <= 35; |dP| <= 36 for the camera origin
+// and every origin of cull()'s domain -- others take the exact fallback), dist <= 700.
 enum QuadExact : int { kOutside = 0, kRejected = 1, kAccepted = 2 };
+template <bool LIMIT = true>
 PTQC_HD int quad_exact(F3 P, F3 pq, F3 a, F3 b, F3 c, F3 d, float ak, float bk, float ck, float dk, float dP,
                        float dD, float yD, float limit, float& dist)
 {
@@ -328,7 +333,7 @@ PTQC_HD int quad_exact(F3 P, F3 pq, F3 a, F3 b, F3 c, F3 d, float ak, float bk, 
     const float ip = (un * ak + vn * ek) + wn * ck;    // :104 / :118, component k
     dist = PTQC_DIV_EXACT(ip - dP, dD, yD);            // :124 / :128 / :132
     if (!inside) return kOutside;
-    return dist > PT_MIN_HIT && dist < limit ? kAccepted : kRejected;   // :135
+    return dist > PT_MIN_HIT && (!LIMIT || dist < limit) ? kAccepted : kRejected;   // :135
 }
 
 }  // namespace ptqc
