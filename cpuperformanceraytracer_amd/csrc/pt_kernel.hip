@@ -137,12 +137,11 @@ __device__ __forceinline__ bool facing(V3 n, V3 D)
 struct AxisRow {
     float a, b, c, d;
 };
-// The per-axis rows of a quad, s_axis[(q * F + fl) * 3 + k]: QV kernels keep them for both vertex
-// orders (F = 2: row (q, fl, k) holds the components in the order after the facing flip, so the
-// culled stage reads its quad's row without selects); the env kernel, whose LDS is full at 4
-// blocks per CU, only the unflipped ones (F = 1).
+// The per-axis rows of a quad, s_axis[(q * 2 + fl) * 3 + k], for both vertex orders: row (q, fl, k)
+// holds the components in the order after the facing flip, so the culled stage reads its quad's
+// rows without selects (the six exact tests of the fallback read the unflipped ones, fl = 0).
 template <bool QV>
-constexpr int kAxisRowsPerQuad = QV ? 6 : 3;
+constexpr int kAxisRowsPerQuad = 6;
 
 // TestQuadTrace, scalar.cpp:65-143.  `pq` = (rayPos + rayDir) - rayPos (ray-constant, hoisted),
 // `axis`/`dP`/`dD`/`yD` = the component :121-133 divides by, its ray origin, direction, RN(1/dir),
@@ -444,19 +443,15 @@ __device__ __forceinline__ Hit trace(const AxisRow* s_axis, const float4* s_qv, 
         r0 = rec[0], r1 = rec[1], r2 = rec[2];
         ar = s_axis[(W * 2 + (fl ? 1 : 0)) * 3 + axis];   // flip-ordered: (ak, bk, ck, dk)
     } else {
-        // rows x, y, z of quad W: (a_k, b_k, c_k, d_k); flipped order d, c, b, a
-        const AxisRow rx = s_axis[W * 3 + 0], ry = s_axis[W * 3 + 1], rz = s_axis[W * 3 + 2];
-        ar = axis == 0 ? rx : (axis == 1 ? ry : rz);
-        const V3 va = v3(fl ? rx.d : rx.a, fl ? ry.d : ry.a, fl ? rz.d : rz.a);
-        const V3 vb = v3(fl ? rx.c : rx.b, fl ? ry.c : ry.b, fl ? rz.c : rz.b);
-        const V3 vc = v3(fl ? rx.b : rx.c, fl ? ry.b : ry.c, fl ? rz.b : rz.c);
-        const V3 vd = v3(fl ? rx.a : rx.d, fl ? ry.a : ry.d, fl ? rz.a : rz.d);
-        r0 = make_float4(va.x, va.y, va.z, vb.x);
-        r1 = make_float4(vb.y, vb.z, vc.x, vc.y);
-        r2 = make_float4(vc.z, vd.x, vd.y, vd.z);
+        // the flip-ordered rows x, y, z of quad W: vertex v of the reference's order is (rx[v], ry[v], rz[v])
+        const AxisRow* rr = s_axis + (W * 2 + (fl ? 1 : 0)) * 3;
+        const AxisRow rx = rr[0], ry = rr[1], rz = rr[2];
+        ar = rr[axis];
+        r0 = make_float4(rx.a, ry.a, rz.a, rx.b);
+        r1 = make_float4(ry.b, rz.b, rx.c, ry.c);
+        r2 = make_float4(rz.c, rx.d, ry.d, rz.d);
     }
-    const float ak = QV ? ar.a : (fl ? ar.d : ar.a), bk = QV ? ar.b : (fl ? ar.c : ar.b);
-    const float ck = QV ? ar.c : (fl ? ar.b : ar.c), dk = QV ? ar.d : (fl ? ar.a : ar.d);
+    const float ak = ar.a, bk = ar.b, ck = ar.c, dk = ar.d;
     float dist;
     const int code = ptqc::quad_exact<false>(Pf, pqf, ptqc::F3{r0.x, r0.y, r0.z}, ptqc::F3{r0.w, r1.x, r1.y},
                                       ptqc::F3{r1.z, r1.w, r2.x}, ptqc::F3{r2.y, r2.z, r2.w}, ak, bk, ck, dk, dP, dD,
@@ -598,11 +593,16 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     constexpr int kWavesPerBlock = waves_per_block<ENV>();
     __shared__ PtLdsPrim s_prim[PT_NPRIMS];
     __shared__ AxisRow s_axis[PT_NQUADS * kAxisRowsPerQuad<!ENV>];
-    // the culled quad stage (pt_quadcull.h); the env kernel's 40 912 B of LDS leave no room for the
-    // 576-B flip-ordered vertex table at 4 blocks per CU, so it reads the per-axis rows (QV false)
+    // the culled quad stage (pt_quadcull.h); the env kernel's LDS (4 blocks per CU: <= 40 960 B) has
+    // no room for the 576-B flip-ordered vertex table, so it assembles W's vertices from the three
+    // flip-ordered per-axis rows (QV false), and computes the lerp weights instead of tabling them
     constexpr bool QV = !ENV;
     __shared__ float4 s_qv[QV ? kQuadVecs : 1];
-    __shared__ float s_w[kMaxWeights];
+    constexpr bool WTAB = !ENV;
+    // the closest-sphere stage; the env kernel keeps the sequential tests (round 3, with the flip-
+    // ordered rows: 0.6024 vs 0.6001 ms at 1080p 16 spp, profiles/r03n_ab.jsonl)
+    constexpr bool SPHC = !ENV;
+    __shared__ float s_w[WTAB ? kMaxWeights : 1];
     constexpr int CH = kChunk;
     // The last frame of a chunk is traced by the pixel's own lane (OWN_LAST): its radiance stays in
     // that lane's registers, and the LDS holds CH - 1 frames per pixel -- 3 KiB less per block,
@@ -645,7 +645,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             }
             s_qv[t - 128] = make_float4(e[0], e[1], e[2], e[3]);
         }
-        if (t < kMaxWeights && t < job.nframes)   // :812 1/(iFrame + 1), iFrame exact below 2^24
+        if (WTAB && t < kMaxWeights && t < job.nframes)   // :812 1/(iFrame + 1), iFrame exact below 2^24
             s_w[t] = pt::rcp_rn((float)(job.frame_first + (uint32_t)t) + 1.0f);   // in [1, 2^24 + 1]: no guard
     }
     __syncthreads();
@@ -728,7 +728,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 acc = v3(px[0], px[cs], px[2 * cs]);
             }
             const Hit h = all_sky ? Hit{PT_SUPER_FAR, -1, 0, 0}
-                                  : trace<DemofoxScene, true, QV, !ENV>(s_axis, s_qv, zero, D0);   // :335 rayPos = origin
+                                  : trace<DemofoxScene, true, QV, SPHC>(s_axis, s_qv, zero, D0);   // :335 rayPos = origin
             if (COUNT) ++n_seg, ++n_prim, n_fb += (unsigned long long)h.fb, n_sky += all_sky ? 1ull : 0ull;
             if (h.best == PT_SUPER_FAR) {                                 // :305-310
                 c_keep = add(zero, miss_radiance<ENV>(job, amb, D0));
@@ -863,7 +863,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                     D = normalize(add(n, random_unit_vector(rng)));
                     DIAG_ADD(2, t_dir);
                     DIAG_MARK(t_tr);
-                    const Hit h = trace<DemofoxScene, false, QV, !ENV>(s_axis, s_qv, P, D);
+                    const Hit h = trace<DemofoxScene, false, QV, SPHC>(s_axis, s_qv, P, D);
                     DIAG_ADD(3, t_tr);
                     DIAG_MARK(t_sh);
                     if (COUNT) ++n_seg, n_fb += (unsigned long long)h.fb;
@@ -937,7 +937,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                     // texel added to that (x + (-0) == x) -- so color is c itself
                     const V3 colr = c;
                     const int f = f0 + fi;
-                    const float t = f < kMaxWeights ? s_w[f] : pt::rcp_rn((float)(job.frame_first + (uint32_t)f) + 1.0f);
+                    const float t = WTAB && f < kMaxWeights ? s_w[f] : pt::rcp_rn((float)(job.frame_first + (uint32_t)f) + 1.0f);
                     acc = add(acc, mul(sub(colr, acc), t));
                 }
             }

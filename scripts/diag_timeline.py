@@ -1,7 +1,6 @@
 """Per-wave / per-tile timeline of one launch (dev tool; diagnostic build).
 
-Build the diagnostic library here:  python -c "from cpuperformanceraytracer_amd.build import build_variant;
-build_variant('diag', ['PT_DIAG=1'])"  and run on the GPU box:
+Build the diagnostic library here:  bash scripts/build_variant.sh diag -DPT_DIAG=1  and run on the GPU box:
     PT_MI355_LIB=build/libpt_diag.so python scripts/diag_timeline.py [W H S B]
 Prints the launch span, wave start/end skew, the idle lane-time at the end of the launch and what
 the last tiles in flight were (pt_capi.cpp diag_dump layout: 4 u64 per wave + 32 tiles x 3 u64).
@@ -75,6 +74,13 @@ dur = a[:, 1] - a[:, 0]
 res["tile_us_pct"] = np.percentile(dur, [50, 90, 99, 100]).round(1).tolist()
 res["tile_work_pct"] = np.percentile(a[:, 3], [50, 90, 99, 100]).tolist()
 res["us_per_work_iter"] = round(float(dur.sum() / a[:, 3].sum()), 3)
+# tiles without pool iterations (work 1: every camera ray missed -- sky tiles and all-miss tiles):
+# their share of the recorded wave-time and their duration (latency-bound: load, lerps, store)
+sky = a[:, 3] == 1
+res["work1_tiles"] = int(sky.sum())
+res["work1_wave_time_frac"] = round(float(dur[sky].sum() / (nw * span)), 4)
+res["work1_tile_us_pct"] = np.percentile(dur[sky], [10, 50, 90]).round(2).tolist() if sky.any() else []
+res["recorded_tiles_frac"] = round(float(len(a) / max(1, ntiles.sum())), 4)
 late = a[:, 1] > 0.9 * span
 res["tiles_ending_last10pct"] = int(late.sum())
 res["late_tile_start_us_pct"] = np.percentile(a[late, 0], [0, 50, 100]).round(1).tolist() if late.any() else []
