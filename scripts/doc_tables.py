@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Regenerate the measurement tables of DESIGN.md §4 and README.md from a profile tag's committed
+files (profiles/<TAG>_bench_*.json, profiles/<TAG>*_pmc.txt, *_kernel_stats.csv):
+    python3 scripts/doc_tables.py TAG
+Rewrites the blocks between the marker comments <!-- tables:design:begin/end --> and
+<!-- tables:readme:begin/end --> (README.md)."""
+import csv
+import json
+import re
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+P = ROOT / "profiles"
+tag = sys.argv[1]
+
+
+def bench(w):
+    return json.loads((P / f"{tag}_bench_{w}.json").read_text())
+
+
+def pmc(short):
+    f = P / f"{tag}{short}_pmc.txt"
+    out = {}
+    if f.exists():
+        for line in f.read_text().splitlines():
+            m = re.match(r"(\w+)\s+n=\s*\d+ mean=(\S+)", line)
+            if m:
+                out[m.group(1)] = float(m.group(2))
+            m = re.match(r"kernel_trace_average_ns\s+(\S+)", line)
+            if m:
+                out["avg_ns"] = float(m.group(1))
+    return out
+
+
+def e(x, d=2):
+    s = f"{x:.{d}e}"
+    m, ex = s.split("e")
+    return f"{m}·10{''.join('⁰¹²³⁴⁵⁶⁷⁸⁹'[int(c)] if c.isdigit() else '⁻' for c in str(int(ex)))}"
+
+
+W = {"c2": "c2_1080p", "c3": "c3_4k", "c4": "c4_env_1080p", "c5": "c5_8k", "v4": "v4_1080p"}
+B = {k: bench(v) for k, v in W.items()}
+M = {"c2": pmc(""), "c3": pmc("_c3"), "c4": pmc("_c4"), "v4": pmc("_v4")}
+
+
+def hbm(k):
+    m = M.get(k, {})
+    if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
+        return (m["FETCH_SIZE"] + m["WRITE_SIZE"]) * 1024 / 1e6
+    return None
+
+
+def ms(k):
+    return B[k]["kernel_ms_avg"]
+
+
+def roc(k):
+    a = M.get(k, {}).get("avg_ns")
+    return f" ({a / 1e6:.4f})" if a else ""
+
+
+rows = [
+    ("kernel time (HIP events bracketing the timed launches, interval / K; rocprofv3 kernel-trace average)",
+     [f"**{ms('c2'):.4f} ms**{roc('c2')}", f"{ms('c3'):.3f} ms{roc('c3')}", f"{ms('c4'):.4f} ms{roc('c4')}", f"{ms('c5'):.1f} ms"]),
+    ("ray-samples/s (BASELINE metric, px·spp·bounces)", [f"**{e(B['c2']['value'])}**"] + [e(B[k]["value"]) for k in ("c3", "c4", "c5")]),
+    ("primary samples/s (north-star target ≥ 10⁹)", [e(B[k]["primary_samples_per_s"]) for k in ("c2", "c3", "c4", "c5")]),
+    ("traced segments per sample (reference: 2.25)", [f"{B[k]['segments_per_sample']:.2f}" for k in ("c2", "c3", "c4", "c5")]),
+    ("algorithmic FLOP/s (frac of 157.3 TF)",
+     [f"{B[k]['roofline']['achieved']:.1f} TF/s ({100 * B[k]['roofline']['frac']:.1f} %)" for k in ("c2", "c3", "c4", "c5")]),
+    ("reference-equivalent FLOP/s", [f"{B[k]['roofline']['achieved_ref_equivalent']:.1f} TF/s" for k in ("c2", "c3", "c4", "c5")]),
+    ("HBM bytes per launch (rocprofv3 FETCH+WRITE) vs algorithmic",
+     [f"{hbm(k):.1f} MB vs {B[k]['roofline']['algorithmic_bytes_per_launch'] / 1e6:.1f} MB" if hbm(k) else "—" for k in ("c2", "c3", "c4", "c5")]),
+    ("VALU wave-instructions per launch (PMC)",
+     [f"{e(M[k]['SQ_INSTS_VALU'])}" + (f" = {M[k]['SQ_INSTS_VALU'] / (M[k]['avg_ns'] * 1024):.2f} per SIMD per ns" if k == "c2" else "")
+      if "SQ_INSTS_VALU" in M.get(k, {}) else "" for k in ("c2", "c3", "c4", "c5")]),
+]
+cpu = B["c2"].get("cpu_baseline") or {}
+if cpu:
+    rows.append((f"CPU baseline: oracle port, {cpu.get('cores')} threads (the box's cgroup CPU quota), ~{cpu.get('sample', '').split(';')[-1].strip()}",
+                 [f"{e(cpu['value'])} ray-samples/s (GPU ×{B['c2']['value'] / cpu['value']:.0f})", "", "", ""]))
+hdr = (f"| quantity (one launch; round 3, bench `profiles/{tag}_bench_*.json`, rocprofv3 `profiles/{tag}_*`) | c2: 1920×1080, 8 spp, 8 b | "
+       "c3: 3840×2160, 64 spp | c4: 1080p, 16 spp, env | c5: 7680×4320, 256 spp (one GPU, whole image) |\n|---|---|---|---|---|\n")
+design = hdr + "".join(f"| {r} | " + " | ".join(v) + " |\n" for r, v in rows)
+v = B["v4"]
+v4rows = [
+    ("kernel time (HIP events; rocprofv3 average)", f"{ms('v4'):.4f} ms{roc('v4')}"),
+    ("ray-samples/s (px·spp·bounces)", e(v["value"])),
+    ("primary samples/s", e(v["primary_samples_per_s"])),
+    ("traced segments per sample", f"{v['segments_per_sample']:.2f} (99.8 % of paths end on the env map)"),
+    ("algorithmic FLOP/s (frac of 157.3 TF)", f"{v['roofline']['achieved']:.1f} TF/s ({100 * v['roofline']['frac']:.1f} %; algorithmic = reference-equivalent: every frame traces its own jittered camera ray)"),
+    ("HBM bytes per launch (rocprofv3) vs algorithmic", f"{hbm('v4'):.1f} MB vs {v['roofline']['algorithmic_bytes_per_launch'] / 1e6:.1f} MB (24 B/px + 12 B per env texel gather)"),
+    ("VALU / SALU wave-instructions per launch (PMC)", f"{e(M['v4']['SQ_INSTS_VALU'])} / {e(M['v4']['SQ_INSTS_SALU'])}"),
+]
+design += "\nThe v4 renderer (`bench.py --workload v4_1080p`: 1920×1080, 8 spp, 8 bounces, default glass scene, 2k synthetic equirect map):\n\n"
+design += "| quantity (one launch) | v4: 1920×1080, 8 spp, 8 b, env |\n|---|---|\n" + "".join(f"| {a} | {b} |\n" for a, b in v4rows)
+readme = ("| workload | kernel time per launch | ray-samples/s (px·spp·bounces) | algorithmic FLOP frac |\n|---|---|---|---|\n"
+          f"| 1920×1080, 8 spp, 8 bounces (headline, `BASELINE.json` configs[1]) | {ms('c2'):.3f} ms | {e(B['c2']['value'])} | {B['c2']['roofline']['frac']:.3f} |\n"
+          f"| 3840×2160, 64 spp, 8 bounces (configs[2]) | {ms('c3'):.2f} ms | {e(B['c3']['value'])} | {B['c3']['roofline']['frac']:.3f} |\n"
+          f"| 1920×1080, 16 spp, env map (configs[3]) | {ms('c4'):.3f} ms | {e(B['c4']['value'])} | {B['c4']['roofline']['frac']:.3f} |\n"
+          f"| 7680×4320, 256 spp, one GPU (configs[4]'s image) | {ms('c5'):.1f} ms | {e(B['c5']['value'])} | {B['c5']['roofline']['frac']:.3f} |\n"
+          f"| v4 renderer, 1920×1080, 8 spp, equirect env | {ms('v4'):.3f} ms | {e(v['value'])} | {v['roofline']['frac']:.3f} |\n"
+          f"\n(`profiles/{tag}_bench_*.json`; rocprofv3 summaries `profiles/{tag}_*`"
+          + (f"; CPU baseline of the headline: {e(cpu['value'])} ray-samples/s on {cpu.get('cores')} host threads, GPU ×{B['c2']['value'] / cpu['value']:.0f}" if cpu else "")
+          + ".)\n")
+
+
+def put(path, key, text):
+    s = path.read_text()
+    b, en = f"<!-- tables:{key}:begin -->\n", f"<!-- tables:{key}:end -->"
+    i, j = s.index(b) + len(b), s.index(en)
+    path.write_text(s[:i] + text + s[j:])
+
+
+put(ROOT / "DESIGN.md", "design", design)
+put(ROOT / "README.md", "readme", readme)
+print(design)
+print(readme)
