@@ -875,13 +875,30 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
                 const unsigned long long qm = pt_ballot(queued);
                 const int nq = __builtin_popcountll(qm);
                 const V3 ed = ENV == PT_V4_ENV_EQUIRECT_ ? v3(-dir.x, dir.y, -dir.z) : dir;
-                if (qn + nq > kEnvQ && nq >= qn) {   // overflow, the new misses the larger batch: now
-                    if (queued) resolve(ed, rng, T, qslot);
-                } else {
-                    if (qn + nq > kEnvQ) {   // overflow, the queue the larger batch: drain it
-                        drain(qn);
-                        qn = 0;
+                if (qn + nq > kEnvQ) {
+                    // overflow: one env pass over the whole wave -- the new misses in their own lanes,
+                    // the other lanes each take one queued miss (the top `take` entries, so the rest
+                    // stay in place).  At least kEnvQ + 1 lanes busy (min(qn + nq, 64)); the drain-or-
+                    // new-batch choice this replaces ran 24-48 of the 64.
+                    const int take = std::min(qn, 64 - nq);
+                    const int r = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(~qm >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)~qm, 0u));
+                    V3 d = ed, t = T;
+                    uint32_t rr = rng;
+                    int k = qslot;
+                    bool act = queued;
+                    if (!queued && r < take) {
+                        const int e = qn - take + r;
+                        const float4 a = s_qd[DEFER ? wv : 0][DEFER ? e : 0], b = s_qt[DEFER ? wv : 0][DEFER ? e : 0];
+                        d = v3(a.x, a.y, a.z);
+                        rr = __builtin_bit_cast(uint32_t, a.w);
+                        t = v3(b.x, b.y, b.z);
+                        k = __builtin_bit_cast(int, b.w);
+                        act = true;
                     }
+                    if (act) resolve(d, rr, t, k);
+                    qn -= take;
+                } else {
                     if (queued) {
                     const int k = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32),
                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
