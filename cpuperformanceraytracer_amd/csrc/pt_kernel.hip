@@ -40,6 +40,12 @@
 #define PT_IT_DIV(a, b) pt::div_guarded((a), (b))
 #define PT_IT_SQRT(x) pt::sqrt_guarded(x)
 #include "pt_invtrig.h"
+// certified texel cells (the exact atan2f/asinf above only where a cell is not certified)
+#define PT_EC_HD __device__ __forceinline__
+#define PT_EC_RCP(x) pt::rcp_rn(x)                       // q in (1, 2^40)
+#define PT_EC_DIV(a, b) pt::div_rn((a), (b), pt::rcp_rn(b))   // |x|, |y| in [2^-20, 2^20)
+#define PT_EC_SQRT(x) pt::sqrt_rn(x)                     // t >= 2^-21 where the value is used
+#include "pt_envcert.h"
 #include "pt_tile_queue.h"
 #include "pt_wave.h"
 #include <math.h>
@@ -509,19 +515,26 @@ __device__ __forceinline__ V3 emissive0(const PtLdsPrim& pr) { return v3(pr.er, 
 // per-lane nearest lookup demofox_path_tracing_simt_textured.cpp:408 adds (unweighted) on a miss.
 // atan2f/asinf are the glibc algorithms (pt_invtrig.h); the texture is H x W x 3 f32, row 0 the
 // bottom row (stbi flip-on-load, asset_loading.cpp:12), L2/MALL-resident.
+// The texel cell is certified from short atan/asin polynomials (pt_envcert.h: the same row and column
+// whenever it certifies); the glibc-exact angles run only for the rare uncertified cells (a divergent
+// branch that s_cbranch_execz skips when no lane needs it).
 __device__ __forceinline__ V3 env_sample(const float* __restrict__ env, int W, int H, V3 d)
 {
-    float u = pt::atan2f_glibc(d.z, d.x);
-    float v = pt::asinf_glibc(d.y);
-    u = u * 0.1591f;                                        // uv *= invAtan
-    v = v * 0.3183f;
-    u = u + 0.5f;
-    v = v + 0.5f;
-    u -= (float)(int32_t)u;                                 // :115-116
-    v -= (float)(int32_t)v;
-    if (u >= 0.0f && u < 1.0f && v >= 0.0f && v < 1.0f) {  // :121
-        const int32_t row = (int32_t)(v * (float)(H - 1));
-        const int32_t col = (int32_t)(u * (float)(W - 1));
+    int32_t row, col;
+    if (__builtin_expect(!pt::ec_cell_nearest(d.z, d.x, d.y, (float)(W - 1), (float)(H - 1), row, col), 0)) {
+        float u = pt::atan2f_glibc(d.z, d.x);
+        float v = pt::asinf_glibc(d.y);
+        u = u * 0.1591f;                                        // uv *= invAtan
+        v = v * 0.3183f;
+        u = u + 0.5f;
+        v = v + 0.5f;
+        u -= (float)(int32_t)u;                                 // :115-116
+        v -= (float)(int32_t)v;
+        const bool in = u >= 0.0f && u < 1.0f && v >= 0.0f && v < 1.0f;   // :121
+        row = in ? (int32_t)(v * (float)(H - 1)) : -1;
+        col = (int32_t)(u * (float)(W - 1));
+    }
+    if (row >= 0) {
         const float* t = env + 3u * (uint32_t)(row * W + col);   // TexelFetch :6-14 (< 2^28 texels)
         return v3(t[0], t[1], t[2]);
     }

@@ -27,6 +27,12 @@
 #define PT_IT_DIV(a, b) pt::div_guarded((a), (b))
 #define PT_IT_SQRT(x) pt::sqrt_guarded(x)
 #include "pt_invtrig.h"
+// certified texel cells (the exact atan2f/asinf above only where a cell is not certified)
+#define PT_EC_HD __device__ __forceinline__
+#define PT_EC_RCP(x) pt::rcp_rn(x)                       // q in (1, 2^40)
+#define PT_EC_DIV(a, b) pt::div_rn((a), (b), pt::rcp_rn(b))   // |x|, |y| in [2^-20, 2^20)
+#define PT_EC_SQRT(x) pt::sqrt_rn(x)                     // t >= 2^-21 where the value is used
+#include "pt_envcert.h"
 #include "pt_v4_default_scene.h"
 #include "pt_tile_queue.h"
 #include "pt_wave.h"
@@ -207,13 +213,23 @@ __device__ __forceinline__ V3 sample_bilinear(const Tex& t, float u, float v)   
 
 __device__ __forceinline__ V3 equirect(const Tex& t, V3 d, bool random, uint32_t& s)
 {
-    const float at = pt::atan2f_glibc(d.z, d.x), as = pt::asinf_glibc(d.y);
-    if (random) {   // EquirectangularTextureSampleRandom :186-203
-        float u = fma_(0.1591f, at, 0.5f), v = fma_(0.3183f, as, 0.5f);
-        u = saturate(u - __builtin_floorf(u));
-        v = saturate(v - __builtin_floorf(v));
-        return sample_random(t, u, v, s);
+    if (random) {   // EquirectangularTextureSampleRandom :186-203 + TexelSampleRandom :78-86
+        // the texel cell certified from short atan/asin polynomials (pt_envcert.h); the glibc-exact
+        // angles only for the rare uncertified cells (a divergent branch, skipped when no lane needs it)
+        const float r1 = randf(s), r2 = randf(s);   // the sampler's draws, Row's first
+        const float fw = (float)t.w, fh = (float)t.h;
+        float rr, rc;
+        if (__builtin_expect(!pt::ec_cell_random(d.z, d.x, d.y, fw, fh, r1, r2, rr, rc), 0)) {
+            const float at = pt::atan2f_glibc(d.z, d.x), as = pt::asinf_glibc(d.y);
+            float u = fma_(0.1591f, at, 0.5f), v = fma_(0.3183f, as, 0.5f);
+            u = saturate(u - __builtin_floorf(u));
+            v = saturate(v - __builtin_floorf(v));
+            rr = __builtin_floorf(fma_(v, fh, -v) + r1);
+            rc = __builtin_floorf(fma_(u, fw, -u) + r2);
+        }
+        return texel_rn(t, fma_(rr, fw, rc));
     }
+    const float at = pt::atan2f_glibc(d.z, d.x), as = pt::asinf_glibc(d.y);
     float u = at * 0.1591f + 0.5f, v = as * 0.3183f + 0.5f;   // Bilinear :164-184
     u = u - __builtin_floorf(u);
     v = v - __builtin_floorf(v);
