@@ -612,9 +612,10 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     constexpr bool QV = !ENV;
     __shared__ float4 s_qv[QV ? kQuadVecs : 1];
     constexpr bool WTAB = !ENV;
-    // the closest-sphere stage; the env kernel keeps the sequential tests (round 3, with the flip-
-    // ordered rows: 0.6024 vs 0.6001 ms at 1080p 16 spp, profiles/r03n_ab.jsonl)
-    constexpr bool SPHC = !ENV;
+    // the closest-sphere stage, in both kernels (the env kernel kept the sequential tests while its
+    // miss term was the exact inverse trig: 0.6024 vs 0.6001 ms at 1080p 16 spp, profiles/r03n_ab.jsonl;
+    // with the certified texel cells 0.5459 vs 0.5524 ms, profiles/r03t_ab_c4.jsonl)
+    constexpr bool SPHC = true;
     __shared__ float s_w[WTAB ? kMaxWeights : 1];
     constexpr int CH = kChunk;
     // The last frame of a chunk is traced by the pixel's own lane (OWN_LAST): its radiance stays in

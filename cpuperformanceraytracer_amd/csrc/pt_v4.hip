@@ -584,7 +584,10 @@ __device__ __forceinline__ size_t out_index(const PtV4Job& j, int x, int r)   //
 // instances -- the exact expf's registers in the Beer branch would otherwise raise the kernel from
 // 93 to 97 VGPRs, i.e. from 5 to 4 waves per SIMD (0.410 -> 0.451 ms at 1080p equirect) -- and as
 // the runtime flag (2) for the diagnostic COUNT instances.
-template <int ENV, int LAYOUT, bool COUNT, bool DEF, int FEXP>
+// DFL: the reference's default sampling flags (USE_RANDOM_JITTER_TEXTURE_SAMPLING 1,
+// USE_UNIT_VECTOR_REJECTION_SAMPLING 1) compiled in -- the default scene's render instance only
+// (0.3950 -> 0.3924 ms at 1080p equirect, profiles/r03r_ab_v4_flags.txt).
+template <int ENV, int LAYOUT, bool COUNT, bool DEF, int FEXP, bool DFL = false>
 __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
 {
     __shared__ float s_col[kWaves][kChunk * 64 * 3];
@@ -611,7 +614,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     float* const col = s_col[wv];
     const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;
     const Tex tex{job.env, job.env_w, job.env_h};
-    const bool random = job.random_jitter != 0, rejection = job.rejection != 0;
+    const bool random = DFL || job.random_jitter != 0, rejection = DFL || job.rejection != 0;
     const int B = job.num_bounces;
     const float W = (float)job.width, H = (float)job.height;
     const float rW = rcp(W), rH = rcp(H);
@@ -984,6 +987,7 @@ hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool 
     };
     if (j.default_scene) {
         if (count) go(pt_v4_kernel<ENV, LAYOUT, true, true, 2>);
+        else if (j.fast_exp && j.random_jitter && j.rejection) go(pt_v4_kernel<ENV, LAYOUT, false, true, 1, true>);
         else if (j.fast_exp) go(pt_v4_kernel<ENV, LAYOUT, false, true, 1>);
         else go(pt_v4_kernel<ENV, LAYOUT, false, true, 0>);
     } else {

@@ -1,12 +1,14 @@
-# Dev tool: interleaved v4 timings of the working tree and build/ variants (gpurun):
-#   bash scripts/gpu_v4_timing.sh TAG "W H S B mode" VARIANT...
+# Dev tool: interleaved timings of the working tree's library and build/ variants (gpurun):
+#   bash scripts/gpu_timing.sh TAG v4|diffuse "W H S B [mode]" VARIANT...
 set -euo pipefail
 export TMPDIR=/tmp PT_QP_K=60
-OUT=gpurun_out/$1; ARGS=$2; shift 2
+OUT=gpurun_out/$1; KIND=$2; ARGS=$3; shift 3
 mkdir -p $OUT
 libs=(default)
 for v in "$@"; do libs+=(build/libpt_$v.so); done
-for r in 1 2 3; do bash scripts/ab_v4.sh $OUT/ab_v4.jsonl "$ARGS" "${libs[@]}"; done
+runner=scripts/ab.sh
+[ "$KIND" = v4 ] && runner=scripts/ab_v4.sh
+for r in 1 2 3; do bash $runner $OUT/ab_$KIND.jsonl "$ARGS" "${libs[@]}"; done
 python3 - $OUT <<'PY'
 import json, sys, collections, glob
 for f in sorted(glob.glob(f"{sys.argv[1]}/ab_*.jsonl")):
