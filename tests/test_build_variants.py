@@ -6,6 +6,8 @@
                                     side that dumps them (pt_capi.cpp)
   PT_SPHERE_FORCE_SEQ=1, PT_V4_SPHERE_FORCE_SEQ=1   every closest-sphere candidate takes the
                                     sequential fallback (the fallback's own parity run)
+  PT_EC_FORCE_EXACT=1               every env texel cell takes the exact inverse-trig fallback
+                                    (pt_envcert.h; the fallback's own parity run)
   PT_AMBIENT_WAVES=4, PT_V4_WAVES=5  occupancy A/B builds
 Every other alternate measured slower was removed from the sources (DESIGN.md records the numbers).
 """
@@ -29,6 +31,8 @@ VARIANTS = [
     ("pt_kernel.hip", ["PT_AMBIENT_WAVES=4"]),
     ("pt_v4.hip", ["PT_V4_SPHERE_FORCE_SEQ=1"]),
     ("pt_v4.hip", ["PT_V4_WAVES=5"]),
+    ("pt_kernel.hip", ["PT_EC_FORCE_EXACT=1"]),
+    ("pt_v4.hip", ["PT_EC_FORCE_EXACT=1"]),
     ("pt_capi.cpp", ["PT_DIAG=1"]),
 ]
 
