@@ -599,7 +599,7 @@ constexpr int waves_per_block() { return 4; }
 //      (:812), reading the radiance of each frame from LDS (or the constant radiance of a pixel
 //      whose camera ray missed / of c_numBounces = 0).
 // Tiles come from a per-launch atomic queue (persistent waves, next tile prefetched).
-template <int LAYOUT, bool ENV, bool COUNT, bool MULTI>
+template <int LAYOUT, bool ENV, bool COUNT, bool MULTI, bool RING>
 __device__ __forceinline__ void render_body(const PtJob& job)
 {
     const PtScene* __restrict__ sc = job.scene;
@@ -624,6 +624,9 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     // per SIMD, what its 96 VGPRs allow).  The env kernel (4 waves per SIMD by VGPRs) keeps CH.
     constexpr bool OWN_LAST = !ENV && CH > 1;
     constexpr int CHS = OWN_LAST ? CH - 1 : CH;   // LDS colour slots per pixel
+    // RING (MULTI launches of the ambient kernel with >= kRingMinFrames frames): one continuous pool
+    // over all frames, the colour slots a ring
+    static_assert(!RING || (MULTI && !ENV), "the ring pool is the ambient kernel's MULTI mode");
     __shared__ float s_col[kWavesPerBlock][64 * CHS * 3];   // phase-B radiance per (pixel, frame)
     // per item pixel: P1.xyz + (id | lane << 8) and n1 (planar), 28 B
     __shared__ float4 s_rec[kWavesPerBlock][64];
@@ -775,6 +778,143 @@ __device__ __forceinline__ void render_body(const PtJob& job)
         const uint32_t this_tile = tile;
         uint32_t tile_work = 1;   // trace iterations of this tile (the schedule's cost)
 
+        if constexpr (RING) {
+            // ------- phases B + C for a launch of several chunks' frames (MULTI): one continuous pool -------
+            // The chunked pool below drains its items at the end of every chunk (the pool tail: 18 % of
+            // the lane slots idle at 4K 64 spp, against 11 % at 8 spp with one chunk).  Here the items
+            // (pixel with items, frame) of ALL the launch's frames form one pool, frame-major, and the
+            // LDS colour slots are a ring: frame f of pixel p lives in slot (p, f mod R).  Each lane folds
+            // its pixel's frames IN FRAME ORDER as their radiance arrives (the reference's lerp, :812),
+            // which frees the slot for frame f + R; an item is handed out only when its slot is free, in
+            // item order.  slot.x < 0 marks a slot free (-1) or reserved by an item in flight (-2); a
+            // sample's radiance is >= +0 or NaN (never negative), i.e. "ready".  Same values, same order:
+            // bit-identical to the chunked path.
+            constexpr int R = CHS;
+            const bool mine = (hitmask >> lane) & 1u;   // this lane's pixel has pool items
+            if (valid && !mine) {   // no items: every frame's radiance is c_keep, folded now in frame order
+                for (int f = 0; f < S; ++f) {
+                    const float t = WTAB && f < kMaxWeights ? s_w[f] : pt::rcp_rn((float)(job.frame_first + (uint32_t)f) + 1.0f);
+                    acc = add(acc, mul(sub(c_keep, acc), t));
+                }
+            }
+            for (int i = lane; i < 64 * R; i += 64) col_lds[i * 3] = -1.0f;   // every slot free
+            const int total = nh * S;                                         // pool items
+            // i / nh as umulhi(i, ceil(2^32 / nh)) for nh >= 2: exact for i < 2^32 / 63 (here i < nh + 64);
+            // nh = 1 (ceil(2^32 / 1) does not fit 32 bits) divides by itself
+            const uint32_t div_nh = nh > 1 ? (uint32_t)((0x100000000ull + (uint64_t)nh - 1u) / (uint64_t)nh) : 0u;
+            int f_next = 0, i_next = 0;   // wave-uniform: (frame, compacted pixel) of the next item
+            int issued = 0, folded = 0;   // wave-uniform
+            int nfold = 0;                // this lane's pixel: frames folded so far
+            int fold_addr = lane * R * 3;  // its slot of frame nfold
+            const bool wtab = WTAB && S <= kMaxWeights;
+            V3 P = zero, D = zero, T = zero, ret = zero, n = zero;
+            uint32_t rng = 0;
+            int bounce = 0;   // 0: no item
+            int it_addr = 0;  // the item's colour slot (floats from col_lds)
+            const uint64_t live = pt_ballot(true);
+            while (true) {
+                const bool had = bounce != 0;
+                const uint64_t idle = pt_ballot(!had);
+                bool took = false;
+                int ntaken = 0;
+                if (idle != 0 && issued < total) {
+                    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                    const int ii = i_next + rank;
+                    const int q = nh == 1 ? ii : (int)__umulhi((uint32_t)ii, div_nh);
+                    const int f = f_next + q, slot = ii - (int)__umul24((uint32_t)q, (uint32_t)nh);
+                    const bool cand = !had && issued + rank < total;
+                    bool free = false;
+                    int addr = 0;
+                    float4 a0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                    if (cand) {
+                        a0 = s_rec[wv][slot];
+                        const int src = __builtin_bit_cast(int, a0.w) >> 8;
+                        addr = (int)__umul24((uint32_t)(src * R + f % R), 3u);
+                        // free, and not the slot of an earlier item of this hand-out (frames < f_next + R)
+                        free = col_lds[addr] == -1.0f && q < R;
+                    }
+                    const uint64_t cm = pt_ballot(cand), fm = pt_ballot(cand && free);
+                    const uint64_t blocked = cm & ~fm;   // items in order: stop at the first blocked one
+                    const uint64_t tm = blocked ? (cm & ((1ull << __builtin_ctzll(blocked)) - 1ull)) : cm;
+                    took = (tm >> lane) & 1u;
+                    if (took) {
+                        col_lds[addr] = -2.0f;   // reserved
+                        const int packed = __builtin_bit_cast(int, a0.w);
+                        const int sId = packed & 0xff;
+                        const int src = packed >> 8;                  // lane owning the pixel
+                        const int slc = txi * 8 + (src & 7), slr = tyi * 8 + (src >> 3);
+                        const PtLdsPrim pr = prim_at(s_prim, sId);
+                        rng = seed_int((uint32_t)(job.col0 + slc),
+                                       (uint32_t)(job.height - 1 - (job.row_start + (int)__umul24((uint32_t)slr, (uint32_t)job.row_stride))),
+                                       job.frame_first + (uint32_t)f);                            // :332
+                        P = v3(a0.x, a0.y, a0.z);                                            // :313 (bounce 0)
+                        n = v3(s_nrm[wv][0][slot], s_nrm[wv][1][slot], s_nrm[wv][2][slot]);
+                        ret = emissive0(pr);                                                 // :319
+                        T = mulv(one, v3(pr.ar, pr.ag, pr.ab));                              // :322
+                        bounce = 1;
+                        it_addr = addr;
+                    }
+                    ntaken = __popcll(tm);
+                    issued += ntaken;
+                    i_next += ntaken;
+                    while (i_next >= nh) {   // (SALU)
+                        i_next -= nh;
+                        ++f_next;
+                    }
+                }
+                if ((live & ~idle) == 0 && ntaken == 0 && folded >= total) break;
+                // (a guard, never reached: every item ends after <= B + 1 segments and a pool of `total`
+                // items drains in < total (B + 2) + S iterations -- a scheduling fault ends the tile
+                // with a wrong image, not a hung GPU)
+                if (__builtin_expect(tile_work > (uint32_t)total * (uint32_t)(B + 2) + (uint32_t)S + 64u, 0)) break;
+                ++tile_work;
+                if (COUNT) ++n_iter;
+                if (had || took) {
+                    D = normalize(add(n, random_unit_vector(rng)));                          // :316
+                    const Hit h = trace<DemofoxScene, false, QV, SPHC>(s_axis, s_qv, P, D);
+                    if (COUNT) ++n_seg, n_fb += (unsigned long long)h.fb;
+                    bool done;
+                    if (h.best == PT_SUPER_FAR) {                                     // :305-310
+                        ret = add(ret, miss_radiance<ENV>(job, amb, D));
+                        done = true;
+                        if (COUNT) ++n_esc;
+                    } else {
+                        const PtLdsPrim pr = prim_at(s_prim, h.id);
+                        n = hit_normal(pr, h, P, D);
+                        P = add(add(P, mul(D, h.best)), mul(n, PT_NUDGE));            // :313
+                        ret = add(ret, mulv(v3(pr.er, pr.eg, pr.eb), T));             // :319
+                        T = mulv(T, v3(pr.ar, pr.ag, pr.ab));                         // :322
+                        bounce += 1;
+                        done = bounce > B;
+                    }
+                    if (done) {
+                        lds_f32* c = col_lds + it_addr;
+                        c[1] = ret.y;
+                        c[2] = ret.z;
+                        c[0] = ret.x;   // (x last: it marks the slot ready)
+                        bounce = 0;
+                    }
+                }
+                // fold this pixel's next frame if its radiance is in (one frame per iteration)
+                bool fnow = false;
+                if (mine && nfold < S) {
+                    lds_f32* c = col_lds + fold_addr;
+                    const float cx = c[0];
+                    if (!(cx < 0.0f)) {
+                        const V3 colr = v3(cx, c[1], c[2]);   // color = c (see the chunked phase C)
+                        const float t = wtab ? s_w[nfold] : pt::rcp_rn((float)(job.frame_first + (uint32_t)nfold) + 1.0f);
+                        acc = add(acc, mul(sub(colr, acc), t));
+                        c[0] = -1.0f;   // free
+                        ++nfold;
+                        fold_addr = fold_addr + 3 == (lane + 1) * R * 3 ? lane * R * 3 : fold_addr + 3;
+                        fnow = true;
+                    }
+                }
+                folded += __popcll(pt_ballot(fnow));
+            }
+            next_tile = tq.next();   // the pool is done
+        } else {
         // one chunk covers the launch's frames unless MULTI (then the loop carries acc and c_keep)
         for (int f0 = 0; f0 < (MULTI ? S : 1); f0 += CH) {
             const int nf = S - f0 < CH ? S - f0 : CH;
@@ -957,6 +1097,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             }
             DIAG_ADD(5, t_c);
         }
+        }
         if (txi * 8 + (lane & 7) < job.ncols && tyi * 8 + (lane >> 3) < job.nrows) {
             float* px = job.buf + out_index<LAYOUT>(job, txi * 8 + (lane & 7), tyi * 8 + (lane >> 3));
             px[0] = acc.x;
@@ -1025,45 +1166,58 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 #define PT_AMBIENT_WAVES 5
 #endif
 // MULTI: the launch accumulates more frames than one LDS chunk holds (nframes > kChunk).
-template <int LAYOUT, bool COUNT, bool MULTI>
+template <int LAYOUT, bool COUNT, bool MULTI, bool RING>
 __global__ __launch_bounds__(64 * waves_per_block<false>()) __attribute__((amdgpu_waves_per_eu(PT_AMBIENT_WAVES, PT_AMBIENT_WAVES))) void
 pt_render_kernel(PtJob job)
 {
-    render_body<LAYOUT, false, COUNT, MULTI>(job);
+    render_body<LAYOUT, false, COUNT, MULTI, RING>(job);
 }
 
 template <int LAYOUT, bool COUNT, bool MULTI>
 __global__ __launch_bounds__(64 * waves_per_block<true>()) void pt_render_env_kernel(PtJob job)
 {
-    render_body<LAYOUT, true, COUNT, MULTI>(job);
+    render_body<LAYOUT, true, COUNT, MULTI, false>(job);
 }
 
-template <int LAYOUT, bool ENV, bool COUNT, bool MULTI>
+template <int LAYOUT, bool ENV, bool COUNT, bool MULTI, bool RING>
 constexpr auto kernel_of()
 {
     if constexpr (ENV) return pt_render_env_kernel<LAYOUT, COUNT, MULTI>;
-    else return pt_render_kernel<LAYOUT, COUNT, MULTI>;
+    else return pt_render_kernel<LAYOUT, COUNT, MULTI, RING>;
 }
 
-template <int LAYOUT, bool ENV, bool COUNT, bool MULTI>
+template <int LAYOUT, bool ENV, bool COUNT, bool MULTI, bool RING = false>
 void launch_k(const PtJob& job, hipStream_t st, unsigned tiles)
 {
     constexpr int wpb = waves_per_block<ENV>();
-    auto k = kernel_of<LAYOUT, ENV, COUNT, MULTI>();
+    auto k = kernel_of<LAYOUT, ENV, COUNT, MULTI, RING>();
     const unsigned blocks = (unsigned)std::min<long>(pt_resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
     hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
 }
+
+// Launches of at least kRingMinFrames frames run the ambient kernel's continuous ring pool (one pool
+// tail per tile instead of one per 8-frame chunk); fewer frames keep the chunked pool, whose own-lane
+// frame and lighter iteration win while there are only a few chunks.  Ring vs chunked at 1080p
+// (profiles/r03y_ab_*.jsonl): 16 spp 0.484 vs 0.462 ms, 32 spp 0.898 vs 0.890, 48 spp 1.307 vs
+// 1.316; 4K 64 spp 6.33 vs 6.74 ms; 8K 256 spp 97.9 vs 106.4 ms.
+#ifndef PT_RING_MIN
+#define PT_RING_MIN 48
+#endif
+constexpr int kRingMinFrames = PT_RING_MIN;
 
 template <int LAYOUT, bool ENV>
 hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 {
     const unsigned tiles = (unsigned)((job.ncols + 7) / 8) * (unsigned)((job.nrows + 7) / 8);
     const bool multi = job.nframes > kChunk;
+    const bool ring = !ENV && job.nframes >= kRingMinFrames && job.nframes > kChunk;
     if (count) {
-        if (multi) launch_k<LAYOUT, ENV, true, true>(job, st, tiles);
+        if (ring) launch_k<LAYOUT, ENV, true, true, !ENV>(job, st, tiles);
+        else if (multi) launch_k<LAYOUT, ENV, true, true>(job, st, tiles);
         else launch_k<LAYOUT, ENV, true, false>(job, st, tiles);
     } else {
-        if (multi) launch_k<LAYOUT, ENV, false, true>(job, st, tiles);
+        if (ring) launch_k<LAYOUT, ENV, false, true, !ENV>(job, st, tiles);
+        else if (multi) launch_k<LAYOUT, ENV, false, true>(job, st, tiles);
         else launch_k<LAYOUT, ENV, false, false>(job, st, tiles);
     }
     return hipGetLastError();

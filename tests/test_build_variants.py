@@ -9,6 +9,8 @@
   PT_EC_FORCE_EXACT=1               every env texel cell takes the exact inverse-trig fallback
                                     (pt_envcert.h; the fallback's own parity run)
   PT_AMBIENT_WAVES=4, PT_V4_WAVES=5  occupancy A/B builds
+  PT_RING_MIN=9                     every MULTI launch on the ring pool (its parity run: all 130 GPU
+                                    tests bit-exact, profiles/r03x_gpu_tests.txt)
 Every other alternate measured slower was removed from the sources (DESIGN.md records the numbers).
 """
 from __future__ import annotations
@@ -32,6 +34,7 @@ VARIANTS = [
     ("pt_v4.hip", ["PT_V4_SPHERE_FORCE_SEQ=1"]),
     ("pt_v4.hip", ["PT_V4_WAVES=5"]),
     ("pt_kernel.hip", ["PT_EC_FORCE_EXACT=1"]),
+    ("pt_kernel.hip", ["PT_RING_MIN=9"]),
     ("pt_v4.hip", ["PT_EC_FORCE_EXACT=1"]),
     ("pt_capi.cpp", ["PT_DIAG=1"]),
 ]
