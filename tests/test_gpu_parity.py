@@ -241,3 +241,35 @@ def test_pinned_pipelined_frames():
         pt.DemofoxRenderSimdTiled(c, w, h, 5, 8, 128, 48, 3)
     assert bits_equal(tiled_to_interleaved(c, w, h, 128, 48), ref)
     pt.shutdown()
+
+
+# ---------------------------------------------------------------- the ring pool (>= 48 frames) ---
+@pytest.mark.parametrize("w,h,frames,bounces", [(333, 97, 49, 8), (64, 40, 64, 8), (200, 120, 50, 1), (96, 64, 48, 0),
+                                                (17, 9, 70, 8)])
+def test_ring_pool_launches_vs_oracle(w, h, frames, bounces):
+    """Launches of >= 48 frames run the continuous ring pool (pt_kernel.hip RING): odd image sizes
+    (edge tiles, tiles with one hit pixel), frame counts that are not multiples of the 7-slot ring,
+    1 and 0 bounces (no pool items)."""
+    pt.init(num_bounces=bounces, samples_per_frame=frames)
+    buf = np.zeros((h, w, 3), np.float32)
+    pt.DemofoxRenderScalar(buf, w, h, 3)
+    ref = pyoracle.render(w, h, nframes=frames, num_bounces=bounces)
+    assert bits_equal(buf, ref), mismatch_report(buf, ref)
+
+
+def test_ring_pool_layouts_and_shards():
+    """The ring pool behind the planar8 layout and in row-interleaved device shards."""
+    w, h, f = 256, 72, 56
+    pt.init(num_bounces=8, samples_per_frame=f)
+    buf = np.zeros(w * h * 3, np.float32)
+    pt.DemofoxRenderSimd(buf, w, h, 3)
+    ref = pyoracle.render(w, h, nframes=f, num_bounces=8)
+    img = planar8_to_interleaved(buf, w, h)
+    assert bits_equal(img, ref), mismatch_report(img, ref)
+    full = _dev_render(w, h, f, 8)
+    assert bits_equal(full, ref), mismatch_report(full, ref)
+    rebuilt = np.zeros_like(full)
+    for r in range(3):
+        n = len(range(r, h, 3))
+        rebuilt[r::3] = _dev_render(w, h, f, 8, row_start=r, row_stride=3, nrows=n)
+    assert bits_equal(rebuilt, full)
