@@ -12,6 +12,7 @@ for wl in $WLS; do
         c3_4k) t=${TAG}_c3 ;;
         c4_env_1080p) t=${TAG}_c4 ;;
         v4_1080p) t=${TAG}_v4 ;;
+        c5_8k) t=${TAG}_c5 ;;
         *) echo "unknown workload $wl"; exit 2 ;;
     esac
     echo "== $wl -> $t"
