@@ -139,15 +139,52 @@ def random_unit_vector(seed_value: int, n: int) -> np.ndarray:
     return out
 
 
-def ref_available() -> bool:
-    return REF_BIN.exists()
+def env_sample(env: np.ndarray, dirs: np.ndarray) -> np.ndarray:
+    """pto_env_sample (texture.cpp:101-139's per-lane body) of every direction: N x 3 texels."""
+    env = np.ascontiguousarray(env, dtype=np.float32)
+    e = Env(env.ctypes.data, env.shape[1], env.shape[0])
+    d = np.ascontiguousarray(dirs, dtype=np.float32).reshape(-1, 3)
+    out = np.zeros_like(d)
+    L = load()
+    fp = ctypes.POINTER(ctypes.c_float)
+    for i in range(d.shape[0]):
+        L.pto_env_sample(ctypes.byref(e), d[i].ctypes.data_as(fp), out[i].ctypes.data_as(fp))
+    return out
 
 
-def ref_render(width: int, height: int, frames: int, tmpdir: Path) -> np.ndarray:
-    """Run the reference's own scalar code (fresh process => iFrame starts at 0)."""
-    out = Path(tmpdir) / f"ref_{width}x{height}_{frames}.f32"
-    subprocess.run([str(REF_BIN), str(width), str(height), str(frames), str(out)], check=True)
+REF_BIN_B8 = HERE / "_ref" / "ref_scalar_b8"
+REF_ENV = HERE / "_ref" / "ref_env"
+
+
+def ref_available(num_bounces: int = 4) -> bool:
+    return (REF_BIN if num_bounces == 4 else REF_BIN_B8).exists()
+
+
+def ref_render(width: int, height: int, frames: int, tmpdir: Path, num_bounces: int = 4) -> np.ndarray:
+    """Run the reference's own scalar code (fresh process => iFrame starts at 0).  num_bounces 8
+    runs the build whose only change is c_numBounces = 8 (scalar.cpp:19, oracle/build_ref.sh)."""
+    if num_bounces not in (4, 8):
+        raise ValueError("the reference builds have c_numBounces 4 (as shipped) or 8 (its //8)")
+    out = Path(tmpdir) / f"ref_{width}x{height}_{frames}_b{num_bounces}.f32"
+    exe = REF_BIN if num_bounces == 4 else REF_BIN_B8
+    subprocess.run([str(exe), str(width), str(height), str(frames), str(out)], check=True)
     return np.fromfile(out, np.float32).reshape(height, width, 3)
+
+
+def ref_env_available() -> bool:
+    return REF_ENV.exists()
+
+
+def ref_env_sample(env: np.ndarray, dirs: np.ndarray, tmpdir: Path) -> np.ndarray:
+    """The reference's own texture.cpp:111-135 (+ TexelFetch :6-14) on every direction (ref_env)."""
+    env = np.ascontiguousarray(env, dtype=np.float32)
+    d = np.ascontiguousarray(dirs, dtype=np.float32).reshape(-1, 3)
+    tdir = Path(tmpdir)
+    env.tofile(tdir / "env_tex.f32")
+    d.tofile(tdir / "env_dirs.f32")
+    subprocess.run([str(REF_ENV), str(tdir / "env_tex.f32"), str(env.shape[1]), str(env.shape[0]),
+                    str(tdir / "env_dirs.f32"), str(tdir / "env_out.f32")], check=True)
+    return np.fromfile(tdir / "env_out.f32", np.float32).reshape(-1, 3)
 
 
 PIXEL_RGBA8 = 0   # PTO_PIXEL_RGBA8 (OutputToFile)

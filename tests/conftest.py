@@ -26,9 +26,15 @@ def manifest() -> dict:
 
 
 def load_golden(name: str) -> np.ndarray:
+    """A golden image (H x W x 3); a case with "rows" holds only rows start::stride of it."""
     m = json.loads((GOLDEN / "manifest.json").read_text())["cases"][name]
     raw = lzma.decompress((GOLDEN / f"{name}.f32.xz").read_bytes())
-    return np.frombuffer(raw, dtype="<f4").reshape(m["height"], m["width"], 3).copy()
+    nrows = m["rows"]["count"] if "rows" in m else m["height"]
+    return np.frombuffer(raw, dtype="<f4").reshape(nrows, m["width"], 3).copy()
+
+
+GOLDEN_B4 = ["g1_256x256_f1", "g2_256x256_f8", "g3_200x120_f3", "g4_64x64_f32"]
+GOLDEN_B8 = ["g5_256x256_f8_b8", "g6_1920x1080_f2_b8", "g7_96x64_f53_b8"]
 
 
 @pytest.fixture(scope="session")

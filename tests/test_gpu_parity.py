@@ -11,7 +11,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import bits_equal, load_golden, mismatch_report
+from conftest import GOLDEN_B4, GOLDEN_B8, bits_equal, load_golden, mismatch_report
 from layouts import planar8_to_interleaved, tiled_to_interleaved
 from oracle import pyoracle
 
@@ -30,7 +30,7 @@ def fresh_backend():
     yield
 
 
-@pytest.mark.parametrize("name", ["g1_256x256_f1", "g2_256x256_f8", "g3_200x120_f3", "g4_64x64_f32"])
+@pytest.mark.parametrize("name", GOLDEN_B4)
 def test_scalar_matches_reference_goldens(manifest, name):
     """configs[0] and friends: DemofoxRenderScalar called F times on a zeroed buffer."""
     c = manifest["cases"][name]
@@ -40,6 +40,42 @@ def test_scalar_matches_reference_goldens(manifest, name):
     assert pt.get_frame() == c["frames"]
     g = load_golden(name)
     assert bits_equal(buf, g), mismatch_report(buf, g)
+
+
+@pytest.mark.parametrize("name", ["g5_256x256_f8_b8", "g7_96x64_f53_b8"])
+def test_scalar_matches_reference_goldens_b8(manifest, name):
+    """B = 8 (configs[1]-[4]'s bounce count) against fixtures of the reference's own code
+    (c_numBounces = 8 build): frame by frame through DemofoxRenderScalar, and all frames in ONE
+    launch -- for g7's 53 frames that is the ring pool (>= 48 frames)."""
+    c = manifest["cases"][name]
+    g = load_golden(name)
+    pt.init(num_bounces=8)
+    buf = np.zeros((c["height"], c["width"], 3), np.float32)
+    for _ in range(c["frames"]):
+        pt.DemofoxRenderScalar(buf, c["width"], c["height"], 3)
+    assert bits_equal(buf, g), mismatch_report(buf, g)
+    pt.init(num_bounces=8, samples_per_frame=c["frames"])
+    one = np.zeros_like(buf)
+    pt.DemofoxRenderScalar(one, c["width"], c["height"], 3)
+    assert pt.get_frame() == c["frames"]
+    assert bits_equal(one, g), mismatch_report(one, g)
+
+
+def test_full_hd_b8_matches_reference_rows(manifest):
+    """configs[1]'s image (1920x1080, 8 bounces) against the reference's own rows 0::54 after 2
+    frames: the host drop-in (whole image), and the device path rendering only those rows (the
+    row-interleaved multi-GPU partition with stride 54)."""
+    c = manifest["cases"]["g6_1920x1080_f2_b8"]
+    r = c["rows"]
+    g = load_golden("g6_1920x1080_f2_b8")
+    w, h = c["width"], c["height"]
+    pt.init(num_bounces=8, samples_per_frame=2)
+    buf = np.zeros((h, w, 3), np.float32)
+    pt.DemofoxRenderScalar(buf, w, h, 3)
+    got = buf[r["start"]::r["stride"]]
+    assert bits_equal(got, g), mismatch_report(got, g)
+    dev = _dev_render(w, h, 2, 8, row_start=r["start"], row_stride=r["stride"], nrows=r["count"])
+    assert bits_equal(dev, g), mismatch_report(dev, g)
 
 
 def test_samples_per_frame_batches_frames(golden):

@@ -12,17 +12,36 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from conftest import bits_equal, load_golden, mismatch_report
+from conftest import GOLDEN_B4, GOLDEN_B8, bits_equal, load_golden, mismatch_report
 from oracle import pyoracle
 
 
-@pytest.mark.parametrize("name", ["g1_256x256_f1", "g2_256x256_f8", "g3_200x120_f3", "g4_64x64_f32"])
+@pytest.mark.parametrize("name", GOLDEN_B4 + GOLDEN_B8)
 def test_oracle_matches_reference_golden(manifest, name):
+    """Every golden: B = 4 (the reference as shipped) and B = 8 (the reference with only
+    c_numBounces = 8, its own `//8`; configs[1]-[4]'s bounce count), incl. the 1080p row sample."""
     c = manifest["cases"][name]
+    rows = c.get("rows")
+    kw = {}
+    if rows:
+        kw = dict(row_start=rows["start"], row_stride=rows["stride"], nrows=rows["count"])
     img = pyoracle.render(c["width"], c["height"], frame_first=c["frame_first"], nframes=c["frames"],
-                          num_bounces=c["num_bounces"])
+                          num_bounces=c["num_bounces"], **kw)
     g = load_golden(name)
     assert bits_equal(img, g), mismatch_report(img, g)
+
+
+def test_b8_goldens_come_from_a_one_line_change(manifest):
+    """The B = 8 fixtures' generator differs from the reference file in line 19 only."""
+    p = manifest["b8_patch"]
+    assert p["line"] == 19 and p["file"] == "demofox_path_tracing_scalar.cpp"
+    assert p["diff"].splitlines() == ["19c19", "< const int c_numBounces = 4; //8", "---",
+                                      "> const int c_numBounces = 8; //8"]
+    for n in GOLDEN_B8:
+        assert manifest["cases"][n]["num_bounces"] == 8
+    # and B = 8 is not B = 4: the fixtures differ from the 4-bounce image of the same size
+    g5 = load_golden("g5_256x256_f8_b8")
+    assert not bits_equal(g5, load_golden("g2_256x256_f8"))
 
 
 def test_golden_integrity(manifest):
@@ -62,6 +81,14 @@ def test_random_unit_vectors_are_unit():
 def test_oracle_matches_live_reference(tmp_path, w, h, frames):
     ref = pyoracle.ref_render(w, h, frames, tmp_path)
     img = pyoracle.render(w, h, nframes=frames, num_bounces=4)
+    assert bits_equal(img, ref), mismatch_report(img, ref)
+
+
+@pytest.mark.skipif(not pyoracle.ref_available(8), reason="reference B=8 build (oracle/_ref) not present")
+@pytest.mark.parametrize("w,h,frames", [(96, 64, 2), (17, 33, 3), (40, 24, 49)])
+def test_oracle_matches_live_reference_b8(tmp_path, w, h, frames):
+    ref = pyoracle.ref_render(w, h, frames, tmp_path, num_bounces=8)
+    img = pyoracle.render(w, h, nframes=frames, num_bounces=8)
     assert bits_equal(img, ref), mismatch_report(img, ref)
 
 
