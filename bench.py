@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X path-tracing hot path (BASELINE.json metric and configs).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]   (N > 1: starts N ranks itself)
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
          --master-port P bench.py --gpus N --steps K --warmup W [--workload NAME]
 
@@ -558,8 +558,55 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
     return res
 
 
+def spawn_ranks(n: int, argv: list[str], script: str | None = None) -> int:
+    """`--gpus N` without a launcher: start N rank processes of `script` (default: this file) with
+    the environment torch.distributed.run gives each rank (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT), rank r on GPU r.  Called before anything
+    touches the GPU; the parent only waits (it is not replaced).  Rank 0 inherits stdout and prints the
+    JSON line.  Returns 0, or the first failing rank's exit code after killing the others."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    script = script or str(Path(__file__).resolve())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script, *argv], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0] if bad[0] > 0 else 128 - bad[0]   # (a signal: 128 + its number)
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(0.1)
+    finally:
+        for p in procs:   # a failed rank leaves the others waiting in a collective: end them
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main() -> None:
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the driver's own invocation (`python bench.py --gpus N`, no torch.distributed.run): one
+        # process per GPU, started here before any GPU call
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     import torch
     import torch.distributed as dist
 
@@ -571,8 +618,7 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            sys.exit("run N>1 under torch.distributed.run (one process per GPU)")
+        sys.exit(f"--gpus {args.gpus} disagrees with WORLD_SIZE {world}")
     # PT_BENCH_REHEARSE=1: rehearsal of the N-rank path on one GPU -- every rank on cuda:0, gloo
     # instead of RCCL, the gather through host memory (correctness of the multi-rank code only;
     # the numbers are not scaling numbers)

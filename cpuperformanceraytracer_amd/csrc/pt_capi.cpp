@@ -75,14 +75,19 @@ struct Dev {
     float* dbuf = nullptr;              // mirror of this device's rows of the host accumulator
     size_t dbuf_cap = 0;
     unsigned long long* dcounters = nullptr;
+    uint32_t* derr = nullptr;           // PT_ERR_WORDS kernel error words (PtJob::err)
+    uint32_t* herr = nullptr;           // their page-locked host copy (read at every synchronisation)
     unsigned int* dqueue = nullptr;     // ring of kQueueRing tile-queue blocks (PT_QUEUE_WORDS each)
     unsigned queue_next = 0;
     bool queue_pre_zeroed = false;      // the last launch's kernel zeroes ring slot queue_next % kQueueRing
     hipStream_t last_stream = nullptr;  // the stream of the last launch
     // per ring slot: the stream of the last launch that used it and an event recorded after that
     // launch; a launch on another stream waits for it before re-zeroing the slot
-    hipStream_t queue_stream[kQueueRing] = {};
-    hipEvent_t queue_event[kQueueRing] = {};
+    hipStream_t queue_stream[kQueueRing] = {};   // (compared for equality only, never used: it may be
+    hipEvent_t queue_event[kQueueRing] = {};     //  a caller's stream that no longer exists)
+    // a slot skipped by a change of stream is ordered by the event of the slot before it (recorded
+    // after the launch whose kernel zeroes the skipped slot): its index, or -1
+    int16_t queue_alias[kQueueRing];
     float* denv = nullptr;              // env map in HBM (pt_set_env_map / textured / v4)
     Sched sched[kSchedSlots];
     unsigned long long sched_clock = 0;
@@ -126,6 +131,9 @@ struct State {
     PtV4SceneDesc v4desc{};
     PtV4Scene v4scene{};
     uint32_t v4_frame = 0;
+    // test hook: PT_MI355_RING_GUARD_CAP (read by pt_init) caps the ring pool's iteration guard so
+    // that it fires -- the error path's own GPU test (tests/test_gpu_state.py)
+    uint32_t ring_guard_cap = ~0u;
 };
 
 State g;
@@ -255,12 +263,33 @@ int xfer(int d, const Geo& geo, float* host, bool to_device, const Region& rg)
     return PT_OK;
 }
 
+// Synchronise every device stream and report what the kernels recorded in their error words since
+// the last synchronisation: a tile the ring pool's iteration guard abandoned mid-pool (pt_kernel.hip)
+// leaves a wrong accumulator, so no call that waited for such a launch returns PT_OK.  The words are
+// reset when reported.
 int sync_all()
 {
+    int rc;
     for (int d = 0; d < g.ndev; ++d) {
-        int rc;
+        Dev& dv = g.dev[d];
+        if ((rc = use_dev(dv))) return rc;
+        HIP_TRY(hipMemcpyAsync(dv.herr, dv.derr, PT_ERR_WORDS * sizeof(uint32_t), hipMemcpyDeviceToHost, dv.stream));
+    }
+    for (int d = 0; d < g.ndev; ++d) {
         if ((rc = use_dev(g.dev[d]))) return rc;
         HIP_TRY(hipStreamSynchronize(g.dev[d].stream));
+    }
+    for (int d = 0; d < g.ndev; ++d) {
+        Dev& dv = g.dev[d];
+        if (dv.herr[0] == 0) continue;
+        const uint32_t n = dv.herr[0], tile = dv.herr[1];
+        if ((rc = use_dev(dv))) return rc;
+        HIP_TRY(hipMemsetAsync(dv.derr, 0, sizeof(uint32_t), dv.stream));
+        HIP_TRY(hipMemsetAsync(dv.derr + 1, 0xff, sizeof(uint32_t), dv.stream));
+        HIP_TRY(hipStreamSynchronize(dv.stream));
+        dv.herr[0] = 0;
+        return fail(PT_EKERNEL, "device %d: the ring pool's iteration guard abandoned %u tile(s) mid-pool (first: tile %u "
+                    "of its launch); the accumulator is invalid", dv.ordinal, n, tile);
     }
     return PT_OK;
 }
@@ -395,6 +424,8 @@ PtJob base_job(float* buf, int32_t w, int32_t h)
     j.units = nullptr;
     j.nunits = nullptr;
     j.cost = nullptr;
+    j.err = nullptr;
+    j.guard_cap = g.ring_guard_cap;
     j.scene = nullptr;
     return j;
 }
@@ -477,6 +508,13 @@ int slot_event(Dev& dv, unsigned slot)
     return PT_OK;
 }
 
+// The event ordering the last use of ring slot `slot` (nullptr: never used).
+hipEvent_t slot_order(const Dev& dv, unsigned slot)
+{
+    const int a = dv.queue_alias[slot];
+    return a >= 0 ? dv.queue_event[a] : dv.queue_event[slot];
+}
+
 // The schedule and queue fields of a launch of geometry `key` on stream `st`.
 struct LaunchSched {
     unsigned slot = 0;   // tile-queue ring slot (queue_done after the launch)
@@ -489,7 +527,6 @@ struct LaunchSched {
 };
 int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls)
 {
-    int rc;
     *ls = LaunchSched{};
     if (Sched* s = find_sched(dv, key, st)) {
         // (re)build the schedule from the last launch's costs on the 2nd launch of a geometry and
@@ -519,23 +556,25 @@ int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls)
     // kernel) and this launch zeroes the slot after it with a memset on its own stream, so launches on
     // different streams overlap.  A slot whose previous user ran on another stream is waited for
     // before it is zeroed or used.
+    // Nothing is ever enqueued on a stream other than `st` (a previous launch's stream may be a
+    // caller's stream that has been destroyed since): the skipped slot takes the previous slot's
+    // event, recorded by queue_done right after the launch whose kernel zeroes it.
     unsigned slot = dv.queue_next++ % kQueueRing;
     bool pre = dv.queue_pre_zeroed;
     if (pre && dv.last_stream != st) {
         const unsigned prev = (slot + kQueueRing - 1) % kQueueRing;
-        if ((rc = slot_event(dv, slot))) return rc;
-        HIP_TRY(hipEventRecord(dv.queue_event[slot], dv.queue_stream[prev]));   // after the zeroing kernel
+        dv.queue_alias[slot] = (int16_t)prev;
         dv.queue_stream[slot] = dv.queue_stream[prev];
         slot = dv.queue_next++ % kQueueRing;
         pre = false;
     }
     ls->slot = slot;
-    if (dv.queue_event[slot] && dv.queue_stream[slot] != st) HIP_TRY(hipStreamWaitEvent(st, dv.queue_event[slot], 0));
+    if (hipEvent_t ev = slot_order(dv, slot); ev && dv.queue_stream[slot] != st) HIP_TRY(hipStreamWaitEvent(st, ev, 0));
     ls->queue = dv.dqueue + (size_t)slot * PT_QUEUE_WORDS;
     if (!pre) HIP_TRY(hipMemsetAsync(ls->queue, 0, PT_QUEUE_WORDS * sizeof(unsigned), st));
     dv.queue_pre_zeroed = false;   // (set by queue_done once this launch's kernel is enqueued)
     const unsigned next = (slot + 1) % kQueueRing;
-    if (dv.queue_event[next] && dv.queue_stream[next] != st) HIP_TRY(hipStreamWaitEvent(st, dv.queue_event[next], 0));
+    if (hipEvent_t ev = slot_order(dv, next); ev && dv.queue_stream[next] != st) HIP_TRY(hipStreamWaitEvent(st, ev, 0));
     ls->queue_next = dv.dqueue + (size_t)next * PT_QUEUE_WORDS;
     return PT_OK;
 }
@@ -548,6 +587,7 @@ int queue_done(Dev& dv, unsigned slot, hipStream_t st, bool zeroed_next)
     if ((rc = slot_event(dv, slot))) return rc;
     HIP_TRY(hipEventRecord(dv.queue_event[slot], st));
     dv.queue_stream[slot] = st;
+    dv.queue_alias[slot] = -1;
     dv.queue_pre_zeroed = zeroed_next;
     dv.last_stream = st;
     return PT_OK;
@@ -565,6 +605,7 @@ int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
     j.units = ls.units;
     j.nunits = ls.nunits;
     j.cost = ls.cost;
+    j.err = dv.derr;
     hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
     return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_render's early return)
@@ -687,7 +728,7 @@ int render_frame(float* buf, PtJob j, int32_t row_align)
     if (banded) {
         g.frame += spf;
         HIP_TRY(hipStreamSynchronize(g.s_out));
-        return PT_OK;
+        return sync_all();
     }
     const Geo geo = geo_of(j.width, j.height, j.layout, j.tile_w, j.tile_h);
     if ((rc = stage_in(buf, geo, Region{}))) return rc;
@@ -1012,6 +1053,8 @@ void free_dev(Dev& dv)
     if (dv.stream) (void)hipStreamSynchronize(dv.stream);
     if (dv.dbuf) (void)hipFree(dv.dbuf);
     if (dv.dcounters) (void)hipFree(dv.dcounters);
+    if (dv.derr) (void)hipFree(dv.derr);
+    if (dv.herr) (void)hipHostFree(dv.herr);
     if (dv.dscene) (void)hipFree(dv.dscene);
     if (dv.dqueue) (void)hipFree(dv.dqueue);
     if (dv.denv) (void)hipFree(dv.denv);
@@ -1029,10 +1072,18 @@ int init_dev(Dev& dv, int32_t ordinal)
 {
     dv = Dev{};
     dv.ordinal = ordinal;
+    for (int16_t& a : dv.queue_alias) a = -1;
     HIP_TRY(hipSetDevice(ordinal));
     HIP_TRY(hipStreamCreateWithFlags(&dv.stream, hipStreamNonBlocking));
     if (hipMalloc(&dv.dcounters, kCounterSlots * sizeof(unsigned long long)) != hipSuccess)
         return fail(PT_ENOMEM, "hipMalloc(counters) failed");
+    if (hipMalloc(&dv.derr, PT_ERR_WORDS * sizeof(uint32_t)) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc(err) failed");
+    if (hipHostMalloc(&dv.herr, PT_ERR_WORDS * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
+        return fail(PT_ENOMEM, "hipHostMalloc(err) failed");
+    HIP_TRY(hipMemset(dv.derr, 0, sizeof(uint32_t)));
+    HIP_TRY(hipMemset(dv.derr + 1, 0xff, sizeof(uint32_t)));
+    dv.herr[0] = 0;
+    dv.herr[1] = ~0u;
     if (hipMalloc(&dv.dqueue, (size_t)kQueueRing * PT_QUEUE_WORDS * sizeof(unsigned)) != hipSuccess)
         return fail(PT_ENOMEM, "hipMalloc(queue) failed");
     if (hipMalloc(&dv.dscene, sizeof(PtScene)) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc(scene) failed");
@@ -1110,6 +1161,11 @@ int pt_init(const pt_config* cfg)
     }
     HIP_TRY(hipEventCreateWithFlags(&g.ev_q, hipEventDisableTiming));
     g.frame = 0;
+    g.ring_guard_cap = ~0u;
+    if (const char* cap = getenv("PT_MI355_RING_GUARD_CAP")) {
+        const unsigned long v = strtoul(cap, nullptr, 10);
+        if (v > 0 && v < 0xfffffffful) g.ring_guard_cap = (uint32_t)v;
+    }
     g.inited = true;
     return PT_OK;
 }
@@ -1223,7 +1279,7 @@ int pt_render_simt_textured(float* buf, int32_t w, int32_t h, int32_t ntx, int32
     if (banded) {
         g.frame += spf;
         HIP_TRY(hipStreamSynchronize(g.s_out));
-        return PT_OK;
+        return sync_all();
     }
     const Geo geo = geo_of(w, h, j.layout, tw, th);
     if ((rc = stage_in(buf, geo, Region{}))) return rc;
@@ -1428,6 +1484,7 @@ int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
 #if PT_DIAG
     diag_dump(h);
 #endif
+    if ((rc = sync_all())) return rc;   // the launch's error words
     out->segments = h[PT_CNT_SEGMENTS];
     out->lane_slots = h[PT_CNT_LANE_SLOTS];
     out->samples = h[PT_CNT_SAMPLES];
@@ -1437,6 +1494,13 @@ int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
     out->sphere_fallbacks = 0;
     out->sky_skipped = h[PT_CNT_SKY];
     return PT_OK;
+}
+
+int pt_check_device_errors(void)
+{
+    if (!g.inited) return PT_OK;
+    DeviceGuard guard;
+    return sync_all();
 }
 
 int32_t pt_initialized_device(void) { return g.inited ? g.dev[0].ordinal : -1; }
@@ -1632,8 +1696,7 @@ int pt_render_opt_v4(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty,
     }
     if (banded) {
         HIP_TRY(hipStreamSynchronize(g.s_out));
-        HIP_TRY(hipStreamSynchronize(g.dev[0].stream));
-        return PT_OK;
+        return sync_all();
     }
     return stage_out(buf, geo, Region{});
 }

@@ -45,11 +45,16 @@ struct PtJob {
     const uint32_t* units;         // schedule runs: unit k = positions [units[k], units[k+1]), nullptr = one tile each
     const uint32_t* nunits;        // device word: number of units (with units)
     uint32_t* cost;                // per-tile work of this launch (trace iterations), nullptr = not recorded
+    uint32_t* err;                 // PT_ERR_WORDS: [0] tiles abandoned by the ring pool's iteration guard,
+                                   // [1] the smallest such tile index (~0u: none); nullptr = not recorded
+    uint32_t guard_cap;            // upper limit of the ring pool's iteration guard: ~0u (tests lower it)
     // mainImage's frame constants (scalar.cpp:338-347), set by pt_launch_render on the host with the
     // same correctly rounded f32 operations: W, H, 1/W, 1/H, W/H, 1/(W/H).  Kernel arguments are
     // scalar registers; computed in the kernel they were VGPRs that the tile loop spilled.
     float cam_W, cam_H, cam_yW, cam_yH, cam_aspect, cam_yAspect;
 };
+
+#define PT_ERR_WORDS 2
 
 // Tile queues: one counter per XCD group, 128 B apart (PT_QUEUE_WORDS u32 per launch).
 #ifndef PT_NQUEUES

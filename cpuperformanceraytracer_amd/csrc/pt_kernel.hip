@@ -812,6 +812,15 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             int bounce = 0;   // 0: no item
             int it_addr = 0;  // the item's colour slot (floats from col_lds)
             const uint64_t live = pt_ballot(true);
+            // iteration guard: every item ends after <= B + 1 segments and a pool of `total` items
+            // drains in < total (B + 2) + S iterations.  The bound is formed in 64 bits (total can be
+            // 2^30 and B 1024) and clamped to what the 32-bit iteration count can reach, so it never
+            // fires early; if it fires (a scheduling fault) the tile is abandoned mid-pool, which the
+            // job's error words record (the host returns PT_EKERNEL naming the tile) instead of
+            // hanging the GPU.
+            // (job.guard_cap: ~0u, or a low test value -- PT_MI355_RING_GUARD_CAP -- that makes it fire)
+            const uint64_t guard64 = (uint64_t)total * (uint64_t)(B + 2) + (uint64_t)S + 64u;
+            const uint32_t guard_lim = guard64 < (uint64_t)job.guard_cap ? (uint32_t)guard64 : job.guard_cap;
             while (true) {
                 const bool had = bounce != 0;
                 const uint64_t idle = pt_ballot(!had);
@@ -864,10 +873,13 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                     }
                 }
                 if ((live & ~idle) == 0 && ntaken == 0 && folded >= total) break;
-                // (a guard, never reached: every item ends after <= B + 1 segments and a pool of `total`
-                // items drains in < total (B + 2) + S iterations -- a scheduling fault ends the tile
-                // with a wrong image, not a hung GPU)
-                if (__builtin_expect(tile_work > (uint32_t)total * (uint32_t)(B + 2) + (uint32_t)S + 64u, 0)) break;
+                if (__builtin_expect(tile_work > guard_lim, 0)) {   // (never reached, see guard_lim)
+                    if (lane == 0 && job.err) {
+                        atomicAdd(&job.err[0], 1u);           // abandoned tiles
+                        atomicMin(&job.err[1], this_tile);     // the first of them
+                    }
+                    break;
+                }
                 ++tile_work;
                 if (COUNT) ++n_iter;
                 if (had || took) {

@@ -85,6 +85,12 @@ def count_device(buf, width: int, height: int, *, frame_first: int, nframes: int
             "primary": out.primary, "quad_fallbacks": out.quad_fallbacks, "sky_skipped": out.sky_skipped}
 
 
+def check_device_errors() -> None:
+    """Raise PtError(PT_EKERNEL) if a device-resident launch since the last check abandoned a tile
+    (pt_check_device_errors).  Call after synchronising the streams the jobs ran on."""
+    N.check(N.load().pt_check_device_errors(), "pt_check_device_errors")
+
+
 def render_v4_device(buf, width: int, height: int, *, frame_first: int, nframes: int, num_bounces: int = 8,
                      row_start: int = 0, row_stride: int = 1, nrows: int | None = None,
                      layout: int = N.PT_LAYOUT_INTERLEAVED, use_env: bool = False, stream=None) -> None:

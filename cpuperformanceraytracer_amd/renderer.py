@@ -73,19 +73,25 @@ def _buf(a: np.ndarray, width: int, height: int, num_channels: int) -> int:
     return a.ctypes.data
 
 
-def init(num_bounces: int = 4, samples_per_frame: int = 1, ambient=(0.1, 0.1, 0.1), device: int = 0,
+def init(num_bounces: int = 4, samples_per_frame: int = 1, ambient=(0.1, 0.1, 0.1), device: int | None = None,
          defer_readback: bool = False, pin_host: bool = False, devices=None) -> None:
     """(Re)initialise the backend: the runtime form of the reference's compile-time settings
     (c_numBounces scalar.cpp:19, NUM_SAMPLES_PER_FRAME global_preprocessor_flags.h:30).
     Resets the frame counter to 0, like a fresh process of the reference.
     pin_host: page-lock the frame buffer and overlap its transfers with rendering (row bands).
     devices: several HIP devices (ordinals may repeat: logical shards of one GPU) that every frame
-    call deals its rows to (row Y -> devices[Y % len]); None: `device` alone (or PT_MI355_DEVICES)."""
+    call deals its rows to (row Y -> devices[Y % len]).  device: that one HIP device alone -- an
+    explicit device overrides PT_MI355_DEVICES (a rank of bench.py / shard.py initialises only its
+    own GPU).  Neither: PT_MI355_DEVICES, else device 0."""
+    if device is not None and devices is not None:
+        raise N.PtError(N.PT_EINVAL, "init", "pass device or devices, not both")
     L = N.load()
     c = N.PtConfig()
     L.pt_default_config(ctypes.byref(c))
-    if devices is None and c.device_count <= 1:
+    if device is not None:
         c.device = device
+        c.device_count = 1
+        c.devices[0] = device
     if devices is not None:
         devices = list(devices)
         if not 1 <= len(devices) <= N.PT_MAX_DEVICES:

@@ -30,6 +30,8 @@ extern "C" {
 #define PT_EHIP (-2)     /* HIP runtime error (no device, launch failure, ...)                     */
 #define PT_ENOMEM (-3)   /* device allocation failed                                               */
 #define PT_ESTATE (-4)   /* call out of order (e.g. readback without a deferred buffer)            */
+#define PT_EKERNEL (-5)  /* a kernel abandoned work (the ring pool's iteration guard fired on a    */
+                         /* tile): the accumulator it wrote is invalid; pt_last_error names the tile */
 
 /* Buffer layouts written by the reference's three frame functions. */
 #define PT_LAYOUT_INTERLEAVED 0    /* DemofoxRenderScalar: RGB of pixel (X,Y) at 3*(Y*W+X)+c          */
@@ -160,6 +162,10 @@ int pt_release_buffer(const void* buf);
 /* the (first) HIP device the library state lives on, or -1 before pt_init (a device job on a device
  * the library was not initialised with is an error, not a re-initialisation) */
 int32_t pt_initialized_device(void);
+/* Device-resident jobs (pt_render_device, ...) return when launched.  After synchronising the streams
+ * they ran on, this reports PT_EKERNEL if any launch since the last check abandoned a tile (every
+ * host-buffer entry point makes the same check before it returns). */
+int pt_check_device_errors(void);
 int32_t pt_device_count(void);               /* logical devices (0 before pt_init)             */
 int32_t pt_device_ordinal(int32_t index);    /* HIP ordinal of logical device `index`, or -1    */
 

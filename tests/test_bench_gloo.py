@@ -98,3 +98,67 @@ def test_bench_n_rank_path_gloo(scaling):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     # the verified frame range ends where the timed steps end (1 warm-up + 2 timed steps)
     assert res["verified"]["frames"] == [1, 3 * wl.spp]
+
+
+# ---- `python bench.py --gpus N` without a launcher: bench.spawn_ranks starts the N ranks itself ----
+def test_spawn_ranks_runs_the_n_rank_path(capfd):
+    """The driver's plain invocation with N > 1 (no torch.distributed.run): spawn_ranks gives each
+    rank the launcher's environment, the ranks rendezvous (gloo here, RCCL on the GPUs), and rank 0's
+    JSON line is the output -- the weak-scaling image gathered and verified bit for bit."""
+    import hashlib
+    import json
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+    from cpuperformanceraytracer_amd.config import Workload
+    from oracle import pyoracle
+    worker = str(Path(__file__).resolve().parent / "bench_rank_worker.py")
+    rc = bench.spawn_ranks(2, ["64", "36", "3", "8", "weak"], script=worker)
+    out = [ln for ln in capfd.readouterr().out.splitlines() if ln.startswith("{")]   # (gloo logs a line too)
+    assert rc == 0
+    assert len(out) == 1, out                      # one JSON line, from rank 0 only
+    res = json.loads(out[0])
+    assert res["n_gpus"] == 2 and res["scaling"] == "weak" and res["verified"]["bit_exact"]
+    wl = Workload("tiny", 64, 36, 3, 8, scaling="weak")
+    Wg, Hg = bench.job_image(wl, 2)
+    ref = pyoracle.render(Wg, Hg, frame_first=1, nframes=5 * wl.spp, num_bounces=8, row_start=0, row_stride=2,
+                          nrows=(Hg + 1) // 2, nthreads=2)
+    assert res["acc_sha256"] == hashlib.sha256(_pad(ref, Hg, Wg)).hexdigest()
+
+
+def _pad(ref, Hg, Wg):
+    """rank 0's accumulator: max_rows(2, Hg) rows of which its (Hg + 1) // 2 rows are rendered."""
+    from cpuperformanceraytracer_amd.shard import max_rows
+    buf = np.zeros((max_rows(2, Hg), Wg, 3), np.float32)
+    buf[:ref.shape[0]] = ref
+    return buf.tobytes()
+
+
+def test_spawn_ranks_reports_a_failed_rank():
+    """A rank that dies makes spawn_ranks end the others (waiting in the rendezvous) and return its
+    exit code instead of hanging."""
+    import sys
+    import time
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+    worker = str(Path(__file__).resolve().parent / "bench_rank_worker.py")
+    t0 = time.time()
+    rc = bench.spawn_ranks(2, ["64", "36", "3", "8", "weak", "1"], script=worker)
+    assert rc == 3 and time.time() - t0 < 120
+
+
+def test_main_dispatches_to_spawn_ranks(monkeypatch):
+    """bench.main with --gpus N > 1 and no WORLD_SIZE goes to spawn_ranks before touching a GPU."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+    seen = {}
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "spawn_ranks", lambda n, argv, script=None: seen.update(n=n, argv=argv) or 7)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    with pytest.raises(SystemExit) as ei:
+        bench.main()
+    assert ei.value.code == 7 and seen == {"n": 4, "argv": ["--gpus", "4", "--steps", "3"]}

@@ -8,7 +8,8 @@
   written back; the same address with another size is a new buffer;
 * device jobs alternating between two HIP streams for more launches than the tile-queue ring has
   slots: a slot reused across streams waits for its previous launch (event-ordered);
-* a device job on a device other than the initialised one is an error, not a silent re-init.
+* a device job on a device other than the initialised one is an error, not a silent re-init;
+* a caller's stream destroyed between launches; the ring pool's guard reported as PT_EKERNEL.
 All results bit-exact against the CPU oracle (oracle/pt_oracle.c).
 """
 from __future__ import annotations
@@ -178,3 +179,65 @@ def test_job_on_other_device_is_an_error():
     assert pt.initialized_device() == 0 and pt.get_frame() == 7
     pt.shutdown()
     assert pt.initialized_device() is None
+
+
+class _RawStream:
+    """A HIP stream the test creates and destroys itself (torch pools its streams: never destroyed)."""
+    def __init__(self, handle: int):
+        self.cuda_stream = handle
+
+
+def test_destroyed_stream_between_launches():
+    """A caller's stream destroyed between device launches on different streams: the
+    library never enqueues work on a previous launch's stream, so the next launch on a new stream
+    neither fails nor waits on a dead handle.  256x256 = 1024 tiles: the scheduled path with
+    tile-queue ring slots skipped on every change of stream."""
+    import ctypes
+    from cpuperformanceraytracer_amd.device import check_device_errors, render_device
+    pt.shutdown()
+    hip = ctypes.CDLL("libamdhip64.so.7")   # the HIP runtime torch loaded (same soname)
+    w, h, b, n = 256, 256, 4, 6
+    buf = torch.zeros(h * w * 3, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    for f in range(n):
+        st = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+        render_device(buf, w, h, frame_first=f + 1, nframes=1, num_bounces=b, stream=_RawStream(st.value))
+        assert hip.hipStreamSynchronize(st) == 0
+        assert hip.hipStreamDestroy(st) == 0
+    torch.cuda.synchronize()
+    check_device_errors()
+    ref = pyoracle.render(w, h, nframes=n, num_bounces=b)
+    got = buf.cpu().numpy().reshape(h, w, 3)
+    assert bits_equal(got, ref), mismatch_report(got, ref)
+    pt.shutdown()
+
+
+def test_ring_guard_fires_loudly(monkeypatch):
+    """The ring pool's iteration guard (pt_kernel.hip RING) abandons a tile only on a scheduling
+    fault; when it fires, no call returns success: the host-buffer call that waited for the launch
+    raises PtError(PT_EKERNEL) naming the tile, and device jobs report it through
+    pt_check_device_errors.  PT_MI355_RING_GUARD_CAP (read by pt_init) lowers the guard so that it
+    fires on a correct launch; errors are reported once, then the library works normally."""
+    from cpuperformanceraytracer_amd.device import check_device_errors, render_device
+    w, h, f = 64, 64, 49                      # >= 48 frames: one ring-pool launch
+    monkeypatch.setenv("PT_MI355_RING_GUARD_CAP", "8")
+    pt.init(num_bounces=8, samples_per_frame=f)
+    buf = np.zeros((h, w, 3), np.float32)
+    with pytest.raises(N.PtError) as ei:
+        pt.DemofoxRenderScalar(buf, w, h, 3)
+    assert ei.value.code == N.PT_EKERNEL and "tile" in str(ei.value), str(ei.value)
+    dev = torch.zeros(h * w * 3, dtype=torch.float32, device="cuda")
+    render_device(dev, w, h, frame_first=1, nframes=f, num_bounces=8)   # returns when launched
+    torch.cuda.synchronize()
+    with pytest.raises(N.PtError) as ei:
+        check_device_errors()
+    assert ei.value.code == N.PT_EKERNEL
+    check_device_errors()                     # reported once
+    monkeypatch.delenv("PT_MI355_RING_GUARD_CAP")
+    pt.init(num_bounces=8, samples_per_frame=f)
+    buf[:] = 0
+    pt.DemofoxRenderScalar(buf, w, h, 3)       # the normal guard never fires
+    ref = pyoracle.render(w, h, nframes=f, num_bounces=8)
+    assert bits_equal(buf, ref), mismatch_report(buf, ref)
+    pt.shutdown()
