@@ -473,10 +473,13 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
                       "(roofline.py, counted by oracle/pt_oracle_v4.c)")
         kernel_name = "pt_v4_kernel<EQUIRECT, INTERLEAVED>"
     else:
-        flops_launch = RL.launch_flops_alg(segs, samples) / K * per_rank
-        flops_launch_ref = RL.launch_flops_ref(segs, prim, samples) / K * per_rank
-        flop_model = ("algorithmic (SURVEY.md §8d) = device-counted segments x F_SEGMENT + samples x F_SAMPLE; "
-                      f"F = {RL.F_SEGMENT}/{RL.F_SAMPLE} (roofline.py; a pixel's camera ray is one segment)")
+        env_esc = escaped if wl.env else 0
+        flops_launch = RL.launch_flops_alg(segs, samples, env_esc) / K * per_rank
+        flops_launch_ref = RL.launch_flops_ref(segs, prim, samples, env_esc) / K * per_rank
+        flop_model = ("algorithmic (SURVEY.md §8d) = device-counted segments x F_SEGMENT + samples x F_SAMPLE"
+                      + (" + escaped paths x F_ENV_ESCAPE" if wl.env else "") +
+                      f"; F = {RL.F_SEGMENT}/{RL.F_SAMPLE}" + (f"/{RL.F_ENV_ESCAPE}" if wl.env else "") +
+                      " (roofline.py; a pixel's camera ray is one segment)")
         kernel_name = "pt_render_env_kernel<INTERLEAVED>" if wl.env else "pt_render_kernel<INTERLEAVED>"
     achieved_tf = flops_launch / avg_kernel_s / 1e12
     pmc = load_pmc(wl.name) if roofline else {}

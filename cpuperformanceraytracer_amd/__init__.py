@@ -43,6 +43,7 @@ from .renderer import (  # noqa: F401
     initialized_devices,
     make_tiles,
     readback,
+    gather_root,
     set_env_map,
     set_frame,
     shutdown,
@@ -57,7 +58,7 @@ from .renderer import (  # noqa: F401
 __all__ = [
     "CONFIGS", "Workload", "check_valid_settings", "BeginFrame", "CopyOutputToFile", "DemofoxRenderScalar", "DemofoxRenderSimd",
     "DemofoxRenderSimdTiled", "DemofoxRenderSimtTextured", "LoadTexture", "RenderBufferInfo", "RenderTile", "RenderTileInfo", "get_frame", "init",
-    "make_tiles", "readback", "set_env_map", "set_frame", "shutdown", "texture", "tonemap", "WriteImage",
+    "make_tiles", "readback", "gather_root", "set_env_map", "set_frame", "shutdown", "texture", "tonemap", "WriteImage",
     "DemofoxRenderOptV4", "InitializeGlobalRenderResources", "ReinitializeRenderTileData", "InitializeScene",
     "ClearScene", "AddMaterialToScene", "AddQuadObjectToScene", "AddSphereObjectToScene", "LoadCubemapTexture",
     "v4_config", "v4_begin_frame", "v4_get_frame", "v4_set_frame", "MakeWorkQueue", "AddWorkQueueEntry",

@@ -95,6 +95,12 @@ struct Dev {
     size_t dtone_in_cap = 0;
     uint32_t* dtone_out = nullptr;
     size_t dtone_out_cap = 0;
+    // PT_FLAG_GATHER_ROOT: the root (device 0) assembles the whole accumulator from every device's
+    // rows -- each device stores its rows into dgather of the root over xGMI (peer access)
+    float* dgather = nullptr;           // root only: W x H x 3
+    size_t dgather_cap = 0;
+    hipEvent_t ev_gather = nullptr;     // recorded after this device's rows were stored
+    bool peer_root = false;             // this device may store into the root's memory
 };
 
 // The host buffer the device mirrors currently represent, and the geometry they were split by.
@@ -125,6 +131,7 @@ struct State {
     hipStream_t s_in = nullptr, s_out = nullptr;
     hipEvent_t ev_in[kBands] = {}, ev_done[kBands] = {};
     hipEvent_t ev_q = nullptr;          // work queues: orders banded copies against the stream
+    hipEvent_t ev_root_free = nullptr;  // PT_FLAG_GATHER_ROOT: the root's earlier reads of dgather are done
     // v4 renderer (demofox_path_tracing_optimization_v4.cpp): its own iFrame (v4 :34) and scene
     pt_v4_config v4cfg{PT_V4_ENV_EQUIRECT, 1, 1, 8, 1, 1, 1, 1, 1};
     bool v4_scene_ready = false;
@@ -819,6 +826,71 @@ int tone_mirror(int32_t layout, int32_t tw, int32_t th, uint32_t* out, int32_t f
     return PT_OK;
 }
 
+// PT_FLAG_GATHER_ROOT (several devices, deferred accumulator): assemble the whole accumulator of the
+// mirrored buffer in the root's dgather.  Every device stores its own rows there (a kernel on its own
+// stream, after its renders; remote stores over its xGMI link), then the root stream waits for all of
+// them.  *out = the assembled W x H x 3 buffer (mirror layout) on the root, ordered on its stream.
+int gather_root(float** out)
+{
+    int rc;
+    const Geo geo = mirror_geo();
+    const int n = g.ndev;
+    Dev& r = g.dev[0];
+    if ((rc = use_dev(r))) return rc;
+    if (n == 1) {
+        *out = r.dbuf;
+        return PT_OK;
+    }
+    for (int d = 1; d < n; ++d)
+        if (!g.dev[d].peer_root)
+            return fail(PT_ESTATE, "PT_FLAG_GATHER_ROOT: device %d has no peer access to device %d", g.dev[d].ordinal,
+                        r.ordinal);
+    const size_t bytes = (size_t)geo.w * geo.h * 3 * sizeof(float);
+    if ((rc = grow(r, (void**)&r.dgather, &r.dgather_cap, bytes))) return rc;
+    HIP_TRY(hipEventRecord(g.ev_root_free, r.stream));   // (the root's earlier tonemap / copy of dgather)
+    for (int d = 0; d < n; ++d) {
+        Dev& dv = g.dev[d];
+        if ((rc = use_dev(dv))) return rc;
+        if (d > 0) HIP_TRY(hipStreamWaitEvent(dv.stream, g.ev_root_free, 0));
+        PtScatterJob j{};
+        j.src = dv.dbuf;
+        j.dst = r.dgather;
+        j.width = geo.w;
+        j.height = geo.h;
+        j.layout = geo.tiled ? PT_LAYOUT_TILED_PLANAR8 : PT_LAYOUT_INTERLEAVED;   // (planar8 rows: same bytes)
+        j.tile_w = geo.tw;
+        j.tile_h = geo.th;
+        j.dev = d;
+        j.ndev = n;
+        j.nrows = shard_rows(geo.h, n, d);
+        hipError_t e = pt_launch_scatter_rows(j, dv.stream);
+        if (e != hipSuccess) return fail(PT_EHIP, "gather launch failed: %s", hipGetErrorString(e));
+        if (d > 0) HIP_TRY(hipEventRecord(dv.ev_gather, dv.stream));
+    }
+    if ((rc = use_dev(r))) return rc;
+    for (int d = 1; d < n; ++d) HIP_TRY(hipStreamWaitEvent(r.stream, g.dev[d].ev_gather, 0));
+    *out = r.dgather;
+    return PT_OK;
+}
+
+// The output stage of the deferred accumulator into host pixels: per device on its own rows, or
+// (PT_FLAG_GATHER_ROOT) gathered on the root and converted there.  Enqueued; the caller synchronises.
+int tone_output(int32_t layout, int32_t tw, int32_t th, uint32_t* out, int32_t format)
+{
+    int rc;
+    if (g.ndev == 1 || !(g.cfg.flags & PT_FLAG_GATHER_ROOT)) return tone_mirror(layout, tw, th, out, format);
+    float* acc = nullptr;
+    if ((rc = gather_root(&acc))) return rc;
+    Dev& r = g.dev[0];
+    const int32_t w = g.m.width, h = g.m.height;
+    if ((rc = grow(r, (void**)&r.dtone_out, &r.dtone_out_cap, (size_t)w * h * sizeof(uint32_t)))) return rc;
+    const PtToneJob j = tone_job(acc, w, h, layout, tw, th, r.dtone_out, format);
+    hipError_t e = pt_launch_tonemap(j, r.stream);
+    if (e != hipSuccess) return fail(PT_EHIP, "tonemap launch failed: %s", hipGetErrorString(e));
+    HIP_TRY(hipMemcpyAsync(out, r.dtone_out, (size_t)w * h * sizeof(uint32_t), hipMemcpyDeviceToHost, r.stream));
+    return PT_OK;
+}
+
 int check_frame_args(const float* buf, int32_t w, int32_t h, int32_t nc)
 {
     if (!buf) return fail(PT_EINVAL, "null buffer");
@@ -1060,6 +1132,8 @@ void free_dev(Dev& dv)
     if (dv.denv) (void)hipFree(dv.denv);
     if (dv.dtone_in) (void)hipFree(dv.dtone_in);
     if (dv.dtone_out) (void)hipFree(dv.dtone_out);
+    if (dv.dgather) (void)hipFree(dv.dgather);
+    if (dv.ev_gather) (void)hipEventDestroy(dv.ev_gather);
     for (Sched& sc : dv.sched)
         if (sc.used) free_sched(sc);
     for (hipEvent_t& e : dv.queue_event)
@@ -1087,6 +1161,7 @@ int init_dev(Dev& dv, int32_t ordinal)
     if (hipMalloc(&dv.dqueue, (size_t)kQueueRing * PT_QUEUE_WORDS * sizeof(unsigned)) != hipSuccess)
         return fail(PT_ENOMEM, "hipMalloc(queue) failed");
     if (hipMalloc(&dv.dscene, sizeof(PtScene)) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc(scene) failed");
+    HIP_TRY(hipEventCreateWithFlags(&dv.ev_gather, hipEventDisableTiming));
     HIP_TRY(hipMemcpy(dv.dscene, &g.scene, sizeof(PtScene), hipMemcpyHostToDevice));
     return PT_OK;
 }
@@ -1152,7 +1227,22 @@ int pt_init(const pt_config* cfg)
             pt_shutdown();
             return rc;
         }
+    // peer access to the root for PT_FLAG_GATHER_ROOT (MI355X nodes: every GPU pair over xGMI)
+    for (int d = 0; d < g.ndev; ++d) {
+        Dev& dv = g.dev[d];
+        if (dv.ordinal == g.dev[0].ordinal) {
+            dv.peer_root = true;
+            continue;
+        }
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, dv.ordinal, g.dev[0].ordinal) != hipSuccess || !can) continue;
+        HIP_TRY(hipSetDevice(dv.ordinal));
+        const hipError_t e = hipDeviceEnablePeerAccess(g.dev[0].ordinal, 0);
+        if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) dv.peer_root = true;
+        (void)hipGetLastError();
+    }
     HIP_TRY(hipSetDevice(g.dev[0].ordinal));
+    HIP_TRY(hipEventCreateWithFlags(&g.ev_root_free, hipEventDisableTiming));
     HIP_TRY(hipStreamCreateWithFlags(&g.s_in, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&g.s_out, hipStreamNonBlocking));
     for (int k = 0; k < kBands; ++k) {
@@ -1182,6 +1272,7 @@ void pt_shutdown(void)
         if (g.ev_done[k]) (void)hipEventDestroy(g.ev_done[k]);
     }
     if (g.ev_q) (void)hipEventDestroy(g.ev_q);
+    if (g.ev_root_free) (void)hipEventDestroy(g.ev_root_free);
     if (g.s_in) (void)hipStreamDestroy(g.s_in);
     if (g.s_out) (void)hipStreamDestroy(g.s_out);
     g = State{};
@@ -1324,9 +1415,28 @@ int pt_readback(float* buf)
     DeviceGuard guard;
     int rc;
     const Geo geo = mirror_geo();
+    if (g.ndev > 1 && (g.cfg.flags & PT_FLAG_GATHER_ROOT)) {   // assembled on the root: one copy
+        float* acc = nullptr;
+        if ((rc = gather_root(&acc))) return rc;
+        HIP_TRY(hipMemcpyAsync(buf, acc, g.m.bytes, hipMemcpyDeviceToHost, g.dev[0].stream));
+        return sync_all();
+    }
     for (int d = 0; d < g.ndev; ++d)
         if ((rc = use_dev(g.dev[d])) || (rc = xfer(d, geo, buf, false, Region{}))) return rc;
     return sync_all();
+}
+
+int pt_gather_root(const float* buf, const float** device_accum)
+{
+    if (!device_accum) return fail(PT_EINVAL, "null output pointer");
+    if (!g.inited || !g.m.valid || buf != g.m.host)
+        return fail(PT_ESTATE, "no deferred device accumulator for this buffer");
+    DeviceGuard guard;
+    int rc;
+    float* acc = nullptr;
+    if ((rc = gather_root(&acc)) || (rc = sync_all())) return rc;
+    *device_accum = acc;
+    return PT_OK;
 }
 
 int pt_release_buffer(const void* buf)
@@ -1417,8 +1527,9 @@ int pt_tonemap(const float* accum, int32_t w, int32_t h, int32_t layout, int32_t
     const bool tiled = layout == PT_LAYOUT_TILED_PLANAR8;
     if (g.m.valid && accum == g.m.host && g.m.bytes == in_bytes && g.m.width == w && g.m.height == h &&
         (g.ndev == 1 || (g.m.tiled == tiled && (!tiled || (g.m.tile_w == tw && g.m.tile_h == th))))) {
-        // the deferred accumulator is already in HBM: each device converts its own rows
-        if ((rc = tone_mirror(layout, tw, th, out, format))) return rc;
+        // the deferred accumulator is already in HBM: each device converts its own rows (or the root
+        // converts the gathered image, PT_FLAG_GATHER_ROOT)
+        if ((rc = tone_output(layout, tw, th, out, format))) return rc;
         return sync_all();
     }
     Dev& dv = g.dev[0];
@@ -1690,7 +1801,7 @@ int pt_render_opt_v4(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty,
             hipError_t e = pt_launch_tonemap(tj, dv.stream);
             if (e != hipSuccess) return fail(PT_EHIP, "tonemap launch failed: %s", hipGetErrorString(e));
             HIP_TRY(hipMemcpyAsync(screen, dv.dtone_out, out_bytes, hipMemcpyDeviceToHost, dv.stream));
-        } else if ((rc = tone_mirror(PT_LAYOUT_TILED_PLANAR8, tw, th, (uint32_t*)screen, PT_PIXEL_XRGB8))) {
+        } else if ((rc = tone_output(PT_LAYOUT_TILED_PLANAR8, tw, th, (uint32_t*)screen, PT_PIXEL_XRGB8))) {
             return rc;
         }
     }

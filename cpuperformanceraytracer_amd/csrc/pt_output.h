@@ -18,3 +18,18 @@ struct PtToneJob {
 };
 
 hipError_t pt_launch_tonemap(const PtToneJob& job, hipStream_t stream);
+
+// Several devices, PT_FLAG_GATHER_ROOT: device `dev` of `ndev` writes the global rows it owns
+// (Y = dev + k * ndev) from its mirror into the root device's full-size accumulator -- remote stores
+// over xGMI (peer access), each device over its own link.  Row layouts: the mirror holds the rows
+// compactly; tiled layout: the mirror is full-size (same offsets as the root's).
+struct PtScatterJob {
+    const float* src;         // this device's mirror
+    float* dst;               // the root's W x H x 3 buffer
+    int32_t width, height;
+    int32_t layout;
+    int32_t tile_w, tile_h;   // PT_LAYOUT_TILED_PLANAR8
+    int32_t dev, ndev, nrows; // owned rows
+};
+
+hipError_t pt_launch_scatter_rows(const PtScatterJob& job, hipStream_t stream);

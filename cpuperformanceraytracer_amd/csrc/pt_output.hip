@@ -122,3 +122,45 @@ hipError_t pt_launch_tonemap(const PtToneJob& j, hipStream_t st)
         default: return hipErrorInvalidValue;
     }
 }
+
+// ---- PT_FLAG_GATHER_ROOT: a device's rows into the root's accumulator (pt_output.h) ----------------
+namespace {
+
+template <bool TILED>
+__global__ __launch_bounds__(256) void pt_scatter_rows_kernel(PtScatterJob j)
+{
+    const int32_t rowf = j.width * 3;   // floats of one image row in every layout
+    for (int32_t k = blockIdx.x; k < j.nrows; k += gridDim.x) {
+        const int32_t Y = j.dev + k * j.ndev;
+        if constexpr (!TILED) {
+            const float* s = j.src + (size_t)k * rowf;
+            float* d = j.dst + (size_t)Y * rowf;
+            for (int32_t i = threadIdx.x; i < rowf; i += blockDim.x) d[i] = s[i];
+        } else {   // simd_tiled.cpp:499-502 offsets: the row's segment in each tile of its tile row
+            const int32_t ty = Y / j.tile_h, ly = Y - ty * j.tile_h, segf = j.tile_w * 3;
+            const size_t base = (size_t)ty * j.tile_h * rowf + (size_t)ly * segf;
+            const size_t tilef = (size_t)j.tile_w * j.tile_h * 3;
+            for (int32_t i = threadIdx.x; i < rowf; i += blockDim.x) {
+                const int32_t tx = i / segf, r = i - tx * segf;
+                const size_t off = base + (size_t)tx * tilef + r;
+                j.dst[off] = j.src[off];
+            }
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t pt_launch_scatter_rows(const PtScatterJob& j, hipStream_t st)
+{
+    if (j.nrows <= 0 || j.width <= 0) return hipSuccess;
+    if (!j.src || !j.dst || j.ndev < 1 || j.dev < 0 || j.dev >= j.ndev) return hipErrorInvalidValue;
+    const unsigned blocks = (unsigned)std::min<int32_t>(j.nrows, 2048);
+    if (j.layout == PT_LAYOUT_TILED_PLANAR8) {
+        if (j.tile_w <= 0 || j.tile_h <= 0) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((pt_scatter_rows_kernel<true>), dim3(blocks), dim3(256), 0, st, j);
+    } else {
+        hipLaunchKernelGGL((pt_scatter_rows_kernel<false>), dim3(blocks), dim3(256), 0, st, j);
+    }
+    return hipGetLastError();
+}

@@ -74,7 +74,7 @@ def _buf(a: np.ndarray, width: int, height: int, num_channels: int) -> int:
 
 
 def init(num_bounces: int = 4, samples_per_frame: int = 1, ambient=(0.1, 0.1, 0.1), device: int | None = None,
-         defer_readback: bool = False, pin_host: bool = False, devices=None) -> None:
+         defer_readback: bool = False, pin_host: bool = False, devices=None, gather_root: bool = False) -> None:
     """(Re)initialise the backend: the runtime form of the reference's compile-time settings
     (c_numBounces scalar.cpp:19, NUM_SAMPLES_PER_FRAME global_preprocessor_flags.h:30).
     Resets the frame counter to 0, like a fresh process of the reference.
@@ -82,7 +82,9 @@ def init(num_bounces: int = 4, samples_per_frame: int = 1, ambient=(0.1, 0.1, 0.
     devices: several HIP devices (ordinals may repeat: logical shards of one GPU) that every frame
     call deals its rows to (row Y -> devices[Y % len]).  device: that one HIP device alone -- an
     explicit device overrides PT_MI355_DEVICES (a rank of bench.py / shard.py initialises only its
-    own GPU).  Neither: PT_MI355_DEVICES, else device 0."""
+    own GPU).  Neither: PT_MI355_DEVICES, else device 0.
+    gather_root (several devices, deferred): the output stage and readback assemble the accumulator on
+    devices[0] over xGMI first (PT_FLAG_GATHER_ROOT)."""
     if device is not None and devices is not None:
         raise N.PtError(N.PT_EINVAL, "init", "pass device or devices, not both")
     L = N.load()
@@ -102,7 +104,8 @@ def init(num_bounces: int = 4, samples_per_frame: int = 1, ambient=(0.1, 0.1, 0.
             c.devices[i] = d
     c.num_bounces = num_bounces
     c.samples_per_frame = samples_per_frame
-    c.flags = (N.PT_FLAG_DEFER_READBACK if defer_readback else 0) | (N.PT_FLAG_PIN_HOST if pin_host else 0)
+    c.flags = ((N.PT_FLAG_DEFER_READBACK if defer_readback else 0) | (N.PT_FLAG_PIN_HOST if pin_host else 0) |
+               (N.PT_FLAG_GATHER_ROOT if gather_root else 0))
     for i in range(3):
         c.ambient[i] = float(ambient[i])
     global _watch_buffers
@@ -154,6 +157,14 @@ def get_frame() -> int:
 def readback(BufferOut: np.ndarray) -> None:
     """defer_readback mode: copy the HBM-resident accumulator into BufferOut."""
     N.check(N.load().pt_readback(_buf(BufferOut, 0, 0, 0)), "pt_readback")
+
+
+def gather_root(BufferOut: np.ndarray) -> int:
+    """defer_readback mode: the accumulator of BufferOut assembled in the root device's HBM
+    (pt_gather_root); returns its device address (library-owned, valid until the next call)."""
+    p = ctypes.c_void_p()
+    N.check(N.load().pt_gather_root(_buf(BufferOut, 0, 0, 0), ctypes.byref(p)), "pt_gather_root")
+    return int(p.value)
 
 
 def DemofoxRenderScalar(BufferOut: np.ndarray, Width: int, Height: int, NumChannels: int) -> None:

@@ -55,9 +55,13 @@ PEAK_HBM_GBPS = 8000.0     # HBM3E spec peak (6.29 TB/s measured copy)
 
 # Algorithmic HBM bytes: the accumulator is read once and written once per launch.
 BYTES_PER_PIXEL_PER_LAUNCH = 24
-# Config 4: one RGB f32 texel gathered per escaping path (texture.cpp:8-13).  The env-sample
-# arithmetic (atan2f/asinf, ~40 FLOP) is not part of F_SEGMENT: the config-4 roofline under-counts.
+# Config 4: one RGB f32 texel gathered per escaping path (texture.cpp:8-13).
 BYTES_PER_ENV_GATHER = 12
+# Config 4: the env miss term's f32 arithmetic per escaping path (EquirectangularTextureSample's
+# per-lane body, texture.cpp:111-124): uv *= invAtan 2, + 0.5 2, fract 2, the four range compares,
+# the (H-1) / (W-1) scaling 2 = 12 FLOP, plus atan2f and asinf counted as 2 transcendentals like
+# sin/cos -- counted by the instrumented oracle (tests/test_flops.py).
+F_ENV_ESCAPE = 12.0
 
 
 def ref_segments(traced: int, camera_rays: int, samples: int) -> int:
@@ -65,13 +69,15 @@ def ref_segments(traced: int, camera_rays: int, samples: int) -> int:
     return traced - camera_rays + samples
 
 
-def launch_flops_ref(traced: int, camera_rays: int, samples: int) -> float:
-    return ref_segments(traced, camera_rays, samples) * F_SEGMENT + samples * F_SAMPLE
+def launch_flops_ref(traced: int, camera_rays: int, samples: int, env_escapes: int = 0) -> float:
+    return ref_segments(traced, camera_rays, samples) * F_SEGMENT + samples * F_SAMPLE + env_escapes * F_ENV_ESCAPE
 
 
-def launch_flops_alg(traced: int, samples: int) -> float:
-    """samples * F_SAMPLE + device-counted segments * F_SEGMENT."""
-    return traced * F_SEGMENT + samples * F_SAMPLE
+def launch_flops_alg(traced: int, samples: int, env_escapes: int = 0) -> float:
+    """samples * F_SAMPLE + device-counted segments * F_SEGMENT (+ config 4's env
+    arithmetic per escaping path, F_ENV_ESCAPE; the device counts escapes per sample, as the
+    reference evaluates them)."""
+    return traced * F_SEGMENT + samples * F_SAMPLE + env_escapes * F_ENV_ESCAPE
 
 
 # ---- v4 renderer (demofox_path_tracing_optimization_v4.cpp) ------------------------------------

@@ -55,6 +55,13 @@ extern "C" {
                                    /* pt_release_buffer(buf) (a Resize that reallocates it): the     */
                                    /* registration of a freed buffer cannot be detected reliably.    */
                                    /* One device only (several devices: the plain path).             */
+#define PT_FLAG_GATHER_ROOT 4u     /* several devices + PT_FLAG_DEFER_READBACK: the output stage    */
+                                   /* (pt_tonemap, v4 screen pixels, CopyOutputToFile) and            */
+                                   /* pt_readback first assemble the whole accumulator on the root    */
+                                   /* device (devices[0]): every device stores its rows there over     */
+                                   /* xGMI (peer access), the root converts / copies it once.  Off:   */
+                                   /* each device converts and copies its own rows over its own PCIe  */
+                                   /* link (faster for a host consumer).         */
 
 #define PT_MAX_DEVICES 16
 
@@ -152,6 +159,10 @@ int pt_render_tile(const pt_buffer_info* buffer, const pt_tile_info* tile);
 int pt_begin_frame(void);
 /* PT_FLAG_DEFER_READBACK: copy the device accumulator of `buf` back into it */
 int pt_readback(float* buf);
+/* PT_FLAG_DEFER_READBACK: the accumulator of `buf` assembled in the root device's HBM (devices[0];
+ * several devices: gathered over xGMI as for PT_FLAG_GATHER_ROOT).  *device_accum = a library-owned
+ * W x H x 3 f32 buffer in buf's layout, valid until the next call; synchronous. */
+int pt_gather_root(const float* buf, const float** device_accum);
 /* PT_FLAG_PIN_HOST: drop the page-lock of `buf` (NULL: of whichever buffer is pinned) before the
  * caller frees or reallocates it (Application.cpp:142-151 Resize).  No-op if it is not pinned. */
 int pt_unpin_host(const void* buf);

@@ -22,6 +22,22 @@ def test_flop_constants(w, h, rs, st, nr, frames):
     assert abs(f_shared - RL.F_SHARED) / RL.F_SHARED < 0.005, f_shared
 
 
+def test_env_flop_constant():
+    """Config 4: the env miss term adds F_ENV_ESCAPE FLOP (and 2 transcendentals) per escaping path,
+    on top of the ambient path's per-segment / per-sample figures (same paths: the env texture changes
+    only the radiance, never a path)."""
+    import numpy as np
+    env = np.random.default_rng(3).random((64, 128, 3), dtype=np.float32)
+    kw = dict(row_start=0, row_stride=8, nrows=60, nframes=1, num_bounces=8)
+    _, a = pyoracle.render_counted(640, 480, **kw)
+    _, e = pyoracle.render_counted(640, 480, env=env, **kw)
+    assert e["segments"] == a["segments"] and e["escaped"] == a["escaped"]
+    assert e["flops_segment"] - a["flops_segment"] == RL.F_ENV_ESCAPE * e["escaped"]
+    assert e["transcendentals"] - a["transcendentals"] == 2 * e["escaped"]
+    assert (RL.launch_flops_alg(e["segments"], e["samples"], e["escaped"]) -
+            RL.launch_flops_alg(a["segments"], a["samples"])) == RL.F_ENV_ESCAPE * e["escaped"]
+
+
 def test_algorithmic_flops_model():
     """samples * F_SAMPLE + device segments * F_SEGMENT; with one frame per pixel
     (camera rays traced once per sample) it equals the reference-equivalent work."""

@@ -163,13 +163,27 @@ def test_opt_v4_frames_screen_and_file(env_mode):
     assert np.array_equal(file_px.reshape(h, w), po.tonemap(ref, po.PIXEL_RGBA8))
 
 
+def _device_lists():
+    """Logical shards of GPU 0, and -- where the box has several GPUs -- every physical GPU (ADVICE r3:
+    hipSetDevice switching, per-device uploads and cross-device copies run only with distinct
+    ordinals)."""
+    import torch
+    lists = [[0, 0, 0]]
+    if torch.cuda.device_count() > 1:
+        lists.append(list(range(min(torch.cuda.device_count(), 8))))
+    return lists
+
+
+@pytest.mark.parametrize("devices", _device_lists(), ids=lambda d: "x".join(map(str, d)))
+@pytest.mark.parametrize("gather", [False, True], ids=["per_device", "gather_root"])
 @pytest.mark.parametrize("layout", ["scalar", "tiled", "v4"])
-def test_deferred_readback_and_tonemap(layout):
+def test_deferred_readback_and_tonemap(layout, gather, devices):
     """PT_FLAG_DEFER_READBACK: each device keeps its rows in HBM across calls; readback merges them,
-    the output stage converts each device's rows in place."""
+    the output stage converts each device's rows in place -- or, PT_FLAG_GATHER_ROOT, every device
+    stores its rows into the root's HBM (xGMI between GPUs) and the root converts / copies once."""
     w, h, ntx, nty = 240, 150, 6, 5
     tw, th = w // ntx, h // nty
-    pt.init(num_bounces=8, defer_readback=True, devices=[0, 0, 0])
+    pt.init(num_bounces=8, defer_readback=True, devices=devices, gather_root=gather)
     buf = np.zeros(w * h * 3, np.float32)
     if layout == "v4":
         pt.v4_config(env_mode=N.PT_V4_ENV_NONE)
@@ -185,6 +199,16 @@ def test_deferred_readback_and_tonemap(layout):
     lay, tws, ths = (N.PT_LAYOUT_INTERLEAVED, 0, 0) if layout == "scalar" else (N.PT_LAYOUT_TILED_PLANAR8, tw, th)
     px = pt.tonemap(buf, w, h, lay, tws, ths)      # from the device-resident accumulator
     assert np.array_equal(px, po.tonemap(ref, po.PIXEL_RGBA8))
+    if gather:   # the assembled accumulator in the root's HBM
+        import ctypes
+        dptr = pt.gather_root(buf)
+        host = np.zeros(w * h * 3, np.float32)
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        assert hip.hipMemcpy(ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(dptr), ctypes.c_size_t(host.nbytes),
+                             2) == 0   # hipMemcpyDeviceToHost
+        g = host.reshape(h, w, 3) if layout == "scalar" else tiled_to_interleaved(host, w, h, tw, th)
+        assert bits_equal(g, ref), mismatch_report(g, ref)
+        assert not buf.any()
     pt.readback(buf)
     got = buf.reshape(h, w, 3) if layout == "scalar" else tiled_to_interleaved(buf, w, h, tw, th)
     assert bits_equal(got, ref), mismatch_report(got, ref)
