@@ -614,8 +614,8 @@ def main() -> None:
     import torch.distributed as dist
 
     from cpuperformanceraytracer_amd.config import CONFIGS, synthetic_env
-    from cpuperformanceraytracer_amd.device import (count_device, count_v4_device, ensure_backend, render_device,
-                                                    render_v4_device, set_env_map)
+    from cpuperformanceraytracer_amd.device import (JobLauncher, check_device_errors, count_device, count_v4_device,
+                                                    ensure_backend, set_env_map)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -644,12 +644,20 @@ def main() -> None:
     if v4:
         from cpuperformanceraytracer_amd.renderer import v4_config
         v4_config(num_bounces=B)   # the reference's default flags (equirect, random jitter, rejection)
-    rfn, cfn = (render_v4_device, count_v4_device) if v4 else (render_device, count_device)
+    cfn = count_v4_device if v4 else count_device
     stream = torch.cuda.current_stream(dev)
 
+    # the step's launch through a prepared job (device.JobLauncher: only frame_first changes from
+    # step to step), so the host enqueues a step in a few microseconds
+    launchers = {}
+
     def render_fn(buf, Wg, Hg, f, n, rs, st, nr):
-        rfn(buf, Wg, Hg, frame_first=f, nframes=n, num_bounces=B, row_start=rs, row_stride=st, nrows=nr,
-            use_env=wl.env, stream=stream)
+        key = (buf.data_ptr(), Wg, Hg, n, rs, st, nr)
+        launch = launchers.get(key)
+        if launch is None:
+            launch = launchers[key] = JobLauncher(buf, Wg, Hg, nframes=n, num_bounces=B, row_start=rs, row_stride=st,
+                                                  nrows=nr, use_env=wl.env, stream=stream, v4=v4)
+        launch(f)
 
     def count_fn(buf, Wg, Hg, f, n, rs, st, nr):
         return cfn(buf, Wg, Hg, frame_first=f, nframes=n, num_bounces=B, row_start=rs, row_stride=st, nrows=nr,
@@ -657,6 +665,7 @@ def main() -> None:
 
     ops = DeviceOps(dev, stream)
     res = run(args, wl, rank, world, ops, render_fn, count_fn, rehearse=rehearse)
+    check_device_errors()   # no launch of the run abandoned a tile (PT_EKERNEL otherwise)
     if rank == 0:
         # the presented frame: rank 0's rendered accumulator (its first W x H pixels when sharded)
         W, H = wl.width, wl.height

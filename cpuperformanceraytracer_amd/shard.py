@@ -40,12 +40,12 @@ def gather_rows(sub, width: int, height: int, rank: int, world: int, dst: int = 
         raise ValueError(f"sub-image must hold {mr} rows of {width}x3 floats, got {sub.numel()}")
     if world == 1:
         return sub.view(height, width, 3)
-    chunks = [torch.empty_like(sub) for _ in range(world)] if rank == dst else None
+    # the root receives every rank's sub-image into one (world, mr, W*3) tensor; rank r's row k is the
+    # global row k * world + r, so the un-interleave is ONE transposing copy (world, mr) -> (mr, world)
+    stacked = torch.empty((world, mr, width * 3), dtype=sub.dtype, device=sub.device) if rank == dst else None
+    chunks = list(stacked.view(world, mr * width * 3).unbind(0)) if rank == dst else None
     dist.gather(sub, gather_list=chunks, dst=dst, group=group)
     if rank != dst:
         return None
-    full = torch.empty(height * width * 3, dtype=sub.dtype, device=sub.device).view(height, width * 3)
-    for r in range(world):
-        _, _, n = rows_of(r, world, height)
-        full[r::world] = chunks[r].view(mr, width * 3)[:n]
-    return full.view(height, width, 3)
+    full = stacked.transpose(0, 1).reshape(mr * world, width * 3)[:height]
+    return full.reshape(height, width, 3)

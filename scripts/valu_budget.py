@@ -70,7 +70,7 @@ def short(fn: str) -> str:
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="_ZN12_GLOBAL__N_116pt_render_kernelILi0ELb0ELb0EEEv5PtJob")
+    ap.add_argument("--kernel", default="_ZN12_GLOBAL__N_116pt_render_kernelILi0ELb0ELb0ELb0EEEv5PtJob")
     ap.add_argument("--defines", nargs="*", default=[])
     ap.add_argument("--src", default="pt_kernel.hip")
     ap.add_argument("--csrc", default=None, help="another tree's csrc/ (e.g. a git worktree of an earlier round)")
