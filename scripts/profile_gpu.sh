@@ -18,4 +18,6 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write"
 [ "${TRACE_ONLY:-0}" = 1 ] && exit 0
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$OUT/sq" -o run -- "${CMD[@]}" > "$OUT/sq.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_ANY --output-format csv -d "$OUT/sq2" -o run -- "${CMD[@]}" > "$OUT/sq2.log" 2>&1 || echo "sq2 pass failed (counter names?)"
+# L2 hit / miss of the render kernel's loads (texel gathers vs accumulator, round 4): 2 TCC counters
+[ "${TCC:-0}" = 1 ] && { timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$OUT/tcc" -o run -- "${CMD[@]}" > "$OUT/tcc.log" 2>&1 || echo "tcc pass failed"; }
 find "$OUT" -name '*.csv' | head -50
