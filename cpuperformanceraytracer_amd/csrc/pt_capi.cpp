@@ -76,6 +76,10 @@ struct Dev {
     size_t dbuf_cap = 0;
     unsigned long long* dcounters = nullptr;
     uint32_t* derr = nullptr;           // PT_ERR_WORDS kernel error words (PtJob::err)
+    float* dct = nullptr;               // continuous-tiles pool slots (PtJob::ct_slots), for dct_waves waves
+    uint32_t dct_waves = 0;
+    int ct_slot = -1;                   // tile-queue ring slot of the last launch that used dct (its event
+                                        // orders the next such launch on another stream: one set of slots)
     uint32_t* herr = nullptr;           // their page-locked host copy (read at every synchronisation)
     unsigned int* dqueue = nullptr;     // ring of kQueueRing tile-queue blocks (PT_QUEUE_WORDS each)
     unsigned queue_next = 0;
@@ -138,9 +142,10 @@ struct State {
     PtV4SceneDesc v4desc{};
     PtV4Scene v4scene{};
     uint32_t v4_frame = 0;
-    // test hook: PT_MI355_RING_GUARD_CAP (read by pt_init) caps the ring pool's iteration guard so
+    // test hook: PT_MI355_RING_GUARD_CAP (read by pt_init) caps the pools' iteration guards so
     // that it fires -- the error path's own GPU test (tests/test_gpu_state.py)
     uint32_t ring_guard_cap = ~0u;
+    bool no_ct = false;   // PT_MI355_NO_CT=1 (read by pt_init): one-chunk launches on render_body (A/B)
 };
 
 State g;
@@ -433,6 +438,8 @@ PtJob base_job(float* buf, int32_t w, int32_t h)
     j.cost = nullptr;
     j.err = nullptr;
     j.guard_cap = g.ring_guard_cap;
+    j.ct_slots = nullptr;
+    j.ct_waves = 0;
     j.scene = nullptr;
     return j;
 }
@@ -613,6 +620,20 @@ int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
     j.nunits = ls.nunits;
     j.cost = ls.cost;
     j.err = dv.derr;
+    if (!j.env && !g.no_ct) {   // ambient launches: the continuous-tiles pool
+        if (!dv.dct) {   // its slots, once per device: 12 KiB per wave of the resident grid (~60 MB)
+            const uint32_t waves = pt_ct_resident_waves();
+            if (hipMalloc(&dv.dct, (size_t)waves * pt_ct_wave_floats() * sizeof(float)) == hipSuccess) dv.dct_waves = waves;
+            else dv.dct = nullptr, (void)hipGetLastError();   // (render_body then: correct, slower)
+        }
+        j.ct_slots = dv.dct;
+        j.ct_waves = dv.dct_waves;
+        if (dv.dct) {   // launches on several streams share the slots: one after the other
+            if (dv.ct_slot >= 0 && dv.queue_stream[dv.ct_slot] != st)
+                if (hipEvent_t ev = slot_order(dv, (unsigned)dv.ct_slot)) HIP_TRY(hipStreamWaitEvent(st, ev, 0));
+            dv.ct_slot = (int)ls.slot;
+        }
+    }
     hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
     return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_render's early return)
@@ -1126,6 +1147,7 @@ void free_dev(Dev& dv)
     if (dv.dbuf) (void)hipFree(dv.dbuf);
     if (dv.dcounters) (void)hipFree(dv.dcounters);
     if (dv.derr) (void)hipFree(dv.derr);
+    if (dv.dct) (void)hipFree(dv.dct);
     if (dv.herr) (void)hipHostFree(dv.herr);
     if (dv.dscene) (void)hipFree(dv.dscene);
     if (dv.dqueue) (void)hipFree(dv.dqueue);
@@ -1252,6 +1274,7 @@ int pt_init(const pt_config* cfg)
     HIP_TRY(hipEventCreateWithFlags(&g.ev_q, hipEventDisableTiming));
     g.frame = 0;
     g.ring_guard_cap = ~0u;
+    g.no_ct = getenv("PT_MI355_NO_CT") && !strcmp(getenv("PT_MI355_NO_CT"), "1");
     if (const char* cap = getenv("PT_MI355_RING_GUARD_CAP")) {
         const unsigned long v = strtoul(cap, nullptr, 10);
         if (v > 0 && v < 0xfffffffful) g.ring_guard_cap = (uint32_t)v;

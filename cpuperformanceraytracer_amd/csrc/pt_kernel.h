@@ -48,6 +48,8 @@ struct PtJob {
     uint32_t* err;                 // PT_ERR_WORDS: [0] tiles abandoned by the ring pool's iteration guard,
                                    // [1] the smallest such tile index (~0u: none); nullptr = not recorded
     uint32_t guard_cap;            // upper limit of the ring pool's iteration guard: ~0u (tests lower it)
+    float* ct_slots;               // continuous-tiles pool (pt_kernel.hip render_body_ct): pt_ct_wave_floats()
+    uint32_t ct_waves;             // f32 per wave for ct_waves waves; nullptr: one-chunk launches use render_body
     // mainImage's frame constants (scalar.cpp:338-347), set by pt_launch_render on the host with the
     // same correctly rounded f32 operations: W, H, 1/W, 1/H, W/H, 1/(W/H).  Kernel arguments are
     // scalar registers; computed in the kernel they were VGPRs that the tile loop spilled.
@@ -64,6 +66,11 @@ struct PtJob {
 
 // Enqueue one render launch on `stream`.  Returns hipSuccess or the launch error.
 hipError_t pt_launch_render(const PtJob& job, hipStream_t stream, bool count);
+
+// The continuous-tiles pool's scratch: f32 per wave, and the waves of its resident grid on the
+// current device (the most a launch uses).
+uint32_t pt_ct_wave_floats();
+uint32_t pt_ct_resident_waves();
 
 // Tiles of a job (8x8 pixel tiles over ncols x nrows).
 inline uint32_t pt_job_tiles(const PtJob& j)

@@ -1172,6 +1172,419 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 #endif
 }
 
+// ---- continuous tiles (CT): the ambient kernel's pool without per-tile tails ----------------------
+// render_body's item pool drains at the end of every tile (and, for MULTI launches, of every 8-frame
+// chunk): its last items run while the other lanes idle -- the pool runs at 81 % of its lane slots at
+// 1080p and 4K, 8 spp, 8 bounces.  Here the work of a wave is a stream of CHUNKS -- (tile, kChunk
+// frames), a tile's chunks in frame order -- and the wave keeps TWO chunk contexts: A, whose items
+// are being handed out, and D, whose items are all handed out and still in flight.  When A's last item
+// is handed out and D is folded, A becomes D and the next chunk starts at once, so the lanes that
+// free up take the next chunk's items instead of idling while the slowest paths end.  A new tile's
+// camera rays are traced coherently by all 64 lanes (render_body's phase A) while lanes keep D's
+// items in their registers; the next chunk of a tile needs no camera rays (the bounce-0 records are
+// the same for every frame).  A chunk is folded -- the reference's progressive lerp of its frames, in
+// frame order, :812 -- as soon as its last item ends, and chunks fold in stream order, so every pixel
+// sees its frames in order.  Storage: one set of bounce-0 records per wave (a tile's records are only
+// read when its items are handed out, which ends before the next tile starts), the pixels' running
+// accumulators between a tile's chunks (LDS), and the per-(pixel, frame) radiance of the two
+// contexts in a global slot area (ct_slots: per wave 2 x 64 pixels x kChunk frames x RGB, 12 KiB;
+// an item's write is one 12-B store, a pixel's fold reads its frames with 16-B loads).  A pixel
+// without pool items (camera ray missed, or 0 bounces) folds its constant radiance for all the
+// launch's frames when its tile starts.  Same operations on the same operands, frames in the same
+// order: bit-identical to render_body (every -m gpu parity test).
+constexpr uint32_t kCtWaveFloats = 2u * 64u * (uint32_t)kChunk * 3u;   // per wave: 12 KiB of f32
+
+template <int LAYOUT, bool COUNT>
+__device__ __forceinline__ void render_body_ct(const PtJob& job)
+{
+    const PtScene* __restrict__ sc = job.scene;
+    constexpr int kWavesPerBlock = waves_per_block<false>();
+    constexpr bool QV = true;
+    __shared__ PtLdsPrim s_prim[PT_NPRIMS];
+    __shared__ AxisRow s_axis[PT_NQUADS * kAxisRowsPerQuad<true>];
+    __shared__ float4 s_qv[kQuadVecs];
+    __shared__ float s_w[kMaxWeights];
+    // the current tile's item pixels: bounce-0 records P1.xyz + (id | lane << 8), n1 (planar), as
+    // render_body's; and the item pixels' running accumulators between the tile's chunks
+    __shared__ float4 s_rec[kWavesPerBlock][64];
+    __shared__ float s_nrm[kWavesPerBlock][3][64];
+    __shared__ float s_acc[kWavesPerBlock][3][64];
+    {
+        const int t = threadIdx.x;
+        if (t < PT_NPRIMS) {
+            PtLdsPrim e;
+            if (t < PT_NQUADS) {
+                e.nx = sc->qn[t][0]; e.ny = sc->qn[t][1]; e.nz = sc->qn[t][2];
+            } else {
+                e.nx = sc->sph[t - PT_NQUADS][0]; e.ny = sc->sph[t - PT_NQUADS][1]; e.nz = sc->sph[t - PT_NQUADS][2];
+            }
+            e.ar = sc->albedo[t][0]; e.ag = sc->albedo[t][1]; e.ab = sc->albedo[t][2];
+            e.er = sc->emissive[t][0]; e.eg = sc->emissive[t][1]; e.eb = sc->emissive[t][2];
+            e.pad0 = e.pad1 = e.pad2 = 0.0f;
+            s_prim[t] = e;
+        } else if (t >= 64 && t < 64 + PT_NQUADS * kAxisRowsPerQuad<true>) {
+            constexpr int F = kAxisRowsPerQuad<true> / 3;
+            const int r = (t - 64) / 3, k = (t - 64) % 3, q = r / F, fl = r % F;
+            const auto vk = [&](int v) { return sc->qv[q][fl ? 3 - v : v][k]; };
+            s_axis[t - 64] = AxisRow{vk(0), vk(1), vk(2), vk(3)};
+        } else if (t >= 128 && t < 128 + kQuadVecs) {
+            const int r = (t - 128) / 3, part = (t - 128) % 3, q = r >> 1, fl = r & 1;
+            float e[4];
+            for (int i = 0; i < 4; ++i) {
+                const int f = part * 4 + i, v = f / 3, k = f % 3;
+                e[i] = sc->qv[q][fl ? 3 - v : v][k];
+            }
+            s_qv[t - 128] = make_float4(e[0], e[1], e[2], e[3]);
+        }
+        if (t < kMaxWeights && t < job.nframes)   // :812 1/(iFrame + 1), iFrame exact below 2^24
+            s_w[t] = pt::rcp_rn((float)(job.frame_first + (uint32_t)t) + 1.0f);
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tiles_x = (job.ncols + 7) >> 3;
+    const uint32_t total_tiles = (uint32_t)tiles_x * (uint32_t)((job.nrows + 7) >> 3);
+    const int S = job.nframes, B = job.num_bounces;
+    const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;   // channel stride
+    float* const slots = job.ct_slots + (size_t)(blockIdx.x * kWavesPerBlock + wv) * kCtWaveFloats;
+    // lerp weight of frame f of the launch: the table, or its correctly rounded reciprocal (:812)
+    auto weight = [&](int f) {
+        return f < kMaxWeights ? s_w[f] : pt::rcp_rn((float)(job.frame_first + (uint32_t)f) + 1.0f);
+    };
+
+    Camera cam;
+    cam.W = job.cam_W;
+    cam.H = job.cam_H;
+    cam.yW = job.cam_yW;
+    cam.yH = job.cam_yH;
+    cam.aspect = job.cam_aspect;
+    cam.yAspect = job.cam_yAspect;
+    cam.cam_dist = sc->cam_dist;
+    const V3 amb = v3(sc->ambient[0], sc->ambient[1], sc->ambient[2]);
+    const V3 zero = v3(0.0f, 0.0f, 0.0f), one = v3(1.0f, 1.0f, 1.0f);
+    unsigned long long n_seg = 0, n_iter = 0, n_samp = 0, n_esc = 0, n_prim = 0, n_fb = 0, n_sky = 0;
+
+    if (job.queue_next && blockIdx.x == 0 && threadIdx.x < PT_NQUEUES) job.queue_next[threadIdx.x * 32u] = 0u;
+    constexpr uint32_t kNone = PtTileQueue<kWavesPerBlock>::kNone;
+    PtTileQueue<kWavesPerBlock> tq(job.queue, job.order, job.units, job.nunits, total_tiles, wv);
+
+    // wave-uniform state (scalar registers).  The tile being chunked:
+    bool claimed = false, queue_done = false;
+    uint32_t tcur = kNone;                 // tile whose chunks are still to start (kNone: none)
+    int tcx = 0, tcy = 0, nhcur = 0, f0next = 0;
+    uint64_t hmcur = 0;
+    uint32_t tile_seg = 0;                 // segments of the folded chunks of the tile being folded
+    // The chunk contexts: A hands out items; D has handed out all of its items
+    int cA = 0;                            // A's slot context (D's is 1 - cA)
+    bool hasA = false, hasD = false;
+    uint32_t tA = 0, tD = 0;
+    int txA = 0, tyA = 0, txD = 0, tyD = 0;
+    int f0A = 0, nfA = 0, f0D = 0, nfD = 0;
+    uint64_t hmA = 0, hmD = 0;
+    int issA = 0, nitA = 0, outA = 0, outD = 0;
+    uint32_t divA = 0;                     // k / nfA as (k * divA) >> 16 (exact for k < 64 nfA, nfA < 32)
+    uint32_t segA = 0, segD = 0;           // segments traced for the chunk's items (the schedule's cost)
+    // per lane: the item (bounce 0: none) and the float index of its radiance slot in `slots`
+    V3 P = zero, D = zero, T = zero, ret = zero, n = zero;
+    uint32_t rng = 0;
+    int bounce = 0;
+    int it_addr = 0;
+    uint64_t ctx1 = 0;   // lanes whose item belongs to slot context 1 (SALU bookkeeping)
+
+    // Start chunks until A is set or the queue is empty: the current tile's next chunk, or a new tile
+    // (render_body's phase A, run by the whole wave while lanes may hold D's items -- item registers
+    // untouched).  A new tile starts only when the previous tile's last chunk has handed out every
+    // item, so its records are free.
+    auto start_chunk = [&]() {
+        while (!hasA) {
+            if (tcur != kNone && f0next < S) {   // the current tile's next chunk
+                hasA = true;
+                tA = tcur;
+                txA = tcx;
+                tyA = tcy;
+                hmA = hmcur;
+                f0A = f0next;
+                nfA = S - f0next < kChunk ? S - f0next : kChunk;
+                f0next += nfA;
+                divA = (65536u + (uint32_t)nfA - 1u) / (uint32_t)nfA;
+                issA = 0;
+                nitA = nhcur * nfA;
+                outA = nitA;
+                segA = 0;
+                break;
+            }
+            tcur = kNone;
+            if (queue_done) break;
+            uint32_t tile = claimed ? tq.next() : tq.first();
+            claimed = true;
+            tile = __builtin_amdgcn_readfirstlane(tile);
+            if (tile == kNone) {
+                queue_done = true;
+                break;
+            }
+            const int tyi = (int)(tile / (uint32_t)tiles_x), txi = (int)(tile % (uint32_t)tiles_x);
+            const int lc = txi * 8 + (lane & 7), lr = tyi * 8 + (lane >> 3);
+            const bool valid = lc < job.ncols && lr < job.nrows;
+            const float fx = (float)(job.col0 + lc);                                            // :806
+            const float fy = (float)(job.height - 1 - (job.row_start + lr * job.row_stride));   // :803
+            const V3 D0 = camera_dir(cam, fx, fy);
+            const bool all_sky = pt_ballot(valid && !sky_ray(D0)) == 0;   // (render_body's sky tiles)
+            bool items = false;
+            V3 P1 = zero, N1 = zero;
+            int id1 = 0;
+            if (valid) {
+                const Hit h = all_sky ? Hit{PT_SUPER_FAR, -1, 0, 0}
+                                      : trace<DemofoxScene, true, QV, true>(s_axis, s_qv, zero, D0);   // :335
+                if (COUNT) ++n_seg, ++n_prim, n_fb += (unsigned long long)h.fb, n_sky += all_sky ? 1ull : 0ull;
+                if (COUNT) n_samp += (unsigned long long)S;
+                V3 c_keep;
+                if (h.best == PT_SUPER_FAR) {                                 // :305-310
+                    c_keep = add(zero, amb);
+                    if (COUNT) n_esc += (unsigned long long)S;
+                } else {
+                    const PtLdsPrim pr = prim_at(s_prim, h.id);
+                    const V3 n1 = hit_normal(pr, h, zero, D0);
+                    P1 = add(add(zero, mul(D0, h.best)), mul(n1, PT_NUDGE));    // :313
+                    N1 = n1;
+                    id1 = h.id;
+                    items = B != 0;
+                    c_keep = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one));    // :319 (ret after bounce 0)
+                }
+                if (!items) {   // the same radiance in every frame: fold all of the launch's frames now
+                    float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
+                    V3 acc = v3(px[0], px[cs], px[2 * cs]);
+                    for (int f = 0; f < S; ++f) acc = add(acc, mul(sub(c_keep, acc), weight(f)));
+                    px[0] = acc.x;
+                    px[cs] = acc.y;
+                    px[2 * cs] = acc.z;
+                }
+            }
+            const uint64_t hm = pt_ballot(items);
+            const int nh = __popcll(hm);
+            if (nh == 0) {
+                if (job.cost && lane == 0) job.cost[tile] = 1u;
+                continue;
+            }
+            if (items) {   // compacted record slot: the pixel's rank among the tile's item pixels
+                const int slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+                s_rec[wv][slot] = make_float4(P1.x, P1.y, P1.z, __builtin_bit_cast(float, id1 | (lane << 8)));
+                s_nrm[wv][0][slot] = N1.x;
+                s_nrm[wv][1][slot] = N1.y;
+                s_nrm[wv][2][slot] = N1.z;
+            }
+            tcur = tile;
+            tcx = txi;
+            tcy = tyi;
+            hmcur = hm;
+            nhcur = nh;
+            f0next = 0;
+        }
+    };
+    // Fold D: every item of it has ended, its radiance is in the slots of context 1 - cA
+    auto fold_D = [&]() {
+        const int c = cA ^ 1;
+        // the slots were written by this wave's lanes (global stores): complete them before reading
+        // (workgroup scope: the same CU's L1 -- LLVM AMDGPU memory model)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const bool first = f0D == 0, last = f0D + nfD == S;
+        if ((hmD >> lane) & 1u) {   // (an item pixel is a valid pixel)
+            const float4* sp = (const float4*)(slots + (c * 64 + lane) * (kChunk * 3));   // 96 B, 16-B aligned
+            float4 v[kChunk * 3 / 4];
+#pragma unroll
+            for (int i = 0; i < kChunk * 3 / 4; ++i)
+                if (i * 4 < nfD * 3) v[i] = sp[i];
+            const float* fr = (const float*)v;
+            const int lc = txD * 8 + (lane & 7), lr = tyD * 8 + (lane >> 3);
+            float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
+            V3 acc = first ? v3(px[0], px[cs], px[2 * cs]) : v3(s_acc[wv][0][lane], s_acc[wv][1][lane], s_acc[wv][2][lane]);
+#pragma unroll
+            for (int f = 0; f < kChunk; ++f) {
+                if (f < nfD) {
+                    // color = the sample's radiance (0 + c * 1 == c, render_body's phase C)
+                    const V3 colr = v3(fr[3 * f], fr[3 * f + 1], fr[3 * f + 2]);
+                    acc = add(acc, mul(sub(colr, acc), weight(f0D + f)));        // :812
+                }
+            }
+            if (last) {
+                px[0] = acc.x;
+                px[cs] = acc.y;
+                px[2 * cs] = acc.z;
+            } else {
+                s_acc[wv][0][lane] = acc.x;
+                s_acc[wv][1][lane] = acc.y;
+                s_acc[wv][2][lane] = acc.z;
+            }
+        }
+        tile_seg += segD;
+        if (last) {
+            if (job.cost && lane == 0) job.cost[tD] = 1u + (tile_seg + 63u) / 64u;   // ~ the tile's pool iterations
+            tile_seg = 0;
+        }
+        hasD = false;
+    };
+
+    start_chunk();
+    const uint64_t live = pt_ballot(true);
+    const uint32_t stall_limit = (uint32_t)B + 8u;   // an item ends within B + 1 iterations
+    uint32_t stall = 0;                               // pool iterations in a row without progress
+    uint32_t idle_events = 0;                         // outer iterations in a row without progress
+    uint32_t wave_it = 0;                             // pool iterations of this wave (test hook below)
+    bool fault = false;
+    // outer loop: the events (D is folded; A becomes D and the next chunk starts); inner loop: pool
+    // iterations until an event is due -- the hot loop holds no start / fold code
+    while (!fault) {
+        bool event = false;
+        if (hasD && outD == 0) {   // D's last item ended: fold it
+            fold_D();
+            event = true;
+        }
+        if (hasA && issA >= nitA && !hasD) {   // A has handed out every item and D is folded
+            hasD = true;
+            tD = tA;
+            txD = txA;
+            tyD = tyA;
+            hmD = hmA;
+            f0D = f0A;
+            nfD = nfA;
+            outD = outA;
+            segD = segA;
+            hasA = false;
+            cA ^= 1;
+            start_chunk();
+            event = true;
+            if (outD == 0) continue;   // (D's items had all ended: fold it first)
+        }
+        if (!hasA && !hasD) break;   // every chunk of every tile of the queue is folded
+        // (guard, never reached: with a chunk left, an outer iteration folds, retires or runs the pool)
+        idle_events = event ? 0u : idle_events + 1u;
+        if (__builtin_expect(idle_events > 2u, 0)) {
+            fault = true;
+            break;
+        }
+        while (true) {
+            const bool had = bounce != 0;
+            const uint64_t idle = pt_ballot(!had);
+            bool took = false;
+            int ntaken = 0;
+            uint64_t tm = 0;   // the lanes that take an item now
+            if (idle != 0 && hasA && issA < nitA) {
+                const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                const int k = issA + rank;
+                const bool take = !had && k < nitA;
+                took = take;
+                // pixel-major: consecutive items are the frames of one pixel (render_body's order)
+                const int slot_pm = take ? (int)(__umul24((uint32_t)k, divA) >> 16) : 0;
+                const int fi = take ? k - (int)__umul24((uint32_t)slot_pm, (uint32_t)nfA) : 0;
+                if (take) {
+                    const float4 a0 = s_rec[wv][slot_pm];
+                    const int packed = __builtin_bit_cast(int, a0.w);
+                    const int sId = packed & 0xff;
+                    const int src = packed >> 8;                  // lane owning the pixel
+                    const int slc = txA * 8 + (src & 7), slr = tyA * 8 + (src >> 3);
+                    const PtLdsPrim pr = prim_at(s_prim, sId);
+                    rng = seed_int((uint32_t)(job.col0 + slc),
+                                   (uint32_t)(job.height - 1 - (job.row_start + (int)__umul24((uint32_t)slr, (uint32_t)job.row_stride))),
+                                   job.frame_first + (uint32_t)(f0A + fi));                          // :332
+                    P = v3(a0.x, a0.y, a0.z);                                            // :313 (bounce 0)
+                    n = v3(s_nrm[wv][0][slot_pm], s_nrm[wv][1][slot_pm], s_nrm[wv][2][slot_pm]);
+                    ret = emissive0(pr);                                                 // :319
+                    T = mulv(one, v3(pr.ar, pr.ag, pr.ab));                              // :322
+                    bounce = 1;
+                    it_addr = (int)__umul24((uint32_t)(cA * 64 + src), (uint32_t)(kChunk * 3)) + fi * 3;
+                }
+                const int npop = __popcll(idle);
+                ntaken = npop < nitA - issA ? npop : nitA - issA;
+                issA += ntaken;
+                // the takers are the first ntaken idle lanes (SALU: drop the highest idle lanes when A
+                // runs out of items)
+                tm = idle;
+                for (int d = npop - ntaken; d > 0; --d) tm &= ~(1ull << (63 - __builtin_clzll(tm)));
+                ctx1 = (ctx1 & ~tm) | (cA ? tm : 0ull);
+            }
+            // no lane holds an item: an event is due (or the wave is done)
+            if ((live & ~idle) == 0 && ntaken == 0) break;
+            idle_events = 0;
+            if (COUNT) ++n_iter;
+            bool done = false;
+            if (had || took) {
+                D = normalize(add(n, random_unit_vector(rng)));                          // :316
+                const Hit h = trace<DemofoxScene, false, QV, true>(s_axis, s_qv, P, D);
+                if (COUNT) ++n_seg, n_fb += (unsigned long long)h.fb;
+                if (h.best == PT_SUPER_FAR) {                                     // :305-310
+                    ret = add(ret, amb);
+                    done = true;
+                    if (COUNT) ++n_esc;
+                } else {
+                    const PtLdsPrim pr = prim_at(s_prim, h.id);
+                    n = hit_normal(pr, h, P, D);
+                    P = add(add(P, mul(D, h.best)), mul(n, PT_NUDGE));            // :313
+                    ret = add(ret, mulv(v3(pr.er, pr.eg, pr.eb), T));             // :319
+                    T = mulv(T, v3(pr.ar, pr.ag, pr.ab));                         // :322
+                    bounce += 1;
+                    done = bounce > B;
+                }
+                if (done) {
+                    float* c = slots + it_addr;
+                    c[0] = ret.x;
+                    c[1] = ret.y;
+                    c[2] = ret.z;
+                    bounce = 0;
+                }
+            }
+            // items that ended, per context (SALU)
+            const uint64_t ended = pt_ballot(done);
+            const uint64_t active = (live & ~idle) | tm;
+            const int endA = __popcll(ended & (cA ? ctx1 : ~ctx1));
+            outA -= endA;
+            outD -= __popcll(ended) - endA;
+            if (job.cost) {   // (only launches whose tile costs feed the next schedule): segments traced
+                const int inA = __popcll(active & (cA ? ctx1 : ~ctx1));
+                segA += (uint32_t)inA;
+                segD += (uint32_t)(__popcll(active) - inA);
+            }
+            // guard (never reached): an item in flight ends within B + 1 iterations, so B + 8
+            // iterations in a row without a hand-out or an ended item are a scheduling fault
+            // (job.guard_cap: ~0u, or a low test value -- PT_MI355_RING_GUARD_CAP -- that ends the
+            // wave after that many iterations, so that the fault path runs on a correct launch)
+            stall = (ntaken != 0 || ended != 0) ? 0u : stall + 1u;
+            ++wave_it;
+            if (__builtin_expect(stall > stall_limit || wave_it > job.guard_cap, 0)) {
+                fault = true;
+                break;
+            }
+            if (hasD && outD == 0) break;                        // fold due
+            if (hasA && issA >= nitA && !hasD) break;            // retire due
+        }
+    }
+    // a fault ends the wave with its chunks unfinished: recorded in the job's error words (the host
+    // returns PT_EKERNEL), instead of a hung GPU
+    if (__builtin_expect(fault, 0) && lane == 0 && job.err) {
+        atomicAdd(&job.err[0], 1u);
+        atomicMin(&job.err[1], hasA ? tA : (hasD ? tD : 0u));
+    }
+    if (COUNT) {
+        for (int off = 32; off > 0; off >>= 1) {
+            n_seg += __shfl_xor(n_seg, off, 64);
+            n_samp += __shfl_xor(n_samp, off, 64);
+            n_esc += __shfl_xor(n_esc, off, 64);
+            n_prim += __shfl_xor(n_prim, off, 64);
+            n_fb += __shfl_xor(n_fb, off, 64);
+            n_sky += __shfl_xor(n_sky, off, 64);
+        }
+        if (lane == 0) {
+            atomicAdd(&job.counters[PT_CNT_SEGMENTS], n_seg);
+            atomicAdd(&job.counters[PT_CNT_LANE_SLOTS], 64ull * n_iter);
+            atomicAdd(&job.counters[PT_CNT_SAMPLES], n_samp);
+            atomicAdd(&job.counters[PT_CNT_ESCAPED], n_esc);
+            atomicAdd(&job.counters[PT_CNT_PRIMARY], n_prim);
+            atomicAdd(&job.counters[PT_CNT_FALLBACK], n_fb);
+            atomicAdd(&job.counters[PT_CNT_SKY], n_sky);
+        }
+    }
+}
+
 // Kernel entry points.  The ambient kernel is held to 96 VGPRs (the 5-waves-per-SIMD budget; 10
 // spilled); the env-map kernel needs ~117 and runs at 4.
 #ifndef PT_AMBIENT_WAVES
@@ -1189,6 +1602,13 @@ template <int LAYOUT, bool COUNT, bool MULTI>
 __global__ __launch_bounds__(64 * waves_per_block<true>()) void pt_render_env_kernel(PtJob job)
 {
     render_body<LAYOUT, true, COUNT, MULTI, false>(job);
+}
+
+template <int LAYOUT, bool COUNT>
+__global__ __launch_bounds__(64 * waves_per_block<false>()) __attribute__((amdgpu_waves_per_eu(PT_AMBIENT_WAVES, PT_AMBIENT_WAVES))) void
+pt_render_ct_kernel(PtJob job)
+{
+    render_body_ct<LAYOUT, COUNT>(job);
 }
 
 template <int LAYOUT, bool ENV, bool COUNT, bool MULTI, bool RING>
@@ -1217,11 +1637,32 @@ void launch_k(const PtJob& job, hipStream_t st, unsigned tiles)
 #endif
 constexpr int kRingMinFrames = PT_RING_MIN;
 
+// One-chunk ambient launches on the continuous-tiles pool (render_body_ct) when the caller provides
+// its slots for the whole grid; false: not launched (render_body then).
+template <int LAYOUT, bool COUNT>
+bool launch_ct(const PtJob& job, hipStream_t st, unsigned tiles)
+{
+#if PT_DIAG
+    return false;   // (the diagnostic timelines are render_body's)
+#else
+    constexpr int wpb = waves_per_block<false>();
+    auto k = pt_render_ct_kernel<LAYOUT, COUNT>;
+    const unsigned blocks = (unsigned)std::min<long>(pt_resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
+    if (!job.ct_slots || (uint64_t)blocks * wpb > job.ct_waves) return false;
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
+    return true;
+#endif
+}
+
 template <int LAYOUT, bool ENV>
 hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 {
     const unsigned tiles = (unsigned)((job.ncols + 7) / 8) * (unsigned)((job.nrows + 7) / 8);
     const bool multi = job.nframes > kChunk;
+    if constexpr (!ENV) {   // the ambient kernel: the continuous-tiles pool when its slots are provided
+        if (count ? launch_ct<LAYOUT, true>(job, st, tiles) : launch_ct<LAYOUT, false>(job, st, tiles))
+            return hipGetLastError();
+    }
     const bool ring = !ENV && job.nframes >= kRingMinFrames && job.nframes > kChunk;
     if (count) {
         if (ring) launch_k<LAYOUT, ENV, true, true, !ENV>(job, st, tiles);
@@ -1363,6 +1804,20 @@ hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* u
     }
     hipLaunchKernelGGL(pt_schedule_kernel, dim3(1), dim3(1024), 0, st, cost, order, units, nunits, ntiles, unit_cost);
     return hipGetLastError();
+}
+
+uint32_t pt_ct_wave_floats() { return kCtWaveFloats; }
+
+uint32_t pt_ct_resident_waves()
+{
+    constexpr int wpb = waves_per_block<false>();
+    const int r[6] = {pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, false>, 64 * wpb),
+                      pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, true>, 64 * wpb),
+                      pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, false>, 64 * wpb),
+                      pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, true>, 64 * wpb),
+                      pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, false>, 64 * wpb),
+                      pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, true>, 64 * wpb)};
+    return (uint32_t)*std::max_element(r, r + 6) * (uint32_t)wpb;
 }
 
 hipError_t pt_launch_render(const PtJob& job_in, hipStream_t st, bool count)

@@ -35,7 +35,8 @@ for i in range(K):
     render_device(buf, W, H, frame_first=1 + S * (i + 4), nframes=S, num_bounces=B, use_env=ENV)
 e1.record(); torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / K
-print(json.dumps({"lib": __import__("os").environ.get("PT_MI355_LIB", "default"), "env": ENV, "W": W, "H": H, "spp": S, "B": B, "ms_per_launch": ms,
+print(json.dumps({"lib": __import__("os").environ.get("PT_MI355_LIB", "default"),
+                  "ct": __import__("os").environ.get("PT_MI355_NO_CT") != "1", "env": ENV, "W": W, "H": H, "spp": S, "B": B, "ms_per_launch": ms,
                   "primary_samples_per_s": W * H * S / ms * 1e3, "ray_samples_per_s": W * H * S * B / ms * 1e3,
                   "segments_per_sample": cnt["segments"] / cnt["samples"],
                   "ref_segments_per_sample": (cnt["segments"] - cnt["primary"]) / cnt["samples"] + 1,

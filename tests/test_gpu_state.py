@@ -213,14 +213,18 @@ def test_destroyed_stream_between_launches():
     pt.shutdown()
 
 
-def test_ring_guard_fires_loudly(monkeypatch):
-    """The ring pool's iteration guard (pt_kernel.hip RING) abandons a tile only on a scheduling
-    fault; when it fires, no call returns success: the host-buffer call that waited for the launch
-    raises PtError(PT_EKERNEL) naming the tile, and device jobs report it through
-    pt_check_device_errors.  PT_MI355_RING_GUARD_CAP (read by pt_init) lowers the guard so that it
-    fires on a correct launch; errors are reported once, then the library works normally."""
+@pytest.mark.parametrize("pool", ["ct", "ring"])
+def test_pool_guard_fires_loudly(monkeypatch, pool):
+    """The pools' iteration guards (pt_kernel.hip: the ring pool's per-tile bound, the continuous-
+    tiles pool's stall bound) end a wave only on a scheduling fault; when one fires, no call returns
+    success: the host-buffer call that waited for the launch raises PtError(PT_EKERNEL) naming the
+    tile, and device jobs report it through pt_check_device_errors.  PT_MI355_RING_GUARD_CAP (read
+    by pt_init) lowers the guards so that they fire on a correct launch; errors are reported once,
+    then the library works normally.  ring: PT_MI355_NO_CT=1 selects the ring pool (>= 48 frames)."""
     from cpuperformanceraytracer_amd.device import check_device_errors, render_device
-    w, h, f = 64, 64, 49                      # >= 48 frames: one ring-pool launch
+    w, h, f = 64, 64, 49                      # >= 48 frames: one launch
+    if pool == "ring":
+        monkeypatch.setenv("PT_MI355_NO_CT", "1")
     monkeypatch.setenv("PT_MI355_RING_GUARD_CAP", "8")
     pt.init(num_bounces=8, samples_per_frame=f)
     buf = np.zeros((h, w, 3), np.float32)
