@@ -53,7 +53,8 @@ struct Sched {
     SchedKey key;
     uint32_t* cost = nullptr;
     uint32_t* order = nullptr;
-    uint32_t* units = nullptr;    // ntiles + 2 words: run starts, then the run count
+    uint32_t* units = nullptr;    // 2 ntiles + 2 words: run starts, then the run count (cost: 2 ntiles words,
+                                  // order: up to 2 ntiles entries -- split tiles, pt_tile_queue.h)
     bool have_cost = false;
     bool built = false;           // order/units hold a schedule
     unsigned long long launches = 0;
@@ -145,6 +146,7 @@ struct State {
     // test hook: PT_MI355_RING_GUARD_CAP (read by pt_init) caps the pools' iteration guards so
     // that it fires -- the error path's own GPU test (tests/test_gpu_state.py)
     uint32_t ring_guard_cap = ~0u;
+    uint32_t split = 2;   // PT_MI355_SPLIT (read by pt_init): tile split factor of the schedule (0: none)
     bool no_ct = false;   // PT_MI355_NO_CT=1 (read by pt_init): one-chunk launches on render_body (A/B)
 };
 
@@ -503,8 +505,9 @@ Sched* find_sched(Dev& dv, const SchedKey& key, hipStream_t st)
         free_sched(*lru);
     }
     Sched s;
-    if (hipMalloc(&s.cost, n * sizeof(uint32_t)) != hipSuccess || hipMalloc(&s.order, n * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&s.units, (n + 2) * sizeof(uint32_t)) != hipSuccess) {
+    if (hipMalloc(&s.cost, 2 * (size_t)n * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&s.order, 2 * (size_t)n * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&s.units, (2 * (size_t)n + 2) * sizeof(uint32_t)) != hipSuccess) {
         free_sched(s);
         return nullptr;   // unscheduled launch (raster order): correct, only slower
     }
@@ -547,14 +550,17 @@ int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls)
         // then every kSchedRebuild launches (the costs of a fixed view barely change; the builder
         // is a one-workgroup kernel of ~57 us at 1080p)
         if (s->have_cost && (!s->built || s->launches % kSchedRebuild == 0)) {
-            hipError_t e = pt_launch_schedule(s->cost, s->order, s->units, s->units + s->key.ntiles + 1, s->key.ntiles, st);
+            // (split tiles: the diffuse kernels; v4 takes whole tiles)
+            const uint32_t split = key.kind == 0 ? g.split : 0u;
+            hipError_t e = pt_launch_schedule(s->cost, s->order, s->units, s->units + 2 * s->key.ntiles + 1, s->key.ntiles,
+                                              split, st);
             if (e != hipSuccess) return fail(PT_EHIP, "schedule launch failed: %s", hipGetErrorString(e));
             s->built = true;
         }
         if (s->built) {
             ls->order = s->order;
             ls->units = s->units;
-            ls->nunits = s->units + s->key.ntiles + 1;
+            ls->nunits = s->units + 2 * s->key.ntiles + 1;
         }
         // the kernel records the tiles' costs only when the next launch builds from them (one 4-B
         // store per tile is a 32-B HBM write: ~1 MB per 1080p launch otherwise)
@@ -1275,6 +1281,8 @@ int pt_init(const pt_config* cfg)
     g.frame = 0;
     g.ring_guard_cap = ~0u;
     g.no_ct = getenv("PT_MI355_NO_CT") && !strcmp(getenv("PT_MI355_NO_CT"), "1");
+    g.split = 2;
+    if (const char* sp = getenv("PT_MI355_SPLIT")) g.split = (uint32_t)strtoul(sp, nullptr, 10);
     if (const char* cap = getenv("PT_MI355_RING_GUARD_CAP")) {
         const unsigned long v = strtoul(cap, nullptr, 10);
         if (v > 0 && v < 0xfffffffful) g.ring_guard_cap = (uint32_t)v;

@@ -63,6 +63,10 @@ struct PtJob {
 #define PT_NQUEUES 8
 #endif
 #define PT_QUEUE_WORDS (PT_NQUEUES * 32)
+// Tile queue entries (pt_tile_queue.h): the tile index in the low 30 bits, its part in the top 2 (0 the
+// whole 8x8 tile, 1 rows 0-3, 2 rows 4-7)
+#define PT_TILE_MASK 0x3fffffffu
+#define PT_TILE_PART_SHIFT 30
 
 // Enqueue one render launch on `stream`.  Returns hipSuccess or the launch error.
 hipError_t pt_launch_render(const PtJob& job, hipStream_t stream, bool count);
@@ -78,7 +82,9 @@ inline uint32_t pt_job_tiles(const PtJob& j)
     return (uint32_t)((j.ncols + 7) / 8) * (uint32_t)((j.nrows + 7) / 8);
 }
 
-// Enqueue the schedule builder: order = the tiles sorted by descending cost (a permutation),
-// units = runs of about equal cost over it (ntiles + 1 words), *nunits = their number.
+// Enqueue the schedule builder: order = the queue entries sorted by descending cost (every tile
+// once, or as its two halves when it costs more than 1/split of a resident wave's share of the
+// launch; split 0: never), units = runs of about equal cost over it, *nunits = their number.
+// cost: 2 x ntiles words (pt_record_cost), order: up to 2 x ntiles entries, units: 2 x ntiles + 1.
 hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* units, uint32_t* nunits,
-                              uint32_t ntiles, hipStream_t stream);
+                              uint32_t ntiles, uint32_t split, hipStream_t stream);

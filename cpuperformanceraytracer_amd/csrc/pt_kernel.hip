@@ -709,7 +709,10 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     tile = tq.first();   // (the whole wave: uniform, scalar registers)
     tile = __builtin_amdgcn_readfirstlane(tile);
     while (tile != kNone) {
-        const int tyi = (int)(tile / (uint32_t)tiles_x), txi = (int)(tile % (uint32_t)tiles_x);
+        // a queue entry is a tile or one half of it (pt_tile_queue.h): the pixels of the other half
+        // are treated as outside the image
+        const uint32_t part = pt_entry_part(tile);
+        const int tyi = (int)(pt_entry_tile(tile) / (uint32_t)tiles_x), txi = (int)(pt_entry_tile(tile) % (uint32_t)tiles_x);
         DIAG_MARK(t_tile);
 #if PT_DIAG && !PT_DIAG_WAVES_ONLY
         const unsigned long long r_tile0 = __builtin_amdgcn_s_memrealtime();
@@ -720,7 +723,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 #endif
         // ---------------- phase A: camera ray, once per pixel ----------------
         const int lc = txi * 8 + (lane & 7), lr = tyi * 8 + (lane >> 3);
-        const bool valid = lc < job.ncols && lr < job.nrows;
+        const bool valid = lc < job.ncols && lr < job.nrows && pt_part_has_lane(part, lane);
         const float fx = (float)(job.col0 + lc);                                            // :806
         const float fy = (float)(job.height - 1 - (job.row_start + lr * job.row_stride));   // :803
         // Registers live across the pool loop are kept to a minimum (the 96-VGPR budget of 5 waves per
@@ -876,7 +879,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 if (__builtin_expect(tile_work > guard_lim, 0)) {   // (never reached, see guard_lim)
                     if (lane == 0 && job.err) {
                         atomicAdd(&job.err[0], 1u);           // abandoned tiles
-                        atomicMin(&job.err[1], this_tile);     // the first of them
+                        atomicMin(&job.err[1], pt_entry_tile(this_tile));   // the first of them
                     }
                     break;
                 }
@@ -1080,7 +1083,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             // ---------------- phase C: progressive lerp in frame order ----------------
             DIAG_MARK(t_c);
             const int clc = txi * 8 + (lane & 7), clr = tyi * 8 + (lane >> 3);
-            const bool cvalid = clc < job.ncols && clr < job.nrows;
+            const bool cvalid = clc < job.ncols && clr < job.nrows && pt_part_has_lane(part, lane);
             if (cvalid) {
                 if (!MULTI) {   // the accumulator, read once (24 B per pixel per launch with the store)
                     const float* px = job.buf + out_index<LAYOUT>(job, clc, clr);
@@ -1110,13 +1113,13 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             DIAG_ADD(5, t_c);
         }
         }
-        if (txi * 8 + (lane & 7) < job.ncols && tyi * 8 + (lane >> 3) < job.nrows) {
+        if (txi * 8 + (lane & 7) < job.ncols && tyi * 8 + (lane >> 3) < job.nrows && pt_part_has_lane(part, lane)) {
             float* px = job.buf + out_index<LAYOUT>(job, txi * 8 + (lane & 7), tyi * 8 + (lane >> 3));
             px[0] = acc.x;
             px[cs] = acc.y;
             px[2 * cs] = acc.z;
         }
-        if (job.cost && lane == 0) job.cost[this_tile] = tile_work;
+        if (job.cost && lane == 0) pt_record_cost(job.cost, this_tile, total_tiles, tile_work);
         if (S <= 0) next_tile = tq.next();   // no chunk ran (nframes 0)
         tile = __builtin_amdgcn_readfirstlane(next_tile);
 #if PT_DIAG && !PT_DIAG_WAVES_ONLY
@@ -1193,6 +1196,13 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 // launch's frames when its tile starts.  Same operations on the same operands, frames in the same
 // order: bit-identical to render_body (every -m gpu parity test).
 constexpr uint32_t kCtWaveFloats = 2u * 64u * (uint32_t)kChunk * 3u;   // per wave: 12 KiB of f32
+// render_body_ct's per-wave LDS words: the tile being chunked (queue entry, pixel terms of the seed,
+// item-pixel mask, item pixels, next chunk's first frame), A's first frame, D (entry, first frame,
+// frames, item-pixel mask), the tile's folded segments, flags (1 claimed, 2 queue done), chunks
+enum : int {
+    kWsTcur, kWsX, kWsY, kWsHm, kWsHm1, kWsNh, kWsF0next, kWsF0A, kWsTD, kWsF0D, kWsNfD, kWsHmD, kWsHmD1,
+    kWsTileSeg, kWsFlags, kWsChunks, kWsWords
+};
 
 template <int LAYOUT, bool COUNT>
 __device__ __forceinline__ void render_body_ct(const PtJob& job)
@@ -1209,6 +1219,8 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     __shared__ float4 s_rec[kWavesPerBlock][64];
     __shared__ float s_nrm[kWavesPerBlock][3][64];
     __shared__ float s_acc[kWavesPerBlock][3][64];
+    __shared__ uint32_t s_ws[kWavesPerBlock][kWsWords];   // the events' wave-uniform state (below)
+    __shared__ uint32_t s_tq[kWavesPerBlock][PtTileQueue<kWavesPerBlock>::kWords];   // the wave's tile queue
     {
         const int t = threadIdx.x;
         if (t < PT_NPRIMS) {
@@ -1264,24 +1276,40 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     const V3 amb = v3(sc->ambient[0], sc->ambient[1], sc->ambient[2]);
     const V3 zero = v3(0.0f, 0.0f, 0.0f), one = v3(1.0f, 1.0f, 1.0f);
     unsigned long long n_seg = 0, n_iter = 0, n_samp = 0, n_esc = 0, n_prim = 0, n_fb = 0, n_sky = 0;
+#if PT_DIAG   // diagnostic build: render_body's per-wave records; tile records from claim to last fold
+    const unsigned long long r_birth = __builtin_amdgcn_s_memrealtime();
+    unsigned long long n_tiles_diag = 0;
+    uint32_t didx_cur = 0, didxA = 0, didxD = 0;   // tile record index of tcur / A / D
+    unsigned long long* const dtl =
+        job.counters ? job.counters + 32 + 4 * 65536 + 96 * (size_t)(blockIdx.x * kWavesPerBlock + wv) : nullptr;
+#endif
 
     if (job.queue_next && blockIdx.x == 0 && threadIdx.x < PT_NQUEUES) job.queue_next[threadIdx.x * 32u] = 0u;
     constexpr uint32_t kNone = PtTileQueue<kWavesPerBlock>::kNone;
-    PtTileQueue<kWavesPerBlock> tq(job.queue, job.order, job.units, job.nunits, total_tiles, wv);
+    PtTileQueue<kWavesPerBlock>(job.queue, job.order, job.units, job.nunits, total_tiles, wv).save(s_tq[wv], lane);
 
-    // wave-uniform state (scalar registers).  The tile being chunked:
-    bool claimed = false, queue_done = false;
-    uint32_t tcur = kNone;                 // tile whose chunks are still to start (kNone: none)
-    int tcx = 0, tcy = 0, nhcur = 0, f0next = 0;
-    uint64_t hmcur = 0;
-    uint32_t tile_seg = 0;                 // segments of the folded chunks of the tile being folded
-    // The chunk contexts: A hands out items; D has handed out all of its items
+    // Wave-uniform state.  What only the events (chunk start, retire, fold) use lives in LDS (s_ws),
+    // not in scalar registers: the pool loop then keeps its constants in SGPRs instead of
+    // rematerialising them every iteration (the scalar register file is the pool's tight budget:
+    // 102 per wave).  ws_ld / ws_st: a uniform load (readfirstlane) / lane 0's store.
+    uint32_t* const ws = s_ws[wv];
+    auto ws_ld = [&](int k) -> uint32_t { return __builtin_amdgcn_readfirstlane(ws[k]); };
+    auto ws_st = [&](int k, uint32_t v) {
+        if (lane == 0) ws[k] = v;
+    };
+    if (lane == 0) {
+        ws[kWsTcur] = kNone;   // the tile being chunked (A's tile whenever A is set)
+        ws[kWsFlags] = 0u;
+        ws[kWsChunks] = 0u;
+        ws[kWsTileSeg] = 0u;
+    }
+    // In the pool loop (scalar registers): the chunk contexts -- A hands out items; D has handed out
+    // all of its items
     int cA = 0;                            // A's slot context (D's is 1 - cA)
     bool hasA = false, hasD = false;
-    uint32_t tA = 0, tD = 0;
-    int txA = 0, tyA = 0, txD = 0, tyD = 0;
-    int f0A = 0, nfA = 0, f0D = 0, nfD = 0;
-    uint64_t hmA = 0, hmD = 0;
+    int nfA = 0;
+    uint32_t fA = 0;                       // frame_first + A's first frame
+    uint32_t xcur = 0, ycur = 0;           // the seed's pixel terms of A's tile's (0, 0) pixel (:332)
     int issA = 0, nitA = 0, outA = 0, outD = 0;
     uint32_t divA = 0;                     // k / nfA as (k * divA) >> 16 (exact for k < 64 nfA, nfA < 32)
     uint32_t segA = 0, segD = 0;           // segments traced for the chunk's items (the schedule's cost)
@@ -1298,34 +1326,49 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     // item, so its records are free.
     auto start_chunk = [&]() {
         while (!hasA) {
-            if (tcur != kNone && f0next < S) {   // the current tile's next chunk
+            const int f0next = (int)ws_ld(kWsF0next);
+            if (ws_ld(kWsTcur) != kNone && f0next < S) {   // the current tile's next chunk
                 hasA = true;
-                tA = tcur;
-                txA = tcx;
-                tyA = tcy;
-                hmA = hmcur;
-                f0A = f0next;
+                fA = job.frame_first + (uint32_t)f0next;
                 nfA = S - f0next < kChunk ? S - f0next : kChunk;
-                f0next += nfA;
+                ws_st(kWsF0A, (uint32_t)f0next);
+                ws_st(kWsF0next, (uint32_t)(f0next + nfA));
+                xcur = ws_ld(kWsX);
+                ycur = ws_ld(kWsY);
                 divA = (65536u + (uint32_t)nfA - 1u) / (uint32_t)nfA;
                 issA = 0;
-                nitA = nhcur * nfA;
+                nitA = (int)ws_ld(kWsNh) * nfA;
                 outA = nitA;
                 segA = 0;
+#if PT_DIAG
+                didxA = didx_cur;
+#endif
                 break;
             }
-            tcur = kNone;
-            if (queue_done) break;
-            uint32_t tile = claimed ? tq.next() : tq.first();
-            claimed = true;
+            ws_st(kWsTcur, kNone);
+            const uint32_t flags = ws_ld(kWsFlags);
+            if (flags & 2u) break;   // the queue is done
+            PtTileQueue<kWavesPerBlock> tq = PtTileQueue<kWavesPerBlock>::restore(s_tq[wv]);
+            uint32_t tile = (flags & 1u) ? tq.next() : tq.first();
             tile = __builtin_amdgcn_readfirstlane(tile);
-            if (tile == kNone) {
-                queue_done = true;
-                break;
+            tq.save(s_tq[wv], lane);
+            ws_st(kWsFlags, tile == kNone ? 3u : 1u);   // claimed (and done)
+            if (tile == kNone) break;
+#if PT_DIAG && !PT_DIAG_WAVES_ONLY
+            didx_cur = (uint32_t)n_tiles_diag;
+            if (dtl && lane == 0 && n_tiles_diag < 32) {
+                dtl[3 * n_tiles_diag + 0] = __builtin_amdgcn_s_memrealtime();
+                dtl[3 * n_tiles_diag + 2] = (unsigned long long)tile << 32;
             }
-            const int tyi = (int)(tile / (uint32_t)tiles_x), txi = (int)(tile % (uint32_t)tiles_x);
+#endif
+#if PT_DIAG
+            ++n_tiles_diag;
+#endif
+            // (a queue entry is a tile or one half of it, pt_tile_queue.h)
+            const uint32_t part = pt_entry_part(tile);
+            const int tyi = (int)(pt_entry_tile(tile) / (uint32_t)tiles_x), txi = (int)(pt_entry_tile(tile) % (uint32_t)tiles_x);
             const int lc = txi * 8 + (lane & 7), lr = tyi * 8 + (lane >> 3);
-            const bool valid = lc < job.ncols && lr < job.nrows;
+            const bool valid = lc < job.ncols && lr < job.nrows && pt_part_has_lane(part, lane);
             const float fx = (float)(job.col0 + lc);                                            // :806
             const float fy = (float)(job.height - 1 - (job.row_start + lr * job.row_stride));   // :803
             const V3 D0 = camera_dir(cam, fx, fy);
@@ -1363,7 +1406,13 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             const uint64_t hm = pt_ballot(items);
             const int nh = __popcll(hm);
             if (nh == 0) {
-                if (job.cost && lane == 0) job.cost[tile] = 1u;
+                if (job.cost && lane == 0) pt_record_cost(job.cost, tile, total_tiles, 1u);
+#if PT_DIAG && !PT_DIAG_WAVES_ONLY
+                if (dtl && lane == 0 && didx_cur < 32) {
+                    dtl[3 * didx_cur + 1] = __builtin_amdgcn_s_memrealtime();
+                    dtl[3 * didx_cur + 2] = ((unsigned long long)tile << 32) | 1u;
+                }
+#endif
                 continue;
             }
             if (items) {   // compacted record slot: the pixel's rank among the tile's item pixels
@@ -1373,12 +1422,13 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 s_nrm[wv][1][slot] = N1.y;
                 s_nrm[wv][2][slot] = N1.z;
             }
-            tcur = tile;
-            tcx = txi;
-            tcy = tyi;
-            hmcur = hm;
-            nhcur = nh;
-            f0next = 0;
+            ws_st(kWsTcur, tile);
+            ws_st(kWsX, (uint32_t)(job.col0 + txi * 8));
+            ws_st(kWsY, (uint32_t)(job.height - 1 - job.row_start) - (uint32_t)(tyi * 8) * (uint32_t)job.row_stride);
+            ws_st(kWsHm, (uint32_t)hm);
+            ws_st(kWsHm + 1, (uint32_t)(hm >> 32));
+            ws_st(kWsNh, (uint32_t)nh);
+            ws_st(kWsF0next, 0u);
         }
     };
     // Fold D: every item of it has ended, its radiance is in the slots of context 1 - cA
@@ -1388,6 +1438,9 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
         // (workgroup scope: the same CU's L1 -- LLVM AMDGPU memory model)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int f0D = (int)ws_ld(kWsF0D), nfD = (int)ws_ld(kWsNfD);
+        const uint32_t tD = ws_ld(kWsTD);
+        const uint64_t hmD = (uint64_t)ws_ld(kWsHmD) | ((uint64_t)ws_ld(kWsHmD + 1) << 32);
         const bool first = f0D == 0, last = f0D + nfD == S;
         if ((hmD >> lane) & 1u) {   // (an item pixel is a valid pixel)
             const float4* sp = (const float4*)(slots + (c * 64 + lane) * (kChunk * 3));   // 96 B, 16-B aligned
@@ -1396,7 +1449,8 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             for (int i = 0; i < kChunk * 3 / 4; ++i)
                 if (i * 4 < nfD * 3) v[i] = sp[i];
             const float* fr = (const float*)v;
-            const int lc = txD * 8 + (lane & 7), lr = tyD * 8 + (lane >> 3);
+            const uint32_t tdi = pt_entry_tile(tD);
+            const int lc = (int)(tdi % (uint32_t)tiles_x) * 8 + (lane & 7), lr = (int)(tdi / (uint32_t)tiles_x) * 8 + (lane >> 3);
             float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
             V3 acc = first ? v3(px[0], px[cs], px[2 * cs]) : v3(s_acc[wv][0][lane], s_acc[wv][1][lane], s_acc[wv][2][lane]);
 #pragma unroll
@@ -1417,20 +1471,24 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 s_acc[wv][2][lane] = acc.z;
             }
         }
-        tile_seg += segD;
+        const uint32_t tile_seg = ws_ld(kWsTileSeg) + segD;   // segments of the tile's folded chunks
+        ws_st(kWsTileSeg, last ? 0u : tile_seg);
         if (last) {
-            if (job.cost && lane == 0) job.cost[tD] = 1u + (tile_seg + 63u) / 64u;   // ~ the tile's pool iterations
-            tile_seg = 0;
+            if (job.cost && lane == 0) pt_record_cost(job.cost, tD, total_tiles, 1u + (tile_seg + 63u) / 64u);   // ~ pool iterations
+#if PT_DIAG && !PT_DIAG_WAVES_ONLY
+            if (dtl && lane == 0 && didxD < 32) {
+                dtl[3 * didxD + 1] = __builtin_amdgcn_s_memrealtime();
+                dtl[3 * didxD + 2] = ((unsigned long long)tD << 32) | (1u + (tile_seg + 63u) / 64u);
+            }
+#endif
         }
         hasD = false;
     };
 
     start_chunk();
-    const uint64_t live = pt_ballot(true);
     const uint32_t stall_limit = (uint32_t)B + 8u;   // an item ends within B + 1 iterations
     uint32_t stall = 0;                               // pool iterations in a row without progress
     uint32_t idle_events = 0;                         // outer iterations in a row without progress
-    uint32_t wave_it = 0;                             // pool iterations of this wave (test hook below)
     bool fault = false;
     // outer loop: the events (D is folded; A becomes D and the next chunk starts); inner loop: pool
     // iterations until an event is due -- the hot loop holds no start / fold code
@@ -1442,16 +1500,26 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
         }
         if (hasA && issA >= nitA && !hasD) {   // A has handed out every item and D is folded
             hasD = true;
-            tD = tA;
-            txD = txA;
-            tyD = tyA;
-            hmD = hmA;
-            f0D = f0A;
-            nfD = nfA;
+            ws_st(kWsTD, ws_ld(kWsTcur));
+            ws_st(kWsHmD, ws_ld(kWsHm));
+            ws_st(kWsHmD + 1, ws_ld(kWsHm + 1));
+            ws_st(kWsF0D, ws_ld(kWsF0A));
+            ws_st(kWsNfD, (uint32_t)nfA);
             outD = outA;
             segD = segA;
+#if PT_DIAG
+            didxD = didxA;
+#endif
             hasA = false;
             cA ^= 1;
+            // (job.guard_cap: ~0u, or a low test value -- PT_MI355_RING_GUARD_CAP -- that ends the
+            // wave after that many chunks, so that the fault path runs on a correct launch)
+            const uint32_t n_chunks = ws_ld(kWsChunks) + 1u;   // chunks retired
+            ws_st(kWsChunks, n_chunks);
+            if (__builtin_expect(n_chunks > job.guard_cap, 0)) {
+                fault = true;
+                break;
+            }
             start_chunk();
             event = true;
             if (outD == 0) continue;   // (D's items had all ended: fold it first)
@@ -1482,11 +1550,10 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                     const int packed = __builtin_bit_cast(int, a0.w);
                     const int sId = packed & 0xff;
                     const int src = packed >> 8;                  // lane owning the pixel
-                    const int slc = txA * 8 + (src & 7), slr = tyA * 8 + (src >> 3);
                     const PtLdsPrim pr = prim_at(s_prim, sId);
-                    rng = seed_int((uint32_t)(job.col0 + slc),
-                                   (uint32_t)(job.height - 1 - (job.row_start + (int)__umul24((uint32_t)slr, (uint32_t)job.row_stride))),
-                                   job.frame_first + (uint32_t)(f0A + fi));                          // :332
+                    // the pixel (tile column + src & 7, tile row + src >> 3) and frame f0A + fi
+                    rng = seed_int(xcur + (uint32_t)(src & 7), ycur - __umul24((uint32_t)(src >> 3), (uint32_t)job.row_stride),
+                                   fA + (uint32_t)fi);                                                // :332
                     P = v3(a0.x, a0.y, a0.z);                                            // :313 (bounce 0)
                     n = v3(s_nrm[wv][0][slot_pm], s_nrm[wv][1][slot_pm], s_nrm[wv][2][slot_pm]);
                     ret = emissive0(pr);                                                 // :319
@@ -1503,10 +1570,11 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 for (int d = npop - ntaken; d > 0; --d) tm &= ~(1ull << (63 - __builtin_clzll(tm)));
                 ctx1 = (ctx1 & ~tm) | (cA ? tm : 0ull);
             }
-            // no lane holds an item: an event is due (or the wave is done)
-            if ((live & ~idle) == 0 && ntaken == 0) break;
+            // no lane holds an item: an event is due (or the wave is done).  (Every lane of the wave
+            // is live: full blocks, no lane has returned.)
+            if (idle == ~0ull && ntaken == 0) break;
             idle_events = 0;
-            if (COUNT) ++n_iter;
+            if (COUNT || PT_DIAG) ++n_iter;
             bool done = false;
             if (had || took) {
                 D = normalize(add(n, random_unit_vector(rng)));                          // :316
@@ -1535,7 +1603,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             }
             // items that ended, per context (SALU)
             const uint64_t ended = pt_ballot(done);
-            const uint64_t active = (live & ~idle) | tm;
+            const uint64_t active = ~idle | tm;
             const int endA = __popcll(ended & (cA ? ctx1 : ~ctx1));
             outA -= endA;
             outD -= __popcll(ended) - endA;
@@ -1546,11 +1614,8 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             }
             // guard (never reached): an item in flight ends within B + 1 iterations, so B + 8
             // iterations in a row without a hand-out or an ended item are a scheduling fault
-            // (job.guard_cap: ~0u, or a low test value -- PT_MI355_RING_GUARD_CAP -- that ends the
-            // wave after that many iterations, so that the fault path runs on a correct launch)
             stall = (ntaken != 0 || ended != 0) ? 0u : stall + 1u;
-            ++wave_it;
-            if (__builtin_expect(stall > stall_limit || wave_it > job.guard_cap, 0)) {
+            if (__builtin_expect(stall > stall_limit, 0)) {
                 fault = true;
                 break;
             }
@@ -1562,8 +1627,17 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     // returns PT_EKERNEL), instead of a hung GPU
     if (__builtin_expect(fault, 0) && lane == 0 && job.err) {
         atomicAdd(&job.err[0], 1u);
-        atomicMin(&job.err[1], hasA ? tA : (hasD ? tD : 0u));
+        atomicMin(&job.err[1], pt_entry_tile(hasA ? ws_ld(kWsTcur) : (hasD ? ws_ld(kWsTD) : 0u)));
     }
+#if PT_DIAG
+    if (job.counters && lane == 0) {
+        unsigned long long* rec = job.counters + 32 + 4 * (size_t)(blockIdx.x * kWavesPerBlock + wv);
+        rec[0] = r_birth;
+        rec[1] = __builtin_amdgcn_s_memrealtime();
+        rec[2] = n_tiles_diag;
+        rec[3] = n_iter;
+    }
+#endif
     if (COUNT) {
         for (int off = 32; off > 0; off >>= 1) {
             n_seg += __shfl_xor(n_seg, off, 64);
@@ -1642,16 +1716,12 @@ constexpr int kRingMinFrames = PT_RING_MIN;
 template <int LAYOUT, bool COUNT>
 bool launch_ct(const PtJob& job, hipStream_t st, unsigned tiles)
 {
-#if PT_DIAG
-    return false;   // (the diagnostic timelines are render_body's)
-#else
     constexpr int wpb = waves_per_block<false>();
     auto k = pt_render_ct_kernel<LAYOUT, COUNT>;
     const unsigned blocks = (unsigned)std::min<long>(pt_resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
     if (!job.ct_slots || (uint64_t)blocks * wpb > job.ct_waves) return false;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
     return true;
-#endif
 }
 
 template <int LAYOUT, bool ENV>
@@ -1723,33 +1793,50 @@ __device__ uint32_t block_exclusive_scan_1024(uint32_t* a, uint32_t* wave_tot)
 
 __global__ __launch_bounds__(1024) void pt_schedule_kernel(const uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
                                                            uint32_t* __restrict__ units, uint32_t* __restrict__ nunits,
-                                                           uint32_t n, uint32_t kUnitCost)
+                                                           uint32_t n, uint32_t kUnitCost, uint32_t split_div)
 {
-    __shared__ uint32_t hist[kCostBins];    // tiles per bin, then the bin's first schedule position
+    __shared__ uint32_t hist[kCostBins];    // entries per bin, then the bin's first schedule position
     __shared__ uint32_t ucnt[kCostBins];    // units per bin, then the bin's first unit index
     __shared__ uint32_t wave_tot[17];
+    __shared__ unsigned long long s_total;
     const uint32_t t = threadIdx.x;
     constexpr uint32_t nt = 1024, kBatch = 8;
-    constexpr uint32_t kNoBin = 0xffffffffu;
+    constexpr uint32_t kNoTile = 0xffffffffu;
     hist[t] = 0;
+    if (t == 0) s_total = 0;
     __syncthreads();
-    auto bin_at = [&](uint32_t i) {   // descending cost: the most expensive tiles get bin 0
-        if (i >= n) return kNoBin;
-        const uint32_t c = cost[i];
+    // a tile's cost: its two words (a whole tile's second is 0, a split tile's halves are one each)
+    auto cost_at = [&](uint32_t i) { return i < n ? cost[i] + cost[n + i] : kNoTile; };
+    // descending cost: the most expensive entries get bin 0
+    auto bin_of = [&](uint32_t c) {
         return (uint32_t)(kCostBins - 1) - (c < (uint32_t)(kCostBins - 1) ? c : (uint32_t)(kCostBins - 1));
     };
+    // (0) the split threshold: tiles costing more than total / split_div become two entries
+    uint32_t thr = 0xffffffffu;
+    if (split_div) {
+        unsigned long long part = 0;
+        for (uint32_t i = t; i < n; i += nt) part += cost[i] + cost[n + i];
+        atomicAdd(&s_total, part);
+        __syncthreads();
+        const unsigned long long th = s_total / split_div;
+        thr = th < 0xffffffffull ? (uint32_t)th : 0xffffffffu;
+    }
+    auto split = [&](uint32_t c) { return c > thr && c >= 2u; };
     for (uint32_t base = 0; base < n; base += nt * kBatch) {
-        uint32_t b[kBatch];
+        uint32_t c[kBatch];
 #pragma unroll
-        for (uint32_t k = 0; k < kBatch; ++k) b[k] = bin_at(base + k * nt + t);   // loads in flight together
+        for (uint32_t k = 0; k < kBatch; ++k) c[k] = cost_at(base + k * nt + t);   // loads in flight together
 #pragma unroll
-        for (uint32_t k = 0; k < kBatch; ++k)
-            if (b[k] != kNoBin) atomicAdd(&hist[b[k]], 1u);
+        for (uint32_t k = 0; k < kBatch; ++k) {
+            if (c[k] == kNoTile) continue;
+            if (split(c[k])) atomicAdd(&hist[bin_of((c[k] + 1u) >> 1)], 2u);
+            else atomicAdd(&hist[bin_of(c[k])], 1u);
+        }
     }
     __syncthreads();
     const uint32_t count = hist[t];   // bin t
-    block_exclusive_scan_1024(hist, wave_tot);   // hist[b]: the bin's first schedule position
-    // units of bin t: cost c = kCostBins - 1 - t, k = max(1, U / c) tiles each
+    const uint32_t npos = block_exclusive_scan_1024(hist, wave_tot);   // hist[b]: the bin's first schedule position
+    // units of bin t: cost c = kCostBins - 1 - t, k = max(1, U / c) entries each
     const uint32_t c = (uint32_t)(kCostBins - 1) - t;
     const uint32_t per = c >= kUnitCost || c == 0 ? 1u : kUnitCost / c;
     ucnt[t] = (count + per - 1) / per;
@@ -1772,23 +1859,33 @@ __global__ __launch_bounds__(1024) void pt_schedule_kernel(const uint32_t* __res
     __syncthreads();   // hist is advanced by the scatter below
     if (t == 0) {
         *nunits = total_units;
-        units[total_units] = n;
+        units[total_units] = npos;
     }
-    // scatter: order[position] = tile (positions inside a bin in arbitrary order)
+    // scatter: order[position] = entry (positions inside a bin in arbitrary order; a split tile's
+    // two halves land next to each other only by chance)
     for (uint32_t base = 0; base < n; base += nt * kBatch) {
-        uint32_t b[kBatch];
+        uint32_t cc[kBatch];
 #pragma unroll
-        for (uint32_t k = 0; k < kBatch; ++k) b[k] = bin_at(base + k * nt + t);
+        for (uint32_t k = 0; k < kBatch; ++k) cc[k] = cost_at(base + k * nt + t);
 #pragma unroll
-        for (uint32_t k = 0; k < kBatch; ++k)
-            if (b[k] != kNoBin) order[atomicAdd(&hist[b[k]], 1u)] = base + k * nt + t;
+        for (uint32_t k = 0; k < kBatch; ++k) {
+            if (cc[k] == kNoTile) continue;
+            const uint32_t tile = base + k * nt + t;
+            if (split(cc[k])) {
+                const uint32_t b = bin_of((cc[k] + 1u) >> 1);
+                order[atomicAdd(&hist[b], 1u)] = tile | (1u << PT_TILE_PART_SHIFT);
+                order[atomicAdd(&hist[b], 1u)] = tile | (2u << PT_TILE_PART_SHIFT);
+            } else {
+                order[atomicAdd(&hist[bin_of(cc[k])], 1u)] = tile;
+            }
+        }
     }
 }
 
 }  // namespace
 
 hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* units, uint32_t* nunits,
-                              uint32_t ntiles, hipStream_t st)
+                              uint32_t ntiles, uint32_t split, hipStream_t st)
 {
     if (ntiles == 0) return hipSuccess;
     if (!cost || !order || !units || !nunits) return hipErrorInvalidValue;
@@ -1802,7 +1899,16 @@ hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* u
         unit_cost = (uint32_t)((2ull * ntiles) / (3ull * waves));
         unit_cost = std::min(kUnitCostMax, std::max(kUnitCostMin, unit_cost));
     }
-    hipLaunchKernelGGL(pt_schedule_kernel, dim3(1), dim3(1024), 0, st, cost, order, units, nunits, ntiles, unit_cost);
+    uint32_t split_div = 0;
+    {   // tiles costing more than 1/split of a wave's share are split (pt_tile_queue.h)
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        split_div = split ? (uint32_t)cus * 20u * split : 0u;
+    }
+    hipLaunchKernelGGL(pt_schedule_kernel, dim3(1), dim3(1024), 0, st, cost, order, units, nunits, ntiles, unit_cost,
+                       split_div);
     return hipGetLastError();
 }
 

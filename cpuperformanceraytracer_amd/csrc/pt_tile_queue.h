@@ -23,6 +23,13 @@
 // only grows, so a load that shows it used up is right; without the screening the tail's atomics
 // tripled the launch time).  Victims are visited in a per-wave rotation.
 //
+// A queue entry is a tile or one half of it: the schedule splits the few tiles that cost more than
+// half a wave's share of the launch (tiles whose paths all bounce to the last bounce: 64 pixels x S
+// frames x (B + 1) segments), so that a launch of about one such tile per wave -- 1080p at 8 spp is
+// 72 pool iterations per heavy tile against a mean of 69 per wave -- does not end on the waves that
+// drew two.  Part 1 is the tile's rows 0-3 (lanes 0-31), part 2 its rows 4-7 (lanes 32-63); the
+// other half's pixels are treated as outside the image.
+//
 // The whole wave runs the queue code (uniform control flow): every value is wave-uniform and lives
 // in scalar registers -- held by lane 0 alone they took vector registers across the whole pool
 // loop, which the 96-VGPR budget of the ambient kernel spilled.  Only the counter atomics are
@@ -35,12 +42,28 @@
 
 #include "pt_kernel.h"   // PT_NQUEUES
 
+__device__ __forceinline__ uint32_t pt_entry_tile(uint32_t e) { return e & PT_TILE_MASK; }
+__device__ __forceinline__ uint32_t pt_entry_part(uint32_t e) { return e >> PT_TILE_PART_SHIFT; }
+__device__ __forceinline__ bool pt_part_has_lane(uint32_t part, int lane)
+{
+    return part == 0u || (uint32_t)(lane >> 5) + 1u == part;
+}
+// The schedule's cost record of entry e (cost: 2 x ntiles words; a tile's cost is the sum of its
+// two words -- a whole tile writes 0 into its second)
+__device__ __forceinline__ void pt_record_cost(uint32_t* cost, uint32_t e, uint32_t ntiles, uint32_t w)
+{
+    const uint32_t tile = pt_entry_tile(e), part = pt_entry_part(e);
+    cost[part == 2u ? ntiles + tile : tile] = w;
+    if (part == 0u) cost[ntiles + tile] = 0u;
+}
+
 template <int WAVES_PER_BLOCK>
 struct PtTileQueue {
     static constexpr uint32_t kNone = 0xffffffffu;
     unsigned int* base;       // PT_NQUEUES counters, 128 B apart (zeroed before the launch)
     const uint32_t* order;    // schedule position -> tile, or nullptr (raster order)
     const uint32_t* units;    // unit -> first schedule position (units[u + 1] its end), or nullptr
+                              // (order: entries -- tile | part << PT_TILE_PART_SHIFT)
     uint32_t nunits, ntiles, ngroups, qg, wave;
     uint32_t dead = 0;        // groups known to be exhausted
     uint32_t c_pos = kNone, c_end = kNone;   // the current unit's remaining schedule positions
@@ -54,6 +77,46 @@ struct PtTileQueue {
         ngroups = gridDim.x < PT_NQUEUES ? gridDim.x : PT_NQUEUES;   // small grids: fewer groups
         qg = blockIdx.x % ngroups;
         wave = (blockIdx.x / ngroups) * WAVES_PER_BLOCK + (uint32_t)wv;   // index inside the group
+    }
+    // The queue's state as kWords words (a wave's LDS copy: a kernel whose pool loop must not hold
+    // the queue in scalar registers keeps it there between dequeues -- render_body_ct).  save: lane 0
+    // stores; restore: uniform loads.
+    static constexpr int kWords = 14;
+    __device__ PtTileQueue() = default;
+    __device__ void save(uint32_t* w, int lane) const
+    {
+        if (lane != 0) return;
+        const uint64_t p[3] = {(uint64_t)base, (uint64_t)order, (uint64_t)units};
+        for (int i = 0; i < 3; ++i) {
+            w[2 * i] = (uint32_t)p[i];
+            w[2 * i + 1] = (uint32_t)(p[i] >> 32);
+        }
+        w[6] = nunits;
+        w[7] = ntiles;
+        w[8] = ngroups;
+        w[9] = qg;
+        w[10] = wave;
+        w[11] = dead;
+        w[12] = c_pos;
+        w[13] = c_end;
+    }
+    __device__ static PtTileQueue restore(const uint32_t* w)
+    {
+        auto u = [&](int i) { return (uint32_t)__builtin_amdgcn_readfirstlane(w[i]); };
+        auto ptr = [&](int i) { return (uint64_t)u(2 * i) | ((uint64_t)u(2 * i + 1) << 32); };
+        PtTileQueue q;
+        q.base = (unsigned int*)ptr(0);
+        q.order = (const uint32_t*)ptr(1);
+        q.units = (const uint32_t*)ptr(2);
+        q.nunits = u(6);
+        q.ntiles = u(7);
+        q.ngroups = u(8);
+        q.qg = u(9);
+        q.wave = u(10);
+        q.dead = u(11);
+        q.c_pos = u(12);
+        q.c_end = u(13);
+        return q;
     }
     __device__ uint32_t group_waves(uint32_t g) const
     {
@@ -69,8 +132,8 @@ struct PtTileQueue {
     // (defensive: a schedule entry outside the launch's tiles ends the wave instead of faulting)
     __device__ uint32_t tile_at(uint32_t i) const
     {
-        const uint32_t tile = order ? __builtin_amdgcn_readfirstlane(order[i]) : i;
-        return tile < ntiles ? tile : kNone;
+        const uint32_t e = order ? __builtin_amdgcn_readfirstlane(order[i]) : i;
+        return pt_entry_tile(e) < ntiles && pt_entry_part(e) < 3u ? e : kNone;
     }
 
     // one returning atomic for the wave (its first active lane), the result broadcast

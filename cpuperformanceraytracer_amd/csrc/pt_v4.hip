@@ -629,7 +629,8 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     tile = tq.first();   // (the whole wave: uniform, scalar registers)
     tile = __builtin_amdgcn_readfirstlane(tile);
     while (tile != kNone) {
-    const int tcol = ((int)tile % tiles_x) * 8, trow = ((int)tile / tiles_x) * 8;
+    // (v4's schedules hold whole tiles: pt_capi.cpp use_sched)
+    const int tcol = ((int)pt_entry_tile(tile) % tiles_x) * 8, trow = ((int)pt_entry_tile(tile) / tiles_x) * 8;
     uint32_t tile_work = 1;   // pool iterations of this tile (the schedule's cost)
 
     // this lane's pixel (phase C) and its accumulator
@@ -955,7 +956,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
         acc_p[cs] = acc.y;
         acc_p[2 * cs] = acc.z;
     }
-    if (job.cost && lane == 0) job.cost[tile] = tile_work;
+    if (job.cost && lane == 0) pt_record_cost(job.cost, tile, (uint32_t)ntiles, tile_work);
     tile = __builtin_amdgcn_readfirstlane(next_tile);
     }
     if (COUNT) {

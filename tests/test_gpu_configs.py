@@ -91,3 +91,35 @@ def test_scheduled_launches_match_oracle():
     got = buf.cpu().numpy().reshape(H, W, 3)
     ref = pyoracle.render(W, H, nframes=K, num_bounces=B)
     assert bits_equal(got, ref), mismatch_report(got, ref)
+
+
+@pytest.mark.parametrize("pool,env,frames", [("ct", False, 2), ("ct", False, 12), ("body", False, 2),
+                                             ("body", False, 12), ("ring", False, 48), ("body", True, 3)])
+def test_split_schedules_match_oracle(monkeypatch, pool, env, frames):
+    """Split tiles (pt_tile_queue.h: a scheduled launch queues a tile that costs more than 1/split
+    of a wave's share of the launch as its two halves, rows 0-3 and 4-7, taken by any two waves)
+    change only which wave traces which pixels.  PT_MI355_SPLIT=100000 (read by pt_init) splits
+    every tile of cost >= 2 from the second launch on; three launches of one geometry -- whole,
+    split, split -- equal the oracle bit for bit on the continuous-tiles pool (ct), the chunked
+    pool (body: PT_MI355_NO_CT=1), the ring pool (>= 48 frames) and the env kernel."""
+    import torch
+    import cpuperformanceraytracer_amd as pt
+    from cpuperformanceraytracer_amd.device import render_device, set_env_map
+    monkeypatch.setenv("PT_MI355_SPLIT", "100000")
+    if pool != "ct":
+        monkeypatch.setenv("PT_MI355_NO_CT", "1")
+    W, H, B, K = 256, 128, 8, 3              # 512 tiles: scheduled
+    pt.init(num_bounces=B)
+    envmap = None
+    if env:
+        rng = np.random.default_rng(5)
+        envmap = (rng.random((16, 32, 3), dtype=np.float32) * 4.0 + 0.01).astype(np.float32)
+        set_env_map(envmap, 0, B)
+    buf = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda:0")
+    for k in range(K):
+        render_device(buf, W, H, frame_first=1 + k * frames, nframes=frames, num_bounces=B, use_env=env)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy().reshape(H, W, 3)
+    ref = pyoracle.render(W, H, nframes=K * frames, num_bounces=B, env=envmap)
+    assert bits_equal(got, ref), mismatch_report(got, ref)
+    pt.shutdown()

@@ -225,7 +225,7 @@ def test_pool_guard_fires_loudly(monkeypatch, pool):
     w, h, f = 64, 64, 49                      # >= 48 frames: one launch
     if pool == "ring":
         monkeypatch.setenv("PT_MI355_NO_CT", "1")
-    monkeypatch.setenv("PT_MI355_RING_GUARD_CAP", "8")
+    monkeypatch.setenv("PT_MI355_RING_GUARD_CAP", "2")   # ct: 7 chunks per tile; ring: per-tile iterations
     pt.init(num_bounces=8, samples_per_frame=f)
     buf = np.zeros((h, w, 3), np.float32)
     with pytest.raises(N.PtError) as ei:
