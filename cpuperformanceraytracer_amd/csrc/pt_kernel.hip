@@ -1200,8 +1200,8 @@ constexpr uint32_t kCtWaveFloats = 2u * 64u * (uint32_t)kChunk * 3u;   // per wa
 // item-pixel mask, item pixels, next chunk's first frame), A's first frame, D (entry, first frame,
 // frames, item-pixel mask), the tile's folded segments, flags (1 claimed, 2 queue done), chunks
 enum : int {
-    kWsTcur, kWsX, kWsY, kWsHm, kWsHm1, kWsNh, kWsF0next, kWsF0A, kWsTD, kWsF0D, kWsNfD, kWsHmD, kWsHmD1,
-    kWsTileSeg, kWsFlags, kWsChunks, kWsWords
+    kWsTcur, kWsHm, kWsHm1, kWsNh, kWsF0next, kWsF0A, kWsTD, kWsF0D, kWsNfD, kWsHmD, kWsHmD1,
+    kWsTileSeg, kWsSegA, kWsSegD, kWsFlags, kWsChunks, kWsWords
 };
 
 template <int LAYOUT, bool COUNT>
@@ -1219,6 +1219,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     __shared__ float4 s_rec[kWavesPerBlock][64];
     __shared__ float s_nrm[kWavesPerBlock][3][64];
     __shared__ float s_acc[kWavesPerBlock][3][64];
+    __shared__ uint32_t s_seed[kWavesPerBlock][64];   // the item pixels' seed terms (x, y) of :332
     __shared__ uint32_t s_ws[kWavesPerBlock][kWsWords];   // the events' wave-uniform state (below)
     __shared__ uint32_t s_tq[kWavesPerBlock][PtTileQueue<kWavesPerBlock>::kWords];   // the wave's tile queue
     {
@@ -1306,40 +1307,40 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     // In the pool loop (scalar registers): the chunk contexts -- A hands out items; D has handed out
     // all of its items
     int cA = 0;                            // A's slot context (D's is 1 - cA)
-    bool hasA = false, hasD = false;
     int nfA = 0;
-    uint32_t fA = 0;                       // frame_first + A's first frame
-    uint32_t xcur = 0, ycur = 0;           // the seed's pixel terms of A's tile's (0, 0) pixel (:332)
-    int issA = 0, nitA = 0, outA = 0, outD = 0;
-    uint32_t divA = 0;                     // k / nfA as (k * divA) >> 16 (exact for k < 64 nfA, nfA < 32)
-    uint32_t segA = 0, segD = 0;           // segments traced for the chunk's items (the schedule's cost)
+    uint32_t fterm = 0;                    // the seed's frame term of A's first frame (:332)
+    int issA = 0, nitA = 0;                // A's items handed out / all (nitA 0: no A)
+    // D's items are the ones in flight when A retired (every earlier chunk was folded then): the lanes
+    // that still hold one.  A lane whose D item ends takes A's items from then on.
+    bool hasD = false;
+    uint64_t dmask = 0;
+    // k / nfA as (k * divA) >> 16 (exact for k < 64 nfA, nfA < 32; __umul24 reads bits 0-23); bit 31:
+    // this launch records the schedule's costs (segments traced, counted in s_ws)
+    uint32_t divA = 0;
+    const uint32_t rec_cost = (job.cost || PT_DIAG) ? 0x80000000u : 0u;
     // per lane: the item (bounce 0: none) and the float index of its radiance slot in `slots`
     V3 P = zero, D = zero, T = zero, ret = zero, n = zero;
     uint32_t rng = 0;
     int bounce = 0;
     int it_addr = 0;
-    uint64_t ctx1 = 0;   // lanes whose item belongs to slot context 1 (SALU bookkeeping)
 
     // Start chunks until A is set or the queue is empty: the current tile's next chunk, or a new tile
     // (render_body's phase A, run by the whole wave while lanes may hold D's items -- item registers
     // untouched).  A new tile starts only when the previous tile's last chunk has handed out every
     // item, so its records are free.
     auto start_chunk = [&]() {
-        while (!hasA) {
+        while (nitA == 0) {
             const int f0next = (int)ws_ld(kWsF0next);
             if (ws_ld(kWsTcur) != kNone && f0next < S) {   // the current tile's next chunk
-                hasA = true;
-                fA = job.frame_first + (uint32_t)f0next;
+                // frame < 2^24 (C ABI): umul24(frame_first + f0A + fi) = fterm + fi * 26699 (mod 2^32)
+                fterm = __umul24(job.frame_first + (uint32_t)f0next, 26699u);
                 nfA = S - f0next < kChunk ? S - f0next : kChunk;
                 ws_st(kWsF0A, (uint32_t)f0next);
                 ws_st(kWsF0next, (uint32_t)(f0next + nfA));
-                xcur = ws_ld(kWsX);
-                ycur = ws_ld(kWsY);
-                divA = (65536u + (uint32_t)nfA - 1u) / (uint32_t)nfA;
+                divA = ((65536u + (uint32_t)nfA - 1u) / (uint32_t)nfA) | rec_cost;
                 issA = 0;
-                nitA = (int)ws_ld(kWsNh) * nfA;
-                outA = nitA;
-                segA = 0;
+                nitA = (int)ws_ld(kWsNh) * nfA;   // >= 1
+                ws_st(kWsSegA, 0u);
 #if PT_DIAG
                 didxA = didx_cur;
 #endif
@@ -1359,6 +1360,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             if (dtl && lane == 0 && n_tiles_diag < 32) {
                 dtl[3 * n_tiles_diag + 0] = __builtin_amdgcn_s_memrealtime();
                 dtl[3 * n_tiles_diag + 2] = (unsigned long long)tile << 32;
+                dtl[3 * n_tiles_diag + 1] = n_iter;   // (until the last fold: the pool iteration of the claim)
             }
 #endif
 #if PT_DIAG
@@ -1421,10 +1423,11 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 s_nrm[wv][0][slot] = N1.x;
                 s_nrm[wv][1][slot] = N1.y;
                 s_nrm[wv][2][slot] = N1.z;
+                // the seed's pixel terms (:332; x, y < 2^24)
+                s_seed[wv][slot] = __umul24((uint32_t)(job.col0 + lc), 1973u) +
+                                   __umul24((uint32_t)(job.height - 1 - (job.row_start + lr * job.row_stride)), 9277u);
             }
             ws_st(kWsTcur, tile);
-            ws_st(kWsX, (uint32_t)(job.col0 + txi * 8));
-            ws_st(kWsY, (uint32_t)(job.height - 1 - job.row_start) - (uint32_t)(tyi * 8) * (uint32_t)job.row_stride);
             ws_st(kWsHm, (uint32_t)hm);
             ws_st(kWsHm + 1, (uint32_t)(hm >> 32));
             ws_st(kWsNh, (uint32_t)nh);
@@ -1471,14 +1474,17 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 s_acc[wv][2][lane] = acc.z;
             }
         }
-        const uint32_t tile_seg = ws_ld(kWsTileSeg) + segD;   // segments of the tile's folded chunks
+        const uint32_t tile_seg = ws_ld(kWsTileSeg) + ws_ld(kWsSegD);   // segments of the tile's folded chunks
         ws_st(kWsTileSeg, last ? 0u : tile_seg);
         if (last) {
             if (job.cost && lane == 0) pt_record_cost(job.cost, tD, total_tiles, 1u + (tile_seg + 63u) / 64u);   // ~ pool iterations
 #if PT_DIAG && !PT_DIAG_WAVES_ONLY
             if (dtl && lane == 0 && didxD < 32) {
+                const unsigned long long it0 = dtl[3 * didxD + 1];
                 dtl[3 * didxD + 1] = __builtin_amdgcn_s_memrealtime();
-                dtl[3 * didxD + 2] = ((unsigned long long)tD << 32) | (1u + (tile_seg + 63u) / 64u);
+                // low word: the tile's cost | the pool iterations from its claim to its last fold << 16
+                dtl[3 * didxD + 2] = ((unsigned long long)tD << 32) | (1u + (tile_seg + 63u) / 64u) |
+                                     ((n_iter - it0) << 16);
             }
 #endif
         }
@@ -1494,23 +1500,24 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     // iterations until an event is due -- the hot loop holds no start / fold code
     while (!fault) {
         bool event = false;
-        if (hasD && outD == 0) {   // D's last item ended: fold it
+        if (hasD && dmask == 0) {   // D's last item ended: fold it
             fold_D();
             event = true;
         }
-        if (hasA && issA >= nitA && !hasD) {   // A has handed out every item and D is folded
-            hasD = true;
+        if (nitA > 0 && issA >= nitA && !hasD) {   // A has handed out every item and D is folded
             ws_st(kWsTD, ws_ld(kWsTcur));
             ws_st(kWsHmD, ws_ld(kWsHm));
             ws_st(kWsHmD + 1, ws_ld(kWsHm + 1));
             ws_st(kWsF0D, ws_ld(kWsF0A));
             ws_st(kWsNfD, (uint32_t)nfA);
-            outD = outA;
-            segD = segA;
+            hasD = true;
+            dmask = pt_ballot(bounce != 0);
+            ws_st(kWsSegD, ws_ld(kWsSegA));
 #if PT_DIAG
             didxD = didxA;
 #endif
-            hasA = false;
+            nitA = 0;   // no A
+            issA = 0;
             cA ^= 1;
             // (job.guard_cap: ~0u, or a low test value -- PT_MI355_RING_GUARD_CAP -- that ends the
             // wave after that many chunks, so that the fault path runs on a correct launch)
@@ -1522,9 +1529,9 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             }
             start_chunk();
             event = true;
-            if (outD == 0) continue;   // (D's items had all ended: fold it first)
+            if (dmask == 0) continue;   // (D's items had all ended: fold it first)
         }
-        if (!hasA && !hasD) break;   // every chunk of every tile of the queue is folded
+        if (nitA == 0 && !hasD) break;   // every chunk of every tile of the queue is folded
         // (guard, never reached: with a chunk left, an outer iteration folds, retires or runs the pool)
         idle_events = event ? 0u : idle_events + 1u;
         if (__builtin_expect(idle_events > 2u, 0)) {
@@ -1536,8 +1543,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             const uint64_t idle = pt_ballot(!had);
             bool took = false;
             int ntaken = 0;
-            uint64_t tm = 0;   // the lanes that take an item now
-            if (idle != 0 && hasA && issA < nitA) {
+            if (idle != 0 && issA < nitA) {
                 const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
                 const int k = issA + rank;
                 const bool take = !had && k < nitA;
@@ -1551,9 +1557,8 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                     const int sId = packed & 0xff;
                     const int src = packed >> 8;                  // lane owning the pixel
                     const PtLdsPrim pr = prim_at(s_prim, sId);
-                    // the pixel (tile column + src & 7, tile row + src >> 3) and frame f0A + fi
-                    rng = seed_int(xcur + (uint32_t)(src & 7), ycur - __umul24((uint32_t)(src >> 3), (uint32_t)job.row_stride),
-                                   fA + (uint32_t)fi);                                                // :332
+                    // seed_int of the pixel and frame f0A + fi (:332)
+                    rng = (s_seed[wv][slot_pm] + fterm + __umul24((uint32_t)fi, 26699u)) | 1u;
                     P = v3(a0.x, a0.y, a0.z);                                            // :313 (bounce 0)
                     n = v3(s_nrm[wv][0][slot_pm], s_nrm[wv][1][slot_pm], s_nrm[wv][2][slot_pm]);
                     ret = emissive0(pr);                                                 // :319
@@ -1564,11 +1569,6 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 const int npop = __popcll(idle);
                 ntaken = npop < nitA - issA ? npop : nitA - issA;
                 issA += ntaken;
-                // the takers are the first ntaken idle lanes (SALU: drop the highest idle lanes when A
-                // runs out of items)
-                tm = idle;
-                for (int d = npop - ntaken; d > 0; --d) tm &= ~(1ull << (63 - __builtin_clzll(tm)));
-                ctx1 = (ctx1 & ~tm) | (cA ? tm : 0ull);
             }
             // no lane holds an item: an event is due (or the wave is done).  (Every lane of the wave
             // is live: full blocks, no lane has returned.)
@@ -1601,17 +1601,15 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                     bounce = 0;
                 }
             }
-            // items that ended, per context (SALU)
             const uint64_t ended = pt_ballot(done);
-            const uint64_t active = ~idle | tm;
-            const int endA = __popcll(ended & (cA ? ctx1 : ~ctx1));
-            outA -= endA;
-            outD -= __popcll(ended) - endA;
-            if (job.cost) {   // (only launches whose tile costs feed the next schedule): segments traced
-                const int inA = __popcll(active & (cA ? ctx1 : ~ctx1));
-                segA += (uint32_t)inA;
-                segD += (uint32_t)(__popcll(active) - inA);
+            if ((int)divA < 0) {   // (only launches whose tile costs feed the next schedule): segments traced
+                const int inD = __popcll(dmask), in_all = __popcll(pt_ballot(had || took));
+                if (lane == 0) {
+                    ws[kWsSegA] += (uint32_t)(in_all - inD);
+                    ws[kWsSegD] += (uint32_t)inD;
+                }
             }
+            dmask &= ~ended;
             // guard (never reached): an item in flight ends within B + 1 iterations, so B + 8
             // iterations in a row without a hand-out or an ended item are a scheduling fault
             stall = (ntaken != 0 || ended != 0) ? 0u : stall + 1u;
@@ -1619,15 +1617,15 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 fault = true;
                 break;
             }
-            if (hasD && outD == 0) break;                        // fold due
-            if (hasA && issA >= nitA && !hasD) break;            // retire due
+            if (hasD && dmask == 0) break;                       // fold due
+            if (nitA > 0 && issA >= nitA && !hasD) break;        // retire due
         }
     }
     // a fault ends the wave with its chunks unfinished: recorded in the job's error words (the host
     // returns PT_EKERNEL), instead of a hung GPU
     if (__builtin_expect(fault, 0) && lane == 0 && job.err) {
         atomicAdd(&job.err[0], 1u);
-        atomicMin(&job.err[1], pt_entry_tile(hasA ? ws_ld(kWsTcur) : (hasD ? ws_ld(kWsTD) : 0u)));
+        atomicMin(&job.err[1], pt_entry_tile(nitA > 0 ? ws_ld(kWsTcur) : (hasD ? ws_ld(kWsTD) : 0u)));
     }
 #if PT_DIAG
     if (job.counters && lane == 0) {

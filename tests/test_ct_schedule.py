@@ -27,7 +27,7 @@ def run_wave(tiles, S, B, rng):
     cA, hasA, hasD = 0, False, False
     A, Dc = {}, {}
     lanes = [None] * 64          # item: dict(tile, f, ctx, rem)
-    ctx1 = 0
+    dmask = 0                    # lanes holding D's items (set at retire, bits only cleared)
     folds, ended_items = [], []
     iters = 0
 
@@ -36,7 +36,7 @@ def run_wave(tiles, S, B, rng):
         while not hasA:
             if tcur is not None and f0next < S:
                 nf = min(KCHUNK, S - f0next)
-                A = dict(tile=tcur, hm=hmcur, f0=f0next, nf=nf, iss=0, nit=nhcur * nf, out=nhcur * nf)
+                A = dict(tile=tcur, hm=hmcur, f0=f0next, nf=nf, iss=0, nit=nhcur * nf)
                 f0next += nf
                 hasA = True
                 break
@@ -64,16 +64,19 @@ def run_wave(tiles, S, B, rng):
     fault = False
     while not fault:
         event = False
-        if hasD and Dc["out"] == 0:
+        if hasD and dmask == 0:
             fold_D()
             event = True
         if hasA and A["iss"] >= A["nit"] and not hasD:
             Dc = A
             hasD, hasA = True, False
+            # every earlier chunk is folded: the items in flight are all A's
+            assert all(it is None or it["ctx"] == cA for it in lanes)
+            dmask = sum(1 << i for i in range(64) if lanes[i] is not None)
             cA ^= 1
             start_chunk()
             event = True
-            if Dc["out"] == 0:
+            if dmask == 0:
                 continue
         if not hasA and not hasD:
             break
@@ -83,16 +86,14 @@ def run_wave(tiles, S, B, rng):
             break
         while True:
             idle = [i for i in range(64) if lanes[i] is None]
-            ntaken, tm = 0, 0
+            ntaken = 0
             if idle and hasA and A["iss"] < A["nit"]:
                 ntaken = min(len(idle), A["nit"] - A["iss"])
                 for r, lane in enumerate(idle[:ntaken]):
                     k = A["iss"] + r
                     slot, fi = k // A["nf"], k % A["nf"]
                     lanes[lane] = dict(tile=A["tile"], f=A["f0"] + fi, ctx=cA, rem=rng.randint(1, B + 1), slot=slot)
-                    tm |= 1 << lane
                 A["iss"] += ntaken
-                ctx1 = (ctx1 & ~tm) | (tm if cA else 0)
             if not any(lanes) and ntaken == 0:
                 break
             iters += 1
@@ -106,18 +107,14 @@ def run_wave(tiles, S, B, rng):
                     ended |= 1 << i
                     ended_items.append((it["tile"], it["f"], it["slot"]))
                     lanes[i] = None
-            mask_A = ctx1 if cA else ~ctx1
-            endA = bin(ended & mask_A & ((1 << 64) - 1)).count("1")
-            A_out_dec, D_out_dec = endA, bin(ended).count("1") - endA
-            if hasA or A_out_dec:
-                A["out"] -= A_out_dec
-            if hasD or D_out_dec:
-                Dc["out"] -= D_out_dec
+            # a lane of dmask holds a D item until it ends (then it is idle or takes A's)
+            assert all(lanes[i] is None or lanes[i]["ctx"] != cA for i in range(64) if (dmask >> i) & 1)
+            dmask &= ~ended
             stall = 0 if (ntaken or ended) else stall + 1
             if stall > stall_limit:
                 fault = True
                 break
-            if hasD and Dc["out"] == 0:
+            if hasD and dmask == 0:
                 break
             if hasA and A["iss"] >= A["nit"] and not hasD:
                 break
