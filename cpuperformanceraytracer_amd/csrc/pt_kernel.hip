@@ -1492,8 +1492,6 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     };
 
     start_chunk();
-    const uint32_t stall_limit = (uint32_t)B + 8u;   // an item ends within B + 1 iterations
-    uint32_t stall = 0;                               // pool iterations in a row without progress
     uint32_t idle_events = 0;                         // outer iterations in a row without progress
     bool fault = false;
     // outer loop: the events (D is folded; A becomes D and the next chunk starts); inner loop: pool
@@ -1610,13 +1608,10 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 }
             }
             dmask &= ~ended;
-            // guard (never reached): an item in flight ends within B + 1 iterations, so B + 8
-            // iterations in a row without a hand-out or an ended item are a scheduling fault
-            stall = (ntaken != 0 || ended != 0) ? 0u : stall + 1u;
-            if (__builtin_expect(stall > stall_limit, 0)) {
-                fault = true;
-                break;
-            }
+            // (no stall guard here: every lane that holds an item advances it by one segment per
+            // iteration and ends it after at most B + 1, hand-outs are bounded by nitA, and an iteration
+            // without an item in flight or a hand-out leaves the loop -- so the loop ends; the outer
+            // loop's guard covers the event logic)
             if (hasD && dmask == 0) break;                       // fold due
             if (nitA > 0 && issA >= nitA && !hasD) break;        // retire due
         }
