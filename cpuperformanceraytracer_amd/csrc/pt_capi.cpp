@@ -627,7 +627,7 @@ int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
     j.nunits = ls.nunits;
     j.cost = ls.cost;
     j.err = dv.derr;
-    if (!j.env && !g.no_ct) {   // ambient launches: the continuous-tiles pool
+    if (!g.no_ct) {   // the continuous-tiles pool (pt_kernel.hip render_body_ct)
         if (!dv.dct) {   // its slots, once per device: 12 KiB per wave of the resident grid (~60 MB)
             const uint32_t waves = pt_ct_resident_waves();
             if (hipMalloc(&dv.dct, (size_t)waves * pt_ct_wave_floats() * sizeof(float)) == hipSuccess) dv.dct_waves = waves;

@@ -1204,11 +1204,15 @@ enum : int {
     kWsTileSeg, kWsSegA, kWsSegD, kWsFlags, kWsChunks, kWsWords
 };
 
-template <int LAYOUT, bool COUNT>
+// ENV (config 4, the env-map miss term): a missed segment's item is queued with its direction and
+// radiance so far (s_envq, 32 B), and the queue is drained 64 at a time by the whole wave -- the
+// coherent texel gathers of render_body's env kernel; a drain writes the items' radiance + texel
+// (render_body's `cp + c`) to their slots.  D's fold drains the whole queue first.
+template <int LAYOUT, bool ENV, bool COUNT>
 __device__ __forceinline__ void render_body_ct(const PtJob& job)
 {
     const PtScene* __restrict__ sc = job.scene;
-    constexpr int kWavesPerBlock = waves_per_block<false>();
+    constexpr int kWavesPerBlock = waves_per_block<ENV>();
     constexpr bool QV = true;
     __shared__ PtLdsPrim s_prim[PT_NPRIMS];
     __shared__ AxisRow s_axis[PT_NQUADS * kAxisRowsPerQuad<true>];
@@ -1222,6 +1226,8 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     __shared__ uint32_t s_seed[kWavesPerBlock][64];   // the item pixels' seed terms (x, y) of :332
     __shared__ uint32_t s_ws[kWavesPerBlock][kWsWords];   // the events' wave-uniform state (below)
     __shared__ uint32_t s_tq[kWavesPerBlock][PtTileQueue<kWavesPerBlock>::kWords];   // the wave's tile queue
+    constexpr int kQ = ENV ? 128 : 1;   // queued misses: direction + slot, radiance so far
+    __shared__ float4 s_envq[ENV ? kWavesPerBlock : 1][kQ][2];
     {
         const int t = threadIdx.x;
         if (t < PT_NPRIMS) {
@@ -1385,7 +1391,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 if (COUNT) n_samp += (unsigned long long)S;
                 V3 c_keep;
                 if (h.best == PT_SUPER_FAR) {                                 // :305-310
-                    c_keep = add(zero, amb);
+                    c_keep = add(zero, miss_radiance<ENV>(job, amb, D0));         // (:408 env kernel)
                     if (COUNT) n_esc += (unsigned long long)S;
                 } else {
                     const PtLdsPrim pr = prim_at(s_prim, h.id);
@@ -1434,8 +1440,24 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             ws_st(kWsF0next, 0u);
         }
     };
+    // ENV: the queued misses [q0, q0 + m) (m <= 64), one per lane: radiance + the texel into the slot
+    int qn = 0;   // queued misses (wave-uniform)
+    auto drain = [&](int q0, int m) {
+        if (ENV && lane < m) {
+            const float4 e = s_envq[ENV ? wv : 0][q0 + lane][0], r = s_envq[ENV ? wv : 0][q0 + lane][1];
+            const V3 c = env_sample(job.env, job.env_w, job.env_h, v3(e.x, e.y, e.z));
+            float* const o = slots + __builtin_bit_cast(int, e.w);
+            o[0] = r.x + c.x;
+            o[1] = r.y + c.y;
+            o[2] = r.z + c.z;
+        }
+    };
     // Fold D: every item of it has ended, its radiance is in the slots of context 1 - cA
     auto fold_D = [&]() {
+        if (ENV && qn > 0) {   // (D's misses among them)
+            drain(0, qn);
+            qn = 0;
+        }
         const int c = cA ^ 1;
         // the slots were written by this wave's lanes (global stores): complete them before reading
         // (workgroup scope: the same CU's L1 -- LLVM AMDGPU memory model)
@@ -1476,14 +1498,18 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
         }
         const uint32_t tile_seg = ws_ld(kWsTileSeg) + ws_ld(kWsSegD);   // segments of the tile's folded chunks
         ws_st(kWsTileSeg, last ? 0u : tile_seg);
+        // the schedule's cost: segments / 64 -- about the tile's pool iterations.  (Lane-time measured
+        // with s_memrealtime instead ordered the tiles worse: 1080p 8 spp 0.2605 vs 0.2535 ms, 1 spp
+        // 0.130 vs 0.112 -- an iteration's time is set more by what shares the SIMD than by the tile.)
+        const uint32_t tile_cost = 1u + (tile_seg + 63u) / 64u;
         if (last) {
-            if (job.cost && lane == 0) pt_record_cost(job.cost, tD, total_tiles, 1u + (tile_seg + 63u) / 64u);   // ~ pool iterations
+            if (job.cost && lane == 0) pt_record_cost(job.cost, tD, total_tiles, tile_cost);
 #if PT_DIAG && !PT_DIAG_WAVES_ONLY
             if (dtl && lane == 0 && didxD < 32) {
                 const unsigned long long it0 = dtl[3 * didxD + 1];
                 dtl[3 * didxD + 1] = __builtin_amdgcn_s_memrealtime();
                 // low word: the tile's cost | the pool iterations from its claim to its last fold << 16
-                dtl[3 * didxD + 2] = ((unsigned long long)tD << 32) | (1u + (tile_seg + 63u) / 64u) |
+                dtl[3 * didxD + 2] = ((unsigned long long)tD << 32) | tile_cost |
                                      ((n_iter - it0) << 16);
             }
 #endif
@@ -1573,13 +1599,14 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             if (idle == ~0ull && ntaken == 0) break;
             idle_events = 0;
             if (COUNT || PT_DIAG) ++n_iter;
-            bool done = false;
+            bool done = false, queued = false;
             if (had || took) {
                 D = normalize(add(n, random_unit_vector(rng)));                          // :316
                 const Hit h = trace<DemofoxScene, false, QV, true>(s_axis, s_qv, P, D);
                 if (COUNT) ++n_seg, n_fb += (unsigned long long)h.fb;
                 if (h.best == PT_SUPER_FAR) {                                     // :305-310
-                    ret = add(ret, amb);
+                    if (ENV) queued = true;   // the env term is added at the drain (:408)
+                    else ret = add(ret, amb);
                     done = true;
                     if (COUNT) ++n_esc;
                 } else {
@@ -1592,11 +1619,26 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                     done = bounce > B;
                 }
                 if (done) {
-                    float* c = slots + it_addr;
-                    c[0] = ret.x;
-                    c[1] = ret.y;
-                    c[2] = ret.z;
+                    if (!queued) {
+                        float* c = slots + it_addr;
+                        c[0] = ret.x;
+                        c[1] = ret.y;
+                        c[2] = ret.z;
+                    }
                     bounce = 0;
+                }
+            }
+            if (ENV) {
+                const uint64_t qm = pt_ballot(queued);
+                if (queued) {
+                    const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
+                    s_envq[ENV ? wv : 0][qn + r][0] = make_float4(D.x, D.y, D.z, __builtin_bit_cast(float, it_addr));
+                    s_envq[ENV ? wv : 0][qn + r][1] = make_float4(ret.x, ret.y, ret.z, 0.0f);
+                }
+                qn += __popcll(qm);
+                if (qn >= 64) {   // a full wave of misses: evaluate the last 64
+                    qn -= 64;
+                    drain(qn, 64);
                 }
             }
             const uint64_t ended = pt_ballot(done);
@@ -1675,7 +1717,13 @@ template <int LAYOUT, bool COUNT>
 __global__ __launch_bounds__(64 * waves_per_block<false>()) __attribute__((amdgpu_waves_per_eu(PT_AMBIENT_WAVES, PT_AMBIENT_WAVES))) void
 pt_render_ct_kernel(PtJob job)
 {
-    render_body_ct<LAYOUT, COUNT>(job);
+    render_body_ct<LAYOUT, false, COUNT>(job);
+}
+
+template <int LAYOUT, bool COUNT>
+__global__ __launch_bounds__(64 * waves_per_block<true>()) void pt_render_ct_env_kernel(PtJob job)
+{
+    render_body_ct<LAYOUT, true, COUNT>(job);
 }
 
 template <int LAYOUT, bool ENV, bool COUNT, bool MULTI, bool RING>
@@ -1706,11 +1754,18 @@ constexpr int kRingMinFrames = PT_RING_MIN;
 
 // One-chunk ambient launches on the continuous-tiles pool (render_body_ct) when the caller provides
 // its slots for the whole grid; false: not launched (render_body then).
-template <int LAYOUT, bool COUNT>
+template <int LAYOUT, bool ENV, bool COUNT>
+constexpr auto ct_kernel_of()
+{
+    if constexpr (ENV) return pt_render_ct_env_kernel<LAYOUT, COUNT>;
+    else return pt_render_ct_kernel<LAYOUT, COUNT>;
+}
+
+template <int LAYOUT, bool ENV, bool COUNT>
 bool launch_ct(const PtJob& job, hipStream_t st, unsigned tiles)
 {
-    constexpr int wpb = waves_per_block<false>();
-    auto k = pt_render_ct_kernel<LAYOUT, COUNT>;
+    constexpr int wpb = waves_per_block<ENV>();
+    auto k = ct_kernel_of<LAYOUT, ENV, COUNT>();
     const unsigned blocks = (unsigned)std::min<long>(pt_resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
     if (!job.ct_slots || (uint64_t)blocks * wpb > job.ct_waves) return false;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
@@ -1722,10 +1777,9 @@ hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 {
     const unsigned tiles = (unsigned)((job.ncols + 7) / 8) * (unsigned)((job.nrows + 7) / 8);
     const bool multi = job.nframes > kChunk;
-    if constexpr (!ENV) {   // the ambient kernel: the continuous-tiles pool when its slots are provided
-        if (count ? launch_ct<LAYOUT, true>(job, st, tiles) : launch_ct<LAYOUT, false>(job, st, tiles))
-            return hipGetLastError();
-    }
+    // the continuous-tiles pool when its slots are provided
+    if (count ? launch_ct<LAYOUT, ENV, true>(job, st, tiles) : launch_ct<LAYOUT, ENV, false>(job, st, tiles))
+        return hipGetLastError();
     const bool ring = !ENV && job.nframes >= kRingMinFrames && job.nframes > kChunk;
     if (count) {
         if (ring) launch_k<LAYOUT, ENV, true, true, !ENV>(job, st, tiles);
@@ -1909,14 +1963,21 @@ uint32_t pt_ct_wave_floats() { return kCtWaveFloats; }
 
 uint32_t pt_ct_resident_waves()
 {
+    static_assert(waves_per_block<false>() == waves_per_block<true>(), "one block shape for the CT kernels");
     constexpr int wpb = waves_per_block<false>();
-    const int r[6] = {pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, false>, 64 * wpb),
-                      pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, true>, 64 * wpb),
-                      pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, false>, 64 * wpb),
-                      pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, true>, 64 * wpb),
-                      pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, false>, 64 * wpb),
-                      pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, true>, 64 * wpb)};
-    return (uint32_t)*std::max_element(r, r + 6) * (uint32_t)wpb;
+    const int r[12] = {pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, false>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, true>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, false>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, true>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, false>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, true>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_INTERLEAVED, false>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_INTERLEAVED, true>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_PLANAR8, false>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_PLANAR8, true>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_TILED_PLANAR8, false>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_TILED_PLANAR8, true>, 64 * wpb)};
+    return (uint32_t)*std::max_element(r, r + 12) * (uint32_t)wpb;
 }
 
 hipError_t pt_launch_render(const PtJob& job_in, hipStream_t st, bool count)

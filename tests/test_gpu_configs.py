@@ -94,14 +94,15 @@ def test_scheduled_launches_match_oracle():
 
 
 @pytest.mark.parametrize("pool,env,frames", [("ct", False, 2), ("ct", False, 12), ("body", False, 2),
-                                             ("body", False, 12), ("ring", False, 48), ("body", True, 3)])
+                                             ("body", False, 12), ("ring", False, 48), ("body", True, 3),
+                                             ("ct", True, 3), ("ct", True, 12)])
 def test_split_schedules_match_oracle(monkeypatch, pool, env, frames):
     """Split tiles (pt_tile_queue.h: a scheduled launch queues a tile that costs more than 1/split
     of a wave's share of the launch as its two halves, rows 0-3 and 4-7, taken by any two waves)
     change only which wave traces which pixels.  PT_MI355_SPLIT=100000 (read by pt_init) splits
     every tile of cost >= 2 from the second launch on; three launches of one geometry -- whole,
     split, split -- equal the oracle bit for bit on the continuous-tiles pool (ct), the chunked
-    pool (body: PT_MI355_NO_CT=1), the ring pool (>= 48 frames) and the env kernel."""
+    pool (body: PT_MI355_NO_CT=1), the ring pool (>= 48 frames) and the env kernels (ct, body)."""
     import torch
     import cpuperformanceraytracer_amd as pt
     from cpuperformanceraytracer_amd.device import render_device, set_env_map
