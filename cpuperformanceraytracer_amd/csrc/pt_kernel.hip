@@ -1721,7 +1721,7 @@ pt_render_ct_kernel(PtJob job)
 }
 
 template <int LAYOUT, bool COUNT>
-__global__ __launch_bounds__(64 * waves_per_block<true>()) void pt_render_ct_env_kernel(PtJob job)
+__global__ __launch_bounds__(64 * waves_per_block<true>()) __attribute__((amdgpu_waves_per_eu(5, 5))) void pt_render_ct_env_kernel(PtJob job)
 {
     render_body_ct<LAYOUT, true, COUNT>(job);
 }
