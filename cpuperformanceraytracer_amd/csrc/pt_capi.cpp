@@ -612,6 +612,28 @@ int queue_done(Dev& dv, unsigned slot, hipStream_t st, bool zeroed_next)
     return PT_OK;
 }
 
+// The continuous-tiles pools' slot area (pt_kernel.hip render_body_ct, pt_v4.hip pt_v4_ct_kernel) for
+// a launch in ring slot ls.slot on `st`: nullptr (the per-tile pool kernels) with PT_MI355_NO_CT=1.
+int use_ct_slots(Dev& dv, const LaunchSched& ls, hipStream_t st, float** slots, uint32_t* waves)
+{
+    *slots = nullptr;
+    *waves = 0;
+    if (g.no_ct) return PT_OK;
+    if (!dv.dct) {   // once per device: 12 KiB per wave of the resident grid (~60 MB)
+        const uint32_t w = pt_ct_resident_waves();
+        if (hipMalloc(&dv.dct, (size_t)w * pt_ct_wave_floats() * sizeof(float)) == hipSuccess) dv.dct_waves = w;
+        else dv.dct = nullptr, (void)hipGetLastError();   // (the per-tile pools then: correct, slower)
+    }
+    *slots = dv.dct;
+    *waves = dv.dct_waves;
+    if (dv.dct) {   // launches on several streams share the slots: one after the other
+        if (dv.ct_slot >= 0 && dv.queue_stream[dv.ct_slot] != st)
+            if (hipEvent_t ev = slot_order(dv, (unsigned)dv.ct_slot)) HIP_TRY(hipStreamWaitEvent(st, ev, 0));
+        dv.ct_slot = (int)ls.slot;
+    }
+    return PT_OK;
+}
+
 int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
 {
     LaunchSched ls;
@@ -627,20 +649,7 @@ int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
     j.nunits = ls.nunits;
     j.cost = ls.cost;
     j.err = dv.derr;
-    if (!g.no_ct) {   // the continuous-tiles pool (pt_kernel.hip render_body_ct)
-        if (!dv.dct) {   // its slots, once per device: 12 KiB per wave of the resident grid (~60 MB)
-            const uint32_t waves = pt_ct_resident_waves();
-            if (hipMalloc(&dv.dct, (size_t)waves * pt_ct_wave_floats() * sizeof(float)) == hipSuccess) dv.dct_waves = waves;
-            else dv.dct = nullptr, (void)hipGetLastError();   // (render_body then: correct, slower)
-        }
-        j.ct_slots = dv.dct;
-        j.ct_waves = dv.dct_waves;
-        if (dv.dct) {   // launches on several streams share the slots: one after the other
-            if (dv.ct_slot >= 0 && dv.queue_stream[dv.ct_slot] != st)
-                if (hipEvent_t ev = slot_order(dv, (unsigned)dv.ct_slot)) HIP_TRY(hipStreamWaitEvent(st, ev, 0));
-            dv.ct_slot = (int)ls.slot;
-        }
-    }
+    if ((rc = use_ct_slots(dv, ls, st, &j.ct_slots, &j.ct_waves))) return rc;
     hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
     return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_render's early return)
@@ -1089,7 +1098,9 @@ int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count)
 {
     LaunchSched ls;
     int rc;
-    if ((rc = use_dev(dv)) || (rc = use_sched(dv, sched_key(j), st, &ls, 0u))) return rc;   // (v4: whole tiles)
+    // v4 takes whole tiles: its per-tile kernel runs launches of < 8 frames (and PT_MI355_NO_CT=1), and
+    // split tiles measured slower on the continuous-tiles one (0.3666 vs 0.3633 ms at 1080p 8 spp)
+    if ((rc = use_dev(dv)) || (rc = use_sched(dv, sched_key(j), st, &ls, 0u))) return rc;
     if (j.env_mode != PT_V4_ENV_NONE) j.env = dv.denv;
     j.queue = ls.queue;
     j.queue_next = ls.queue_next;
@@ -1097,6 +1108,8 @@ int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count)
     j.units = ls.units;
     j.nunits = ls.nunits;
     j.cost = ls.cost;
+    // (the v4 pool's slots per wave: pt_v4_ct_wave_floats() <= pt_ct_wave_floats(), pt_v4.hip)
+    if ((rc = use_ct_slots(dv, ls, st, &j.ct_slots, &j.ct_waves))) return rc;
     hipError_t e = pt_launch_v4(j, g.v4scene, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "v4 render launch failed: %s", hipGetErrorString(e));
     return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_v4's early return)

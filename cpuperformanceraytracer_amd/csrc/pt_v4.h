@@ -62,6 +62,10 @@ struct PtV4Job {
     const uint32_t* units;
     const uint32_t* nunits;
     uint32_t* cost;                 // per-tile cost written by this launch, or nullptr
+    // continuous-tiles pool (pt_v4.hip pt_v4_ct_kernel): pt_ct_wave_floats() f32 per wave for ct_waves
+    // waves (the diffuse kernels' slot area, pt_kernel.h); nullptr: the per-tile pool kernel
+    float* ct_slots;
+    uint32_t ct_waves;
 };
 
 // Scene description in AddQuad/Sphere/MaterialToScene order (v4 :1368-1401).

@@ -573,6 +573,171 @@ __device__ __forceinline__ size_t out_index(const PtV4Job& j, int x, int r)   //
            ((size_t)ly * j.tile_w + (size_t)(lx & ~7)) * 3u + (size_t)(lx & 7);
 }
 
+// One iteration of an item's path: GetColorForRay's bounce loop, :733-909 (the pool kernels' shared
+// body).  done: the path ended (queued: DEFER, the miss's env term is deferred to the queue's drain).
+template <int ENV, bool COUNT, bool DEF, int FEXP, bool DFL>
+__device__ __forceinline__ void v4_segment(const PtV4Job& job, const PtV4Scene& sc, const PtV4Mat* s_mat,
+                                           const MatX* s_mx, const float4* s_sc, const Tex& tex, bool random,
+                                           bool rejection, int B, bool all_sky, V3& pos, V3& dir, V3& T, V3& ret,
+                                           uint32_t& rng, int& bounce, bool& done, bool& queued,
+                                           unsigned long long& n_seg, unsigned long long& n_esc,
+                                           unsigned long long& n_fb, unsigned long long& n_sky)
+{
+    constexpr bool DEFER = ENV != PT_V4_ENV_NONE_;
+    // one iteration of GetColorForRay's bounce loop (:733-909)
+    int fb = 0;
+    const Hit h = all_sky ? Hit{kSuperFar, v3(0.0f, 0.0f, 0.0f), false, 0} : trace<DEF>(sc, pos, dir, s_sc, fb);
+    if (COUNT) ++n_seg, n_fb += (unsigned long long)fb, n_sky += all_sky ? 1ull : 0ull;
+    const bool miss = h.dist == kSuperFar;
+    done = false;
+    if (miss) {
+        if (DEFER) {
+            queued = true;
+        } else {
+            V3 amb = v3(0.11f, 0.1f, 0.15f);   // :782
+            if (ENV == PT_V4_ENV_EQUIRECT_) amb = equirect(tex, v3(-dir.x, dir.y, -dir.z), random, rng);
+            if (ENV == PT_V4_ENV_CUBEMAP_) amb = cubemap(tex, dir, random, rng);
+            ret = v3(fma_(amb.x, T.x, ret.x), fma_(amb.y, T.y, ret.y), fma_(amb.z, T.z, ret.z));   // :787
+        }
+        done = true;
+        if (COUNT) ++n_esc;
+    } else {
+        if (ENV != PT_V4_ENV_NONE_ && random) {   // the env sample's two draws happen on hits too
+            wang(rng);
+            wang(rng);
+        }
+        const PtV4Mat& M = s_mat[h.mat];
+        if (h.inside) {   // :797, Beer's law
+            if (FEXP == 2 ? job.fast_exp != 0 : FEXP == 1)   // USE_FAST_APPROXIMATE_EXP 1 (:783-784)
+                T = mul(T, v3(approx_exp(-M.refr_color[0] * h.dist), approx_exp(-M.refr_color[1] * h.dist),
+                              approx_exp(-M.refr_color[2] * h.dist)));
+            else                // 0 (:785-787): exp_ps -> glibc-exact expf (pt_libmf.h)
+                T = mul(T, v3(pt::lm::expf_glibc(-M.refr_color[0] * h.dist),
+                              pt::lm::expf_glibc(-M.refr_color[1] * h.dist),
+                              pt::lm::expf_glibc(-M.refr_color[2] * h.dist)));
+        }
+        const V3 em = ld3(M.emissive);
+        if (bounce == B) {   // last iteration: only its emissive term is used
+            ret = v3(fma_(em.x, T.x, ret.x), fma_(em.y, T.y, ret.y), fma_(em.z, T.z, ret.z));
+            done = true;
+        } else {
+            float spec = M.spec_chance, refr = M.refr_chance;
+            if (spec > 0.0f) {   // :807-829 (the Fresnel result is used only with a specular chance)
+                const MatX& X = s_mx[h.mat];
+                const float nspec = fresnel_m(h.inside, M.ior, X, h.n, dir, M.spec_chance);
+                const float rscc = X.rscc;
+                spec = nspec;
+                refr = refr * fma_(-nspec, rscc, rscc);
+            }
+            const float roll = randf(rng);   // :831
+            const bool do_spec = spec > 0.0f && roll < spec;
+            const bool do_refr = !do_spec && refr > 0.0f && roll < spec + refr;
+            const float diff_chance = max_ps(1.0f - (spec + refr), 0.0f);
+            float prob = do_spec ? spec : (do_refr ? refr : diff_chance);
+            prob = max_ps(prob, 0.001f);
+            const float nudge = kNudge * (do_refr ? -1.0f : 1.0f);   // :848-849
+            const V3 npos = v3(fma_(nudge, h.n.x, fma_(dir.x, h.dist, pos.x)),
+                               fma_(nudge, h.n.y, fma_(dir.y, h.dist, pos.y)),
+                               fma_(nudge, h.n.z, fma_(dir.z, h.dist, pos.z)));
+            // :852-888.  The reference evaluates the diffuse, specular and refraction
+            // directions and selects one; only the selected one (and the diffuse direction
+            // the specular one lerps towards) is evaluated here.  Both random unit vectors
+            // are still drawn, in the reference's order (diffuse first).
+            const bool unified = rejection;   // one straight-line direction for all three outcomes
+            uint32_t s_diff = rng, s_refr = rng;
+            uint32_t h0 = 0, h1 = 0, h2 = 0;   // unified: the chosen stream's three draws
+            if (unified) {
+                // both streams' draws once (6 hashes, not 6 skipped + 3 redrawn), then the
+                // chosen stream's three selected -- the same values in the same order
+                const uint32_t d0 = wang(rng), d1 = wang(rng), d2 = wang(rng);
+                const uint32_t r0 = wang(rng), r1 = wang(rng), r2 = wang(rng);
+                h0 = do_refr ? r0 : d0;
+                h1 = do_refr ? r1 : d1;
+                h2 = do_refr ? r2 : d2;
+            } else {
+                rng_skip(rng, rejection ? 3 : 2);
+                s_refr = rng;
+                rng_skip(rng, rejection ? 3 : 2);
+            }
+            V3 ndir;
+            if (unified) {
+                // The three outcomes share one shape: a unit vector u drawn from the chosen
+                // stream, nb = (u +- n) * rcp(sqrt(|u +- n|^2)) (diffuse: n + u; refraction:
+                // u - n == u + (-n) exactly), and -- for specular and refraction -- the
+                // reference's fma lerp from a mirror direction R (reflect or refract) towards
+                // nb.  Evaluated once per lane with per-lane operands instead of as two
+                // divergent branches; every value is the branch's own, bit for bit.
+                const V3 u = ruv_rejection_of(h0, h1, h2);
+                const V3 sn = do_refr ? neg(h.n) : h.n;
+                const V3 a = u + sn;
+                const V3 nb = a * rcp_nonneg(sqrt_(dot(a, a)));   // |a| <= 2
+                const float vdn = dot(dir, h.n);
+                // reflect (:861-862): dir - 2 dot(dir, n) n as fma
+                const float d2 = 2.0f * vdn;
+                const V3 sd = v3(fma_(-d2, h.n.x, dir.x), fma_(-d2, h.n.y, dir.y), fma_(-d2, h.n.z, dir.z));
+                // refract (rfrct, mathlib.h:781-789); k of the lanes that do not refract is
+                // replaced by 1 so that no lane takes sqrt's slow path for a discarded value
+                const float ior = h.inside ? M.ior : s_mx[h.mat].rior;
+                const float k = fma_(-ior, ior * fma_(-vdn, vdn, 1.0f), 1.0f);
+                const float sk = fma_(ior, vdn, sqrt_(do_refr ? k : 1.0f));
+                V3 rd = v3(fma_(ior, dir.x, -(sk * h.n.x)), fma_(ior, dir.y, -(sk * h.n.y)),
+                           fma_(ior, dir.z, -(sk * h.n.z)));
+                rd = k < 0.0f ? v3(0.0f, 0.0f, 0.0f) : rd;
+                const V3 R = do_refr ? rd : sd;
+                const float rough = do_refr ? M.refr_rough : M.spec_rough;
+                const float rsq = rough * rough;
+                const V3 lr = v3(fma_(rsq, nb.x - R.x, R.x), fma_(rsq, nb.y - R.y, R.y), fma_(rsq, nb.z - R.z, R.z));
+                ndir = (do_spec || do_refr) ? lr : nb;
+            } else if (!do_refr) {
+                uint32_t r = s_diff;
+                V3 diffuse;
+                if (rejection) {
+                    const V3 a = h.n + ruv_rejection(r);
+                    diffuse = a * rcp(sqrt_(dot(a, a)));   // fast_approx_normalize, rsroot -> 1/sqrtf
+                } else {
+                    diffuse = normalize(h.n + ruv_angle(r));
+                }
+                ndir = diffuse;
+                if (do_spec) {
+                    const float d2 = 2.0f * dot(dir, h.n);
+                    const V3 sd = v3(fma_(-d2, h.n.x, dir.x), fma_(-d2, h.n.y, dir.y), fma_(-d2, h.n.z, dir.z));
+                    const float srsq = M.spec_rough * M.spec_rough;
+                    ndir = v3(fma_(srsq, diffuse.x - sd.x, sd.x), fma_(srsq, diffuse.y - sd.y, sd.y),
+                              fma_(srsq, diffuse.z - sd.z, sd.z));
+                }
+            } else {
+                uint32_t r = s_refr;
+                const float ior = h.inside ? M.ior : s_mx[h.mat].rior;
+                const float rrsq = M.refr_rough * M.refr_rough;
+                V3 rd = refract(dir, h.n, ior);
+                if (rejection) {
+                    const V3 a = ruv_rejection(r) - h.n;
+                    const V3 nrd = a * rcp(sqrt_(dot(a, a)));
+                    rd = v3(fma_(rrsq, nrd.x - rd.x, rd.x), fma_(rrsq, nrd.y - rd.y, rd.y),
+                            fma_(rrsq, nrd.z - rd.z, rd.z));
+                } else {
+                    const V3 nrd = normalize(ruv_angle(r) - h.n);
+                    rd = normalize(rd + (nrd - rd) * rrsq);
+                }
+                ndir = rd;
+            }
+            ndir = normalize_small(ndir);   // a unit vector or a lerp of two
+            ret = v3(fma_(em.x, T.x, ret.x), fma_(em.y, T.y, ret.y), fma_(em.z, T.z, ret.z));
+            const V3 cf = do_spec ? ld3(M.spec_color) : ld3(M.albedo);
+            if (!do_refr) T = mul(T, cf);
+            T = T * rcp(prob);   // (prob >= 0.001; materials may set any chance)
+            {   // :891-899 (boost only; the path continues either way)
+                const float pm = max_ps(T.x, max_ps(T.y, T.z));
+                const bool term = randf(rng) > pm;
+                if (!term) T = T * rcp(pm);
+            }
+            pos = npos;
+            dir = ndir;
+            ++bounce;
+        }
+    }
+}
+
 #ifdef PT_V4_WAVES   // A/B builds: force the occupancy (waves per SIMD)
 #define PT_V4_OCC __attribute__((amdgpu_waves_per_eu(PT_V4_WAVES, PT_V4_WAVES)))
 #else
@@ -629,7 +794,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     tile = tq.first();   // (the whole wave: uniform, scalar registers)
     tile = __builtin_amdgcn_readfirstlane(tile);
     while (tile != kNone) {
-    // (v4's schedules hold whole tiles: pt_capi.cpp use_sched)
+    // (this kernel's schedules hold whole tiles: pt_capi.cpp v4_launch)
     const int tcol = ((int)pt_entry_tile(tile) % tiles_x) * 8, trow = ((int)pt_entry_tile(tile) / tiles_x) * 8;
     uint32_t tile_work = 1;   // pool iterations of this tile (the schedule's cost)
 
@@ -722,158 +887,9 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
             if (DEF && pt_ballot(item >= 0 && bounce != 0) == 0)
                 all_sky = pt_ballot(item >= 0 && !sky_ray_v4(dir)) == 0;
             if (item >= 0) {
-                // one iteration of GetColorForRay's bounce loop (:733-909)
-                int fb = 0;
-                const Hit h = all_sky ? Hit{kSuperFar, v3(0.0f, 0.0f, 0.0f), false, 0} : trace<DEF>(sc, pos, dir, s_sc, fb);
-                if (COUNT) ++n_seg, n_fb += (unsigned long long)fb, n_sky += all_sky ? 1ull : 0ull;
-                const bool miss = h.dist == kSuperFar;
                 bool done = false;
-                if (miss) {
-                    if (DEFER) {
-                        queued = true;
-                    } else {
-                        V3 amb = v3(0.11f, 0.1f, 0.15f);   // :782
-                        if (ENV == PT_V4_ENV_EQUIRECT_) amb = equirect(tex, v3(-dir.x, dir.y, -dir.z), random, rng);
-                        if (ENV == PT_V4_ENV_CUBEMAP_) amb = cubemap(tex, dir, random, rng);
-                        ret = v3(fma_(amb.x, T.x, ret.x), fma_(amb.y, T.y, ret.y), fma_(amb.z, T.z, ret.z));   // :787
-                    }
-                    done = true;
-                    if (COUNT) ++n_esc;
-                } else {
-                    if (ENV != PT_V4_ENV_NONE_ && random) {   // the env sample's two draws happen on hits too
-                        wang(rng);
-                        wang(rng);
-                    }
-                    const PtV4Mat& M = s_mat[h.mat];
-                    if (h.inside) {   // :797, Beer's law
-                        if (FEXP == 2 ? job.fast_exp != 0 : FEXP == 1)   // USE_FAST_APPROXIMATE_EXP 1 (:783-784)
-                            T = mul(T, v3(approx_exp(-M.refr_color[0] * h.dist), approx_exp(-M.refr_color[1] * h.dist),
-                                          approx_exp(-M.refr_color[2] * h.dist)));
-                        else                // 0 (:785-787): exp_ps -> glibc-exact expf (pt_libmf.h)
-                            T = mul(T, v3(pt::lm::expf_glibc(-M.refr_color[0] * h.dist),
-                                          pt::lm::expf_glibc(-M.refr_color[1] * h.dist),
-                                          pt::lm::expf_glibc(-M.refr_color[2] * h.dist)));
-                    }
-                    const V3 em = ld3(M.emissive);
-                    if (bounce == B) {   // last iteration: only its emissive term is used
-                        ret = v3(fma_(em.x, T.x, ret.x), fma_(em.y, T.y, ret.y), fma_(em.z, T.z, ret.z));
-                        done = true;
-                    } else {
-                        float spec = M.spec_chance, refr = M.refr_chance;
-                        if (spec > 0.0f) {   // :807-829 (the Fresnel result is used only with a specular chance)
-                            const MatX& X = s_mx[h.mat];
-                            const float nspec = fresnel_m(h.inside, M.ior, X, h.n, dir, M.spec_chance);
-                            const float rscc = X.rscc;
-                            spec = nspec;
-                            refr = refr * fma_(-nspec, rscc, rscc);
-                        }
-                        const float roll = randf(rng);   // :831
-                        const bool do_spec = spec > 0.0f && roll < spec;
-                        const bool do_refr = !do_spec && refr > 0.0f && roll < spec + refr;
-                        const float diff_chance = max_ps(1.0f - (spec + refr), 0.0f);
-                        float prob = do_spec ? spec : (do_refr ? refr : diff_chance);
-                        prob = max_ps(prob, 0.001f);
-                        const float nudge = kNudge * (do_refr ? -1.0f : 1.0f);   // :848-849
-                        const V3 npos = v3(fma_(nudge, h.n.x, fma_(dir.x, h.dist, pos.x)),
-                                           fma_(nudge, h.n.y, fma_(dir.y, h.dist, pos.y)),
-                                           fma_(nudge, h.n.z, fma_(dir.z, h.dist, pos.z)));
-                        // :852-888.  The reference evaluates the diffuse, specular and refraction
-                        // directions and selects one; only the selected one (and the diffuse direction
-                        // the specular one lerps towards) is evaluated here.  Both random unit vectors
-                        // are still drawn, in the reference's order (diffuse first).
-                        const bool unified = rejection;   // one straight-line direction for all three outcomes
-                        uint32_t s_diff = rng, s_refr = rng;
-                        uint32_t h0 = 0, h1 = 0, h2 = 0;   // unified: the chosen stream's three draws
-                        if (unified) {
-                            // both streams' draws once (6 hashes, not 6 skipped + 3 redrawn), then the
-                            // chosen stream's three selected -- the same values in the same order
-                            const uint32_t d0 = wang(rng), d1 = wang(rng), d2 = wang(rng);
-                            const uint32_t r0 = wang(rng), r1 = wang(rng), r2 = wang(rng);
-                            h0 = do_refr ? r0 : d0;
-                            h1 = do_refr ? r1 : d1;
-                            h2 = do_refr ? r2 : d2;
-                        } else {
-                            rng_skip(rng, rejection ? 3 : 2);
-                            s_refr = rng;
-                            rng_skip(rng, rejection ? 3 : 2);
-                        }
-                        V3 ndir;
-                        if (unified) {
-                            // The three outcomes share one shape: a unit vector u drawn from the chosen
-                            // stream, nb = (u +- n) * rcp(sqrt(|u +- n|^2)) (diffuse: n + u; refraction:
-                            // u - n == u + (-n) exactly), and -- for specular and refraction -- the
-                            // reference's fma lerp from a mirror direction R (reflect or refract) towards
-                            // nb.  Evaluated once per lane with per-lane operands instead of as two
-                            // divergent branches; every value is the branch's own, bit for bit.
-                            const V3 u = ruv_rejection_of(h0, h1, h2);
-                            const V3 sn = do_refr ? neg(h.n) : h.n;
-                            const V3 a = u + sn;
-                            const V3 nb = a * rcp_nonneg(sqrt_(dot(a, a)));   // |a| <= 2
-                            const float vdn = dot(dir, h.n);
-                            // reflect (:861-862): dir - 2 dot(dir, n) n as fma
-                            const float d2 = 2.0f * vdn;
-                            const V3 sd = v3(fma_(-d2, h.n.x, dir.x), fma_(-d2, h.n.y, dir.y), fma_(-d2, h.n.z, dir.z));
-                            // refract (rfrct, mathlib.h:781-789); k of the lanes that do not refract is
-                            // replaced by 1 so that no lane takes sqrt's slow path for a discarded value
-                            const float ior = h.inside ? M.ior : s_mx[h.mat].rior;
-                            const float k = fma_(-ior, ior * fma_(-vdn, vdn, 1.0f), 1.0f);
-                            const float sk = fma_(ior, vdn, sqrt_(do_refr ? k : 1.0f));
-                            V3 rd = v3(fma_(ior, dir.x, -(sk * h.n.x)), fma_(ior, dir.y, -(sk * h.n.y)),
-                                       fma_(ior, dir.z, -(sk * h.n.z)));
-                            rd = k < 0.0f ? v3(0.0f, 0.0f, 0.0f) : rd;
-                            const V3 R = do_refr ? rd : sd;
-                            const float rough = do_refr ? M.refr_rough : M.spec_rough;
-                            const float rsq = rough * rough;
-                            const V3 lr = v3(fma_(rsq, nb.x - R.x, R.x), fma_(rsq, nb.y - R.y, R.y), fma_(rsq, nb.z - R.z, R.z));
-                            ndir = (do_spec || do_refr) ? lr : nb;
-                        } else if (!do_refr) {
-                            uint32_t r = s_diff;
-                            V3 diffuse;
-                            if (rejection) {
-                                const V3 a = h.n + ruv_rejection(r);
-                                diffuse = a * rcp(sqrt_(dot(a, a)));   // fast_approx_normalize, rsroot -> 1/sqrtf
-                            } else {
-                                diffuse = normalize(h.n + ruv_angle(r));
-                            }
-                            ndir = diffuse;
-                            if (do_spec) {
-                                const float d2 = 2.0f * dot(dir, h.n);
-                                const V3 sd = v3(fma_(-d2, h.n.x, dir.x), fma_(-d2, h.n.y, dir.y), fma_(-d2, h.n.z, dir.z));
-                                const float srsq = M.spec_rough * M.spec_rough;
-                                ndir = v3(fma_(srsq, diffuse.x - sd.x, sd.x), fma_(srsq, diffuse.y - sd.y, sd.y),
-                                          fma_(srsq, diffuse.z - sd.z, sd.z));
-                            }
-                        } else {
-                            uint32_t r = s_refr;
-                            const float ior = h.inside ? M.ior : s_mx[h.mat].rior;
-                            const float rrsq = M.refr_rough * M.refr_rough;
-                            V3 rd = refract(dir, h.n, ior);
-                            if (rejection) {
-                                const V3 a = ruv_rejection(r) - h.n;
-                                const V3 nrd = a * rcp(sqrt_(dot(a, a)));
-                                rd = v3(fma_(rrsq, nrd.x - rd.x, rd.x), fma_(rrsq, nrd.y - rd.y, rd.y),
-                                        fma_(rrsq, nrd.z - rd.z, rd.z));
-                            } else {
-                                const V3 nrd = normalize(ruv_angle(r) - h.n);
-                                rd = normalize(rd + (nrd - rd) * rrsq);
-                            }
-                            ndir = rd;
-                        }
-                        ndir = normalize_small(ndir);   // a unit vector or a lerp of two
-                        ret = v3(fma_(em.x, T.x, ret.x), fma_(em.y, T.y, ret.y), fma_(em.z, T.z, ret.z));
-                        const V3 cf = do_spec ? ld3(M.spec_color) : ld3(M.albedo);
-                        if (!do_refr) T = mul(T, cf);
-                        T = T * rcp(prob);   // (prob >= 0.001; materials may set any chance)
-                        {   // :891-899 (boost only; the path continues either way)
-                            const float pm = max_ps(T.x, max_ps(T.y, T.z));
-                            const bool term = randf(rng) > pm;
-                            if (!term) T = T * rcp(pm);
-                        }
-                        pos = npos;
-                        dir = ndir;
-                        ++bounce;
-                    }
-                }
+                v4_segment<ENV, COUNT, DEF, FEXP, DFL>(job, sc, s_mat, s_mx, s_sc, tex, random, rejection, B, all_sky, pos,
+                                                       dir, T, ret, rng, bounce, done, queued, n_seg, n_esc, n_fb, n_sky);
                 if (done) {
                     const int p = item & 63, f = item >> 6;
                     qslot = (f * 64 + p) * 3;
@@ -977,24 +993,453 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     }
 }
 
+// ---- continuous tiles (CT): the v4 pool without per-tile tails ----------------------------------
+// pt_v4_kernel's pool drains at the end of every tile chunk (lane efficiency 0.898 at 1080p: the
+// last paths of a chunk run while the other lanes idle).  Here, as in pt_kernel.hip's
+// render_body_ct, a wave's items form one stream over its tiles' chunks: two chunk contexts, A
+// (handing out items) and D (all handed out, in flight), the per-(pixel, frame) radiance in the
+// global slot area (ct_slots, 12 KiB per wave), D folded -- the progressive lerp of its frames in
+// frame order, :1233-1250 -- when its last item ends, the next chunk started as soon as A's last
+// item is handed out and D is folded.  v4 items need no records: each generates its own jittered
+// camera ray from (pixel, frame); a tile's valid pixels are listed in LDS (compacted, with their
+// seed terms).  The deferred env misses keep the wave-wide drains of pt_v4_kernel; a queue entry
+// also carries the radiance so far (48 B), and D's fold drains the whole queue first.  The same
+// operations on the same operands: bit-identical to pt_v4_kernel (the -m gpu v4 parity tests).
+constexpr uint32_t kV4CtWaveFloats = 2u * 64u * (uint32_t)kChunk * 3u;
+static_assert(kV4CtWaveFloats == 2u * 64u * 8u * 3u, "the slot area is the diffuse pool's (pt_ct_wave_floats)");
+enum : int {   // per-wave LDS words of the events (pt_kernel.hip kWs*)
+    kVwTcur, kVwNh, kVwF0next, kVwF0A, kVwTD, kVwF0D, kVwNfD, kVwHmD, kVwHmD1, kVwHm, kVwHm1, kVwTileSeg,
+    kVwSegA, kVwSegD, kVwFlags, kVwSky, kVwSkyD, kVwWords
+};
+
+template <int ENV, int LAYOUT, bool COUNT, bool DEF, int FEXP, bool DFL = false>
+__global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_ct_kernel(PtV4Job job, PtV4Scene sc)
+{
+    __shared__ PtV4Mat s_mat[PT_V4_MAX_OBJECTS];
+    __shared__ float4 s_sc[DEF ? pt_v4_default::kSpheres : 1];   // default scene: sphere centre, radius
+    __shared__ MatX s_mx[PT_V4_MAX_OBJECTS];                        // per-material constants (mat_consts)
+    constexpr bool DEFER = ENV != PT_V4_ENV_NONE_;
+    __shared__ float4 s_qd[DEFER ? kWaves : 1][DEFER ? kEnvQ : 1];   // env dir, rng
+    __shared__ float4 s_qt[DEFER ? kWaves : 1][DEFER ? kEnvQ : 1];   // throughput, slot
+    __shared__ float4 s_qr[DEFER ? kWaves : 1][DEFER ? kEnvQ : 1];   // radiance so far
+    __shared__ float s_acc[kWaves][3][64];    // the pixels' accumulators between a tile's chunks
+    __shared__ uint32_t s_pl[kWaves][64];     // the current tile's valid pixels: lane | X << 8
+    __shared__ uint32_t s_py[kWaves][64];     // and their y term (height - 1 - Y) of the seed
+    __shared__ uint32_t s_ws[kWaves][kVwWords];
+    __shared__ uint32_t s_tq[kWaves][PtTileQueue<kWaves>::kWords];
+    for (int t = threadIdx.x; t < PT_V4_MAX_OBJECTS * 17; t += 64 * kWaves)
+        reinterpret_cast<float*>(s_mat)[t] = reinterpret_cast<const float*>(sc.mat)[t];
+    __syncthreads();
+    if (threadIdx.x < PT_V4_MAX_OBJECTS) s_mx[threadIdx.x] = mat_consts(s_mat[threadIdx.x]);
+    if (DEF && threadIdx.x < pt_v4_default::kSpheres) {
+        const float* c = pt_v4_default::kSphere[threadIdx.x];
+        s_sc[threadIdx.x] = make_float4(c[0], c[1], c[2], c[3]);
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (job.queue_next && blockIdx.x == 0 && threadIdx.x < PT_NQUEUES) job.queue_next[threadIdx.x * 32u] = 0u;   // (as pt_kernel.hip)
+    const int tiles_x = (job.ncols + 7) >> 3;
+    const uint32_t ntiles = (uint32_t)tiles_x * (uint32_t)((job.nrows + 7) >> 3);
+    const int S = job.nframes;
+    float* const slots = job.ct_slots + (size_t)(blockIdx.x * kWaves + wv) * kV4CtWaveFloats;
+    const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;
+    const Tex tex{job.env, job.env_w, job.env_h};
+    const bool random = DFL || job.random_jitter != 0, rejection = DFL || job.rejection != 0;
+    const int B = job.num_bounces;
+    const float W = (float)job.width, H = (float)job.height;
+    const float rW = rcp(W), rH = rcp(H);
+    const float cam_dist = 1.0f;   // (as pt_v4_kernel, InitializeCamera :1500)
+    unsigned long long n_seg = 0, n_esc = 0, n_slots = 0, n_fb = 0, n_sky = 0;
+
+    constexpr uint32_t kNone = PtTileQueue<kWaves>::kNone;
+    PtTileQueue<kWaves>(job.queue, job.order, job.units, job.nunits, ntiles, wv).save(s_tq[wv], lane);
+    // the events' wave-uniform state in LDS (as render_body_ct: the pool loop's SGPRs stay free)
+    uint32_t* const ws = s_ws[wv];
+    auto ws_ld = [&](int k) -> uint32_t { return __builtin_amdgcn_readfirstlane(ws[k]); };
+    auto ws_st = [&](int k, uint32_t v) {
+        if (lane == 0) ws[k] = v;
+    };
+    if (lane == 0) {
+        ws[kVwTcur] = kNone;
+        ws[kVwFlags] = 0u;
+        ws[kVwTileSeg] = 0u;
+    }
+    // pool state (scalar registers): A's slot context, frames, items handed out / all (nitA 0: no A),
+    // its pixels and the item -> (frame, pixel) divisor, its first frame; D
+    int cA = 0, nfA = 0, issA = 0, nitA = 0, nhA = 1;
+    uint32_t div_nh = 0;   // frame-major items: fi = k / nhA as umulhi(k, ceil(2^32 / nhA)) (nhA >= 2)
+    uint32_t fA = 0;
+    bool hasD = false;
+    uint64_t dmask = 0;    // lanes holding D's items
+    const bool rec_cost = job.cost != nullptr;
+    // per lane: the item (slot < 0: none)
+    V3 pos = v3(0.0f, 0.0f, 0.0f), dir = pos, T = pos, ret = pos;
+    uint32_t rng = 0;
+    int bounce = 0;
+    int slot = -1;         // float index of the item's radiance slot in `slots`
+    int qn = 0;            // queued misses (DEFER), wave-uniform
+
+    // a deferred miss: env(d) with the rng state r, fma'd with throughput t onto the radiance so far,
+    // into slot k (pt_v4_kernel's resolve, its slot read replaced by the entry's radiance)
+    auto resolve = [&](V3 d, uint32_t r, V3 t, V3 rs, int k) {
+        V3 amb = v3(0.0f, 0.0f, 0.0f);
+        if (ENV == PT_V4_ENV_EQUIRECT_) amb = equirect(tex, d, random, r);
+        if (ENV == PT_V4_ENV_CUBEMAP_) amb = cubemap(tex, d, random, r);
+        const V3 rt = v3(fma_(amb.x, t.x, rs.x), fma_(amb.y, t.y, rs.y), fma_(amb.z, t.z, rs.z));   // :787
+        float* const o = slots + k;
+        o[0] = fma_(rt.x, 1.0f, 0.0f);   // :1127
+        o[1] = fma_(rt.y, 1.0f, 0.0f);
+        o[2] = fma_(rt.z, 1.0f, 0.0f);
+    };
+    auto drain = [&](int m) {   // the queued misses [0, m), one per lane
+        if (DEFER && lane < m) {
+            const float4 a = s_qd[DEFER ? wv : 0][lane], b = s_qt[DEFER ? wv : 0][lane], c = s_qr[DEFER ? wv : 0][lane];
+            resolve(v3(a.x, a.y, a.z), __builtin_bit_cast(uint32_t, a.w), v3(b.x, b.y, b.z), v3(c.x, c.y, c.z),
+                    __builtin_bit_cast(int, b.w));
+        }
+    };
+
+    // an item's camera ray: mainImage :1092-1130 (as pt_v4_kernel) for pixel column X, flipped row
+    // fyi (height - 1 - Y) and frame
+    const auto camera = [&](int X, int fyi, uint32_t frame, uint32_t& r, V3& d) {
+        // 24 x 24-bit products: X, fyi, frame < 2^24 (C ABI), low words = the u32 products
+        r = 1u | (__umul24((uint32_t)X, 1973u) + __umul24((uint32_t)fyi, 9277u) + __umul24(frame, 26699u));
+        const float jx = randf(r) - 0.5f;
+        const float jy = randf(r) - 0.5f;
+        const float tx = fma_(((float)X + jx) * rW, 2.0f, -1.0f);
+        float ty = fma_(((float)fyi + jy) * rH, 2.0f, -1.0f);
+        ty = ty * (rW * H);
+        const V3 cv = v3(tx, ty, -cam_dist) - v3(0.0f, 0.0f, 0.0f);
+        d = cv * pt::rcp_rn(pt::sqrt_rn(dot(cv, cv)));
+    };
+    // Start chunks until A is set or the queue is done: the current tile's next chunk, or a new tile
+    // (its valid pixels listed; a new tile starts only when the previous tile's last chunk has handed
+    // out every item, so its list is free)
+    auto start_chunk = [&]() {
+        while (nitA == 0) {
+            const int f0next = (int)ws_ld(kVwF0next);
+            if (ws_ld(kVwTcur) != kNone && f0next < S) {
+                nfA = S - f0next < kChunk ? S - f0next : kChunk;
+                fA = job.frame_first + (uint32_t)f0next;
+                ws_st(kVwF0A, (uint32_t)f0next);
+                ws_st(kVwF0next, (uint32_t)(f0next + nfA));
+                nhA = (int)ws_ld(kVwNh);
+                div_nh = nhA > 1 ? (uint32_t)((0x100000000ull + (uint64_t)nhA - 1u) / (uint64_t)nhA) : 0u;
+                issA = 0;
+                nitA = nhA * nfA;   // >= 1
+                if (rec_cost) ws_st(kVwSegA, 0u);
+                break;
+            }
+            ws_st(kVwTcur, kNone);
+            const uint32_t flags = ws_ld(kVwFlags);
+            if (flags & 2u) break;   // the queue is done
+            PtTileQueue<kWaves> tq = PtTileQueue<kWaves>::restore(s_tq[wv]);
+            uint32_t tile = (flags & 1u) ? tq.next() : tq.first();
+            tile = __builtin_amdgcn_readfirstlane(tile);
+            tq.save(s_tq[wv], lane);
+            ws_st(kVwFlags, tile == kNone ? 3u : 1u);
+            if (tile == kNone) break;
+            // (a queue entry is a tile or one half of it, pt_tile_queue.h)
+            const int tcol = ((int)pt_entry_tile(tile) % tiles_x) * 8, trow = ((int)pt_entry_tile(tile) / tiles_x) * 8;
+            const bool valid = (tcol + (lane & 7)) < job.ncols && trow + (lane >> 3) < job.nrows &&
+                               pt_part_has_lane(pt_entry_part(tile), lane);
+            const uint64_t hm = pt_ballot(valid);
+            const int X = job.col0 + tcol + (lane & 7), pr = trow + (lane >> 3);
+            const int fyi = job.height - 1 - (job.row_start + pr * job.row_stride);
+            if (valid) {
+                const int k = __builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+                s_pl[wv][k] = (uint32_t)lane | ((uint32_t)X << 8);   // X < 2^24 (C ABI)
+                s_py[wv][k] = (uint32_t)fyi;
+            }
+            // DEF: the tile's leading frames whose camera rays ALL leave the scene's silhouette
+            // (sky_ray_v4, exact per ray) are rendered here, by the whole wave: pt_v4_kernel skips
+            // their trace when every busy lane holds such a ray, which the pool's mix of tiles
+            // rarely allows -- half of the 1080p tiles are sky.  Each is the pool's miss at bounce 0
+            // (T = 1, ret = 0: v4_segment, resolve) and the fold's lerp, with the same operations.
+            int fsky = 0;
+            if (DEF) {
+                const int orow = LAYOUT == PT_LAYOUT_TILED_PLANAR8 ? job.row_start + pr * job.row_stride : pr;
+                float* const acc_p = valid ? job.buf + out_index<LAYOUT>(job, X, orow) : nullptr;
+                V3 acc = v3(0.0f, 0.0f, 0.0f);
+                if (valid && job.accumulate) acc = v3(acc_p[0], acc_p[cs], acc_p[2 * cs]);
+                for (; fsky < S; ++fsky) {
+                    uint32_t r;
+                    V3 d;
+                    camera(X, fyi, job.frame_first + (uint32_t)fsky, r, d);
+                    if (pt_ballot(valid && !sky_ray_v4(d)) != 0) break;
+                    if (COUNT) n_slots += 64;
+                    if (valid) {
+                        V3 amb = v3(0.11f, 0.1f, 0.15f);   // :782
+                        if (ENV == PT_V4_ENV_EQUIRECT_) amb = equirect(tex, v3(-d.x, d.y, -d.z), random, r);
+                        if (ENV == PT_V4_ENV_CUBEMAP_) amb = cubemap(tex, d, random, r);
+                        const V3 rt = v3(fma_(amb.x, 1.0f, 0.0f), fma_(amb.y, 1.0f, 0.0f), fma_(amb.z, 1.0f, 0.0f));   // :787
+                        const V3 c = v3(fma_(rt.x, 1.0f, 0.0f), fma_(rt.y, 1.0f, 0.0f), fma_(rt.z, 1.0f, 0.0f));     // :1127
+                        if (job.accumulate) {   // :1233-1241
+                            const float bf = rcp((float)(job.frame_first + (uint32_t)fsky) + 1.0f);   // :1200
+                            acc = v3(fma_(bf, c.x - acc.x, acc.x), fma_(bf, c.y - acc.y, acc.y), fma_(bf, c.z - acc.z, acc.z));
+                        } else {                // :1245-1250
+                            acc = c;
+                        }
+                        if (COUNT) ++n_seg, ++n_sky, ++n_esc;
+                    }
+                }
+                if (fsky > 0 && valid) {   // (the pool's first chunk of the tile reads it back)
+                    acc_p[0] = acc.x;
+                    acc_p[cs] = acc.y;
+                    acc_p[2 * cs] = acc.z;
+                }
+                if (fsky == S) {   // the whole tile: ~one pool iteration per frame (the schedule's cost)
+                    if (rec_cost && lane == 0) pt_record_cost(job.cost, tile, ntiles, 1u + (uint32_t)fsky);
+                    continue;
+                }
+            }
+            ws_st(kVwTcur, tile);
+            ws_st(kVwHm, (uint32_t)hm);
+            ws_st(kVwHm1, (uint32_t)(hm >> 32));
+            ws_st(kVwNh, (uint32_t)__popcll(hm));   // >= 1 (a tile of the launch has a pixel)
+            ws_st(kVwF0next, (uint32_t)fsky);
+            ws_st(kVwSky, (uint32_t)fsky);
+        }
+    };
+    // Fold D: its misses drained, every item of it ended; the radiance is in slot context 1 - cA
+    auto fold_D = [&]() {
+        if (DEFER && qn > 0) {
+            drain(qn);
+            qn = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   // (the lanes' slot stores, then reads)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const int c = cA ^ 1;
+        const int f0D = (int)ws_ld(kVwF0D), nfD = (int)ws_ld(kVwNfD);
+        const uint32_t tD = ws_ld(kVwTD);
+        const uint64_t hmD = (uint64_t)ws_ld(kVwHmD) | ((uint64_t)ws_ld(kVwHmD1) << 32);
+        // first: the tile's first pool chunk (after its sky frames, if any): the accumulator from buf
+        const bool first = f0D == (int)ws_ld(kVwSkyD), last = f0D + nfD == S;
+        if ((hmD >> lane) & 1u) {   // this lane's pixel of D's tile
+            const int tcol = ((int)pt_entry_tile(tD) % tiles_x) * 8, trow = ((int)pt_entry_tile(tD) / tiles_x) * 8;
+            const int px = job.col0 + tcol + (lane & 7), pr = trow + (lane >> 3);
+            const int orow = LAYOUT == PT_LAYOUT_TILED_PLANAR8 ? job.row_start + pr * job.row_stride : pr;
+            float* const acc_p = job.buf + out_index<LAYOUT>(job, px, orow);
+            V3 acc = v3(0.0f, 0.0f, 0.0f);
+            if (first) {
+                if (job.accumulate) acc = v3(acc_p[0], acc_p[cs], acc_p[2 * cs]);   // (:1233: only to blend)
+            } else {
+                acc = v3(s_acc[wv][0][lane], s_acc[wv][1][lane], s_acc[wv][2][lane]);
+            }
+            const float4* sp = (const float4*)(slots + (c * 64 + lane) * (kChunk * 3));   // 96 B, 16-B aligned
+            float4 v[kChunk * 3 / 4];
+#pragma unroll
+            for (int i = 0; i < kChunk * 3 / 4; ++i)
+                if (i * 4 < nfD * 3) v[i] = sp[i];
+            const float* fr = (const float*)v;
+#pragma unroll
+            for (int f = 0; f < kChunk; ++f) {
+                if (f < nfD) {
+                    const V3 cc = v3(fr[3 * f], fr[3 * f + 1], fr[3 * f + 2]);
+                    if (job.accumulate) {   // ACCUMULATE_FRAMES 1: fmadd(blend_factor, color - last, last) :1233-1241
+                        const float bf = rcp((float)(job.frame_first + (uint32_t)(f0D + f)) + 1.0f);   // :1200
+                        acc = v3(fma_(bf, cc.x - acc.x, acc.x), fma_(bf, cc.y - acc.y, acc.y), fma_(bf, cc.z - acc.z, acc.z));
+                    } else {                // ACCUMULATE_FRAMES 0: the frame's colour is stored (:1245-1250)
+                        acc = cc;
+                    }
+                }
+            }
+            if (last) {
+                acc_p[0] = acc.x;
+                acc_p[cs] = acc.y;
+                acc_p[2 * cs] = acc.z;
+            } else {
+                s_acc[wv][0][lane] = acc.x;
+                s_acc[wv][1][lane] = acc.y;
+                s_acc[wv][2][lane] = acc.z;
+            }
+        }
+        if (rec_cost) {   // the schedule's cost: about the tile's pool iterations (its sky frames: one each)
+            const uint32_t tile_seg = ws_ld(kVwTileSeg) + ws_ld(kVwSegD) + (first ? 64u * ws_ld(kVwSkyD) : 0u);
+            ws_st(kVwTileSeg, last ? 0u : tile_seg);
+            if (last && lane == 0) pt_record_cost(job.cost, tD, ntiles, 1u + (tile_seg + 63u) / 64u);
+        }
+        hasD = false;
+    };
+
+    start_chunk();
+    uint32_t idle_events = 0;   // outer iterations in a row without progress (guard)
+    bool fault = false;
+    while (!fault) {
+        bool event = false;
+        if (hasD && dmask == 0) {   // D's last item ended: fold it
+            fold_D();
+            event = true;
+        }
+        if (nitA > 0 && issA >= nitA && !hasD) {   // A has handed out every item and D is folded
+            ws_st(kVwTD, ws_ld(kVwTcur));
+            ws_st(kVwHmD, ws_ld(kVwHm));
+            ws_st(kVwHmD1, ws_ld(kVwHm1));
+            ws_st(kVwF0D, ws_ld(kVwF0A));
+            ws_st(kVwNfD, (uint32_t)nfA);
+            ws_st(kVwSkyD, ws_ld(kVwSky));
+            if (rec_cost) ws_st(kVwSegD, ws_ld(kVwSegA));
+            hasD = true;
+            dmask = pt_ballot(slot >= 0);   // every earlier chunk is folded: the items in flight are A's
+            nitA = 0;
+            issA = 0;
+            cA ^= 1;
+            start_chunk();
+            event = true;
+            if (dmask == 0) continue;   // (D's items had all ended: fold it first)
+        }
+        if (nitA == 0 && !hasD) break;   // every chunk of every tile of the queue is folded
+        idle_events = event ? 0u : idle_events + 1u;
+        if (__builtin_expect(idle_events > 2u, 0)) {   // (guard, never reached)
+            fault = true;
+            break;
+        }
+        while (true) {
+            const bool had = slot >= 0;
+            const uint64_t idle = pt_ballot(!had);
+            bool took = false;
+            int ntaken = 0;
+            if (idle != 0 && issA < nitA) {
+                const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
+                const int k = issA + rank;
+                const bool take = !had && k < nitA;
+                took = take;
+                if (take) {
+                    // frame-major (pt_v4_kernel's order): item k is frame k / nhA of listed pixel k % nhA
+                    const int fi = nhA == 1 ? k : (int)__umulhi((uint32_t)k, div_nh);
+                    const int sl = k - (int)__umul24((uint32_t)fi, (uint32_t)nhA);
+                    const uint32_t pl = s_pl[wv][sl];
+                    const int p = (int)(pl & 63u), X = (int)(pl >> 8);
+                    const int fyi = (int)s_py[wv][sl];
+                    camera(X, fyi, fA + (uint32_t)fi, rng, dir);
+                    pos = v3(0.0f, 0.0f, 1.0f * 40.0f);   // camera.Position :1501
+                    T = v3(1.0f, 1.0f, 1.0f);
+                    ret = v3(0.0f, 0.0f, 0.0f);
+                    bounce = 0;
+                    slot = (int)__umul24((uint32_t)(cA * 64 + p), (uint32_t)(kChunk * 3)) + fi * 3;
+                }
+                const int npop = __popcll(idle);
+                ntaken = npop < nitA - issA ? npop : nitA - issA;
+                issA += ntaken;
+            }
+            if (idle == ~0ull && ntaken == 0) break;   // no item in flight: an event is due
+            idle_events = 0;
+            if (COUNT) n_slots += 64;
+            const bool busy = had || took;
+            bool all_sky = false;   // (as pt_v4_kernel)
+            if (DEF && pt_ballot(busy && bounce != 0) == 0) all_sky = pt_ballot(busy && !sky_ray_v4(dir)) == 0;
+            bool done = false, queued = false;
+            int qslot = 0;
+            if (busy) {
+                v4_segment<ENV, COUNT, DEF, FEXP, DFL>(job, sc, s_mat, s_mx, s_sc, tex, random, rejection, B, all_sky, pos,
+                                                       dir, T, ret, rng, bounce, done, queued, n_seg, n_esc, n_fb, n_sky);
+                if (done) {
+                    qslot = slot;
+                    if (!(DEFER && queued)) {   // mainImage :1127: fmadd(color, 1/c_numRendersPerFrame, 0)
+                        float* const o = slots + slot;
+                        o[0] = fma_(ret.x, 1.0f, 0.0f);
+                        o[1] = fma_(ret.y, 1.0f, 0.0f);
+                        o[2] = fma_(ret.z, 1.0f, 0.0f);
+                    }
+                    slot = -1;
+                }
+            }
+            if (DEFER) {   // (pt_v4_kernel's queue, each entry with its radiance)
+                const uint64_t qm = pt_ballot(queued);
+                const int nq = __popcll(qm);
+                const V3 ed = ENV == PT_V4_ENV_EQUIRECT_ ? v3(-dir.x, dir.y, -dir.z) : dir;
+                if (qn + nq > kEnvQ) {
+                    const int take = std::min(qn, 64 - nq);
+                    const int r = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(~qm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)~qm, 0u));
+                    V3 d = ed, t = T, rs = ret;
+                    uint32_t rr = rng;
+                    int k = qslot;
+                    bool act = queued;
+                    if (!queued && r < take) {
+                        const int e = qn - take + r;
+                        const float4 a = s_qd[DEFER ? wv : 0][DEFER ? e : 0], b = s_qt[DEFER ? wv : 0][DEFER ? e : 0];
+                        const float4 c = s_qr[DEFER ? wv : 0][DEFER ? e : 0];
+                        d = v3(a.x, a.y, a.z);
+                        rr = __builtin_bit_cast(uint32_t, a.w);
+                        t = v3(b.x, b.y, b.z);
+                        k = __builtin_bit_cast(int, b.w);
+                        rs = v3(c.x, c.y, c.z);
+                        act = true;
+                    }
+                    if (act) resolve(d, rr, t, rs, k);
+                    qn -= take;
+                } else {
+                    if (queued) {
+                        const int k = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
+                        s_qd[DEFER ? wv : 0][k] = make_float4(ed.x, ed.y, ed.z, __builtin_bit_cast(float, rng));
+                        s_qt[DEFER ? wv : 0][k] = make_float4(T.x, T.y, T.z, __builtin_bit_cast(float, qslot));
+                        s_qr[DEFER ? wv : 0][k] = make_float4(ret.x, ret.y, ret.z, 0.0f);
+                    }
+                    qn += nq;
+                }
+            }
+            const uint64_t ended = pt_ballot(done);
+            if (rec_cost) {   // segments traced per context (the schedule's cost)
+                const int inD = __popcll(dmask), in_all = __popcll(pt_ballot(busy));
+                if (lane == 0) {
+                    ws[kVwSegA] += (uint32_t)(in_all - inD);
+                    ws[kVwSegD] += (uint32_t)inD;
+                }
+            }
+            dmask &= ~ended;
+            if (hasD && dmask == 0) break;                    // fold due
+            if (nitA > 0 && issA >= nitA && !hasD) break;     // retire due
+        }
+    }
+    if (__builtin_expect(fault, 0) && DEFER && qn > 0) drain(qn);
+    if (COUNT) {
+        for (int off = 32; off > 0; off >>= 1) {
+            n_seg += __shfl_down(n_seg, off);
+            n_esc += __shfl_down(n_esc, off);
+            n_fb += __shfl_down(n_fb, off);
+            n_sky += __shfl_down(n_sky, off);
+        }
+        if (lane == 0) {
+            atomicAdd(&job.counters[0], n_seg);
+            atomicAdd(&job.counters[2], n_esc);
+            atomicAdd(&job.counters[3], n_slots);
+            atomicAdd(&job.counters[4], n_fb);
+            atomicAdd(&job.counters[5], n_sky);
+        }
+    }
+}
+
 template <int ENV, int LAYOUT>
 hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool count)
 {
     const int tiles = ((j.ncols + 7) / 8) * ((j.nrows + 7) / 8);
     const dim3 block(64 * kWaves);
-    auto go = [&](auto kern) {   // persistent grid: the resident blocks, at most one tile per wave
+    // persistent grid: the resident blocks, at most one tile per wave.  The continuous-tiles kernel
+    // for launches of >= 8 frames when the caller provides its slots for the whole grid, else the
+    // per-tile pool kernel.  Measured (scripts/gpu_v4_ab.sh, CT vs per-tile): 1080p 32 spp 1.257 vs
+    // 1.320 ms, 4K 8 spp 1.308 vs 1.328, 1080p 8 spp 0.3602 vs 0.3589 -- but 1 spp 0.133 vs 0.115:
+    // a one-frame chunk is one item per pixel, and its chunk events (claim, fold) dominate.
+    const auto go = [&](auto kern, auto ct_kern) {
+        const long ct_blocks = std::min<long>(pt_resident_blocks(ct_kern, 64 * kWaves), (tiles + kWaves - 1) / kWaves);
+        if (j.ct_slots && j.nframes >= kChunk && (uint64_t)ct_blocks * kWaves <= j.ct_waves) {
+            hipLaunchKernelGGL(ct_kern, dim3((unsigned)ct_blocks), block, 0, st, j, sc);
+            return;
+        }
         const long blocks = std::min<long>(pt_resident_blocks(kern, 64 * kWaves), (tiles + kWaves - 1) / kWaves);
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), block, 0, st, j, sc);
     };
     if (j.default_scene) {
-        if (count) go(pt_v4_kernel<ENV, LAYOUT, true, true, 2>);
-        else if (j.fast_exp && j.random_jitter && j.rejection) go(pt_v4_kernel<ENV, LAYOUT, false, true, 1, true>);
-        else if (j.fast_exp) go(pt_v4_kernel<ENV, LAYOUT, false, true, 1>);
-        else go(pt_v4_kernel<ENV, LAYOUT, false, true, 0>);
+        if (count) go(pt_v4_kernel<ENV, LAYOUT, true, true, 2>, pt_v4_ct_kernel<ENV, LAYOUT, true, true, 2>);
+        else if (j.fast_exp && j.random_jitter && j.rejection)
+            go(pt_v4_kernel<ENV, LAYOUT, false, true, 1, true>, pt_v4_ct_kernel<ENV, LAYOUT, false, true, 1, true>);
+        else if (j.fast_exp) go(pt_v4_kernel<ENV, LAYOUT, false, true, 1>, pt_v4_ct_kernel<ENV, LAYOUT, false, true, 1>);
+        else go(pt_v4_kernel<ENV, LAYOUT, false, true, 0>, pt_v4_ct_kernel<ENV, LAYOUT, false, true, 0>);
     } else {
-        if (count) go(pt_v4_kernel<ENV, LAYOUT, true, false, 2>);
-        else if (j.fast_exp) go(pt_v4_kernel<ENV, LAYOUT, false, false, 1>);
-        else go(pt_v4_kernel<ENV, LAYOUT, false, false, 0>);
+        if (count) go(pt_v4_kernel<ENV, LAYOUT, true, false, 2>, pt_v4_ct_kernel<ENV, LAYOUT, true, false, 2>);
+        else if (j.fast_exp) go(pt_v4_kernel<ENV, LAYOUT, false, false, 1>, pt_v4_ct_kernel<ENV, LAYOUT, false, false, 1>);
+        else go(pt_v4_kernel<ENV, LAYOUT, false, false, 0>, pt_v4_ct_kernel<ENV, LAYOUT, false, false, 0>);
     }
     return hipGetLastError();
 }

@@ -175,3 +175,16 @@ def test_reference_host_with_flag_overrides(tmp_path, defines, kw):
     px = po.tonemap(ref, po.PIXEL_RGBA8, fast_aces=kw.get("fast_aces", True), fast_gamma=kw.get("fast_gamma", True))
     rows = np.frombuffer(bmp.read_bytes()[54:], np.uint8).reshape(h, w, 3)[::-1, :, ::-1]   # bottom-up, BGR
     assert np.array_equal(rows, px.view(np.uint8).reshape(h, w, 4)[..., :3])
+
+
+@pytest.mark.parametrize("fast_exp", [True, False])
+@pytest.mark.parametrize("accumulate", [True, False])
+def test_v4_ct_accumulate_and_exp(accumulate, fast_exp):
+    """As above through the continuous-tiles v4 kernel (launches of >= 8 frames): 9 frames from 7."""
+    w, h, frames = 136, 88, 9
+    env = _tex(64, 128, seed=3)
+    start = np.random.default_rng(8).random((h, w, 3), dtype=np.float32)
+    got = _device_v4(w, h, frames, env, frame_first=7, start=start, accumulate_frames=accumulate, fast_exp=fast_exp)
+    ref = po.render4(w, h, frame_first=7, nframes=frames, env=env, buf=start.copy(), accumulate=accumulate,
+                     fast_exp=fast_exp)
+    assert bits_equal(got, ref), mismatch_report(got, ref)

@@ -322,3 +322,52 @@ def test_v4_scheduled_launches_match_oracle(env_mode):
     got = buf.cpu().numpy().reshape(h, w, 3)
     ref = _oracle(w, h, k, env=env, env_mode=po.ENV_CUBEMAP if cube else po.ENV_EQUIRECT)
     assert bits_equal(got, ref), mismatch_report(got, ref)
+
+
+# pt_v4_ct_kernel (launches of >= 8 frames, pt_v4.hip): partial tiles, several chunks and a partial
+# one, the sky-frame prefix (default scene), every env mode and sampling flag, fast / exact exp
+@pytest.mark.parametrize("w,h,frames,env_mode,rj,rej", [
+    (97, 61, 8, N.PT_V4_ENV_EQUIRECT, True, True),     # partial tiles, one chunk
+    (130, 70, 17, N.PT_V4_ENV_EQUIRECT, True, True),   # 3 chunks, the last of 1 frame
+    (64, 48, 9, N.PT_V4_ENV_NONE, True, True),         # ambient miss term
+    (100, 60, 8, N.PT_V4_ENV_EQUIRECT, False, False),  # bilinear texels, angle-sampled directions
+    (96, 64, 12, N.PT_V4_ENV_CUBEMAP, True, True),
+    (96, 64, 8, N.PT_V4_ENV_CUBEMAP, False, True),
+])
+def test_v4_ct_pool(w, h, frames, env_mode, rj, rej):
+    cube = env_mode == N.PT_V4_ENV_CUBEMAP
+    env = None if env_mode == N.PT_V4_ENV_NONE else (_tex(6 * 16, 16, seed=41) if cube else _tex(64, 128, seed=41))
+    got = _device_v4(w, h, frames, env=env, env_mode=env_mode, random_jitter=rj, rejection=rej)
+    ref = _oracle(w, h, frames, env=env, env_mode=po.ENV_CUBEMAP if cube else po.ENV_EQUIRECT, random_jitter=rj,
+                  rejection=rej)
+    assert bits_equal(got, ref), mismatch_report(got, ref)
+
+
+def test_v4_ct_pool_custom_scene_and_shards():
+    """The continuous-tiles v4 kernel on an Add*ToScene scene (no sky prefix, scene tables) and on
+    row shards (row_start / row_stride), against the oracle."""
+    s, quads, spheres, mats = _random_scene(4)
+    from cpuperformanceraytracer_amd.device import ensure_backend
+    ensure_backend(0)
+    pt.ClearScene()
+    for m in mats:
+        pt.AddMaterialToScene(m["albedo"], m["emissive"], m["spec_chance"], m["spec_rough"], m["spec_color"],
+                              m["ior"], m["refr_chance"], m["refr_rough"], m["refr_color"])
+    for q in quads:
+        pt.AddQuadObjectToScene(q)
+    for q in spheres:
+        pt.AddSphereObjectToScene(q)
+    try:
+        env = _tex(32, 64, seed=43)
+        got = _device_v4(112, 72, 10, env=env)
+        ref = po.render4(112, 72, nframes=10, env=env, scene=s)
+        assert bits_equal(got, ref), mismatch_report(got, ref)
+    finally:
+        pt.InitializeScene()
+    env = _tex(64, 128, seed=47)
+    w, h = 120, 90
+    full = _oracle(w, h, 8, env=env)
+    for start, stride in ((1, 4), (3, 7)):
+        nrows = (h - start + stride - 1) // stride
+        got = _device_v4(w, h, 8, env=env, row_start=start, row_stride=stride, nrows=nrows)
+        assert bits_equal(got, full[start::stride]), mismatch_report(got, full[start::stride])
