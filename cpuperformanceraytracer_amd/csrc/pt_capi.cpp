@@ -146,6 +146,7 @@ struct State {
     // test hook: PT_MI355_RING_GUARD_CAP (read by pt_init) caps the pools' iteration guards so
     // that it fires -- the error path's own GPU test (tests/test_gpu_state.py)
     uint32_t ring_guard_cap = ~0u;
+    int32_t v4_ct_force = 0;   // PT_MI355_V4_CT=1 (read by pt_init): PtV4Job::ct_force (tests)
     uint32_t split = 2;   // PT_MI355_SPLIT (read by pt_init): tile split factor of the schedule (0: none)
     bool no_ct = false;   // PT_MI355_NO_CT=1 (read by pt_init): one-chunk launches on render_body (A/B)
 };
@@ -1110,6 +1111,7 @@ int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count)
     j.cost = ls.cost;
     // (the v4 pool's slots per wave: pt_v4_ct_wave_floats() <= pt_ct_wave_floats(), pt_v4.hip)
     if ((rc = use_ct_slots(dv, ls, st, &j.ct_slots, &j.ct_waves))) return rc;
+    j.ct_force = g.v4_ct_force;
     hipError_t e = pt_launch_v4(j, g.v4scene, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "v4 render launch failed: %s", hipGetErrorString(e));
     return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_v4's early return)
@@ -1295,6 +1297,7 @@ int pt_init(const pt_config* cfg)
     g.frame = 0;
     g.ring_guard_cap = ~0u;
     g.no_ct = getenv("PT_MI355_NO_CT") && !strcmp(getenv("PT_MI355_NO_CT"), "1");
+    g.v4_ct_force = getenv("PT_MI355_V4_CT") && !strcmp(getenv("PT_MI355_V4_CT"), "1");
     g.split = 2;
     if (const char* sp = getenv("PT_MI355_SPLIT")) g.split = (uint32_t)strtoul(sp, nullptr, 10);
     if (const char* cap = getenv("PT_MI355_RING_GUARD_CAP")) {

@@ -66,6 +66,7 @@ struct PtV4Job {
     // waves (the diffuse kernels' slot area, pt_kernel.h); nullptr: the per-tile pool kernel
     float* ct_slots;
     uint32_t ct_waves;
+    int32_t ct_force;               // 1: the continuous-tiles kernel for every launch of >= 8 frames (tests)
 };
 
 // Scene description in AddQuad/Sphere/MaterialToScene order (v4 :1368-1401).

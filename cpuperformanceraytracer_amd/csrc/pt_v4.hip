@@ -1417,13 +1417,16 @@ hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool 
     const int tiles = ((j.ncols + 7) / 8) * ((j.nrows + 7) / 8);
     const dim3 block(64 * kWaves);
     // persistent grid: the resident blocks, at most one tile per wave.  The continuous-tiles kernel
-    // for launches of >= 8 frames when the caller provides its slots for the whole grid, else the
-    // per-tile pool kernel.  Measured (scripts/gpu_v4_ab.sh, CT vs per-tile): 1080p 32 spp 1.257 vs
-    // 1.320 ms, 4K 8 spp 1.308 vs 1.328, 1080p 8 spp 0.3602 vs 0.3589 -- but 1 spp 0.133 vs 0.115:
-    // a one-frame chunk is one item per pixel, and its chunk events (claim, fold) dominate.
+    // when the caller provides its slots for the whole grid and the launch holds >= 12 full chunks
+    // (8 frames x tile) per wave, else the per-tile pool kernel.  Measured (scripts/gpu_v4_ab.sh, CT
+    // vs per-tile): 1080p 32 spp 1.257 vs 1.320 ms (51 chunks per wave), 4K 8 spp 1.308 vs 1.328 (25),
+    // 1080p 8 spp 0.3602 vs 0.3589 (6), 1 spp 0.133 vs 0.115 (one item per pixel and chunk: the
+    // chunk events, claim and fold, dominate).
     const auto go = [&](auto kern, auto ct_kern) {
         const long ct_blocks = std::min<long>(pt_resident_blocks(ct_kern, 64 * kWaves), (tiles + kWaves - 1) / kWaves);
-        if (j.ct_slots && j.nframes >= kChunk && (uint64_t)ct_blocks * kWaves <= j.ct_waves) {
+        const uint64_t ct_waves = (uint64_t)ct_blocks * kWaves;
+        if (j.ct_slots && ct_waves <= j.ct_waves && j.nframes >= kChunk &&
+            (j.ct_force || (uint64_t)j.nframes * (uint64_t)tiles >= 12ull * kChunk * ct_waves)) {
             hipLaunchKernelGGL(ct_kern, dim3((unsigned)ct_blocks), block, 0, st, j, sc);
             return;
         }

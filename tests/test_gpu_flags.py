@@ -179,8 +179,11 @@ def test_reference_host_with_flag_overrides(tmp_path, defines, kw):
 
 @pytest.mark.parametrize("fast_exp", [True, False])
 @pytest.mark.parametrize("accumulate", [True, False])
-def test_v4_ct_accumulate_and_exp(accumulate, fast_exp):
-    """As above through the continuous-tiles v4 kernel (launches of >= 8 frames): 9 frames from 7."""
+def test_v4_ct_accumulate_and_exp(monkeypatch, accumulate, fast_exp):
+    """As above through the continuous-tiles v4 kernel (PT_MI355_V4_CT=1: every launch of >= 8
+    frames): 9 frames from 7."""
+    monkeypatch.setenv("PT_MI355_V4_CT", "1")
+    pt.init()
     w, h, frames = 136, 88, 9
     env = _tex(64, 128, seed=3)
     start = np.random.default_rng(8).random((h, w, 3), dtype=np.float32)

@@ -324,8 +324,18 @@ def test_v4_scheduled_launches_match_oracle(env_mode):
     assert bits_equal(got, ref), mismatch_report(got, ref)
 
 
-# pt_v4_ct_kernel (launches of >= 8 frames, pt_v4.hip): partial tiles, several chunks and a partial
-# one, the sky-frame prefix (default scene), every env mode and sampling flag, fast / exact exp
+# pt_v4_ct_kernel (pt_v4.hip; large launches: >= 12 chunks per wave; PT_MI355_V4_CT=1 forces it for
+# every launch of >= 8 frames): partial tiles, several chunks and a partial one, the sky-frame
+# prefix (default scene), every env mode and sampling flag
+@pytest.fixture
+def force_v4_ct(monkeypatch):
+    monkeypatch.setenv("PT_MI355_V4_CT", "1")
+    pt.init()   # (pt_init reads it)
+    yield
+    monkeypatch.delenv("PT_MI355_V4_CT")
+    pt.init()
+
+
 @pytest.mark.parametrize("w,h,frames,env_mode,rj,rej", [
     (97, 61, 8, N.PT_V4_ENV_EQUIRECT, True, True),     # partial tiles, one chunk
     (130, 70, 17, N.PT_V4_ENV_EQUIRECT, True, True),   # 3 chunks, the last of 1 frame
@@ -334,7 +344,7 @@ def test_v4_scheduled_launches_match_oracle(env_mode):
     (96, 64, 12, N.PT_V4_ENV_CUBEMAP, True, True),
     (96, 64, 8, N.PT_V4_ENV_CUBEMAP, False, True),
 ])
-def test_v4_ct_pool(w, h, frames, env_mode, rj, rej):
+def test_v4_ct_pool(force_v4_ct, w, h, frames, env_mode, rj, rej):
     cube = env_mode == N.PT_V4_ENV_CUBEMAP
     env = None if env_mode == N.PT_V4_ENV_NONE else (_tex(6 * 16, 16, seed=41) if cube else _tex(64, 128, seed=41))
     got = _device_v4(w, h, frames, env=env, env_mode=env_mode, random_jitter=rj, rejection=rej)
@@ -343,7 +353,7 @@ def test_v4_ct_pool(w, h, frames, env_mode, rj, rej):
     assert bits_equal(got, ref), mismatch_report(got, ref)
 
 
-def test_v4_ct_pool_custom_scene_and_shards():
+def test_v4_ct_pool_custom_scene_and_shards(force_v4_ct):
     """The continuous-tiles v4 kernel on an Add*ToScene scene (no sky prefix, scene tables) and on
     row shards (row_start / row_stride), against the oracle."""
     s, quads, spheres, mats = _random_scene(4)
