@@ -471,7 +471,12 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
         flops_launch_ref = flops_launch
         flop_model = (f"segments x V4_F_SEGMENT + samples x V4_F_SAMPLE; F = {RL.V4_F_SEGMENT}/{RL.V4_F_SAMPLE} "
                       "(roofline.py, counted by oracle/pt_oracle_v4.c)")
-        kernel_name = "pt_v4_kernel<EQUIRECT, INTERLEAVED>"
+        # pt_v4.hip launch_t: the continuous-tiles kernel for launches of >= 12 8-frame chunks per
+        # resident wave (5120 on MI355X), the per-tile pool kernel else (this label mirrors that rule)
+        tiles = ((Wg + 7) // 8) * (((Hg + world - 1) // world + 7) // 8)
+        v4_ct = os.environ.get("PT_MI355_NO_CT") != "1" and S >= 8 and (
+            os.environ.get("PT_MI355_V4_CT") == "1" or S * tiles >= 12 * 8 * 5120)
+        kernel_name = "pt_v4_ct_kernel<EQUIRECT, INTERLEAVED>" if v4_ct else "pt_v4_kernel<EQUIRECT, INTERLEAVED>"
     else:
         env_esc = escaped if wl.env else 0
         flops_launch = RL.launch_flops_alg(segs, samples, env_esc) / K * per_rank
@@ -480,7 +485,10 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
                       + (" + escaped paths x F_ENV_ESCAPE" if wl.env else "") +
                       f"; F = {RL.F_SEGMENT}/{RL.F_SAMPLE}" + (f"/{RL.F_ENV_ESCAPE}" if wl.env else "") +
                       " (roofline.py; a pixel's camera ray is one segment)")
-        kernel_name = "pt_render_env_kernel<INTERLEAVED>" if wl.env else "pt_render_kernel<INTERLEAVED>"
+        # the continuous-tiles kernels (pt_kernel.hip render_body_ct) unless PT_MI355_NO_CT=1
+        ct = os.environ.get("PT_MI355_NO_CT") != "1"
+        kernel_name = (("pt_render_ct_env_kernel" if ct else "pt_render_env_kernel") if wl.env else
+                       ("pt_render_ct_kernel" if ct else "pt_render_kernel")) + "<INTERLEAVED>"
     achieved_tf = flops_launch / avg_kernel_s / 1e12
     pmc = load_pmc(wl.name) if roofline else {}
     # config 4: one 12-byte texel gather per escaping path

@@ -30,7 +30,13 @@ ENV = workload.startswith("c4")
 # Family prefix of the timed (COUNT = false) instance; the remaining template arguments (MULTI for
 # launches that chain chunks, v4's exp switch) are resolved below to the instance with the most
 # kernel-trace time.
-KERNEL = "pt_render_env_kernel<0, false," if ENV else "pt_render_kernel<0, false,"
+# (round 4: the continuous-tiles kernels, pt_kernel.hip render_body_ct; PT_MI355_NO_CT=1 profiles of the
+# per-tile pool: PT_PROFILE_PER_TILE=1)
+import os
+if os.environ.get("PT_PROFILE_PER_TILE") == "1":
+    KERNEL = "pt_render_env_kernel<0, false," if ENV else "pt_render_kernel<0, false,"
+else:
+    KERNEL = "pt_render_ct_env_kernel<0, false" if ENV else "pt_render_ct_kernel<0, false"
 if workload.startswith("v4"):
     KERNEL = "pt_v4_kernel<1, 0, false, true,"   # <EQUIRECT, INTERLEAVED, COUNT = false, default-scene literals, FEXP>
 SUMMARY = "pmc_summary.json" if workload == "c2_1080p" else f"pmc_summary_{workload}.json"
