@@ -69,7 +69,7 @@ rows = [
     ("algorithmic FLOP/s (frac of 157.3 TF)",
      [f"{B[k]['roofline']['achieved']:.1f} TF/s ({100 * B[k]['roofline']['frac']:.1f} %)" for k in ("c2", "c3", "c4", "c5")]),
     ("reference-equivalent FLOP/s", [f"{B[k]['roofline']['achieved_ref_equivalent']:.1f} TF/s" for k in ("c2", "c3", "c4", "c5")]),
-    ("HBM bytes per launch (rocprofv3 FETCH+WRITE) vs algorithmic",
+    ("fabric bytes per launch (rocprofv3 FETCH+WRITE: L2 misses and write-backs, Infinity-Cache hits included; with the continuous-tiles slot area, §3c) vs algorithmic",
      [f"{hbm(k):.1f} MB vs {B[k]['roofline']['algorithmic_bytes_per_launch'] / 1e6:.1f} MB" if hbm(k) else "—" for k in ("c2", "c3", "c4", "c5")]),
     ("VALU wave-instructions per launch (PMC)",
      [f"{e(M[k]['SQ_INSTS_VALU'])}" + (f" = {M[k]['SQ_INSTS_VALU'] / (M[k]['avg_ns'] * 1024):.2f} per SIMD per ns" if k == "c2" else "")
@@ -79,7 +79,7 @@ cpu = B["c2"].get("cpu_baseline") or {}
 if cpu:
     rows.append((f"CPU baseline: oracle port, {cpu.get('cores')} threads (the box's cgroup CPU quota), ~{cpu.get('sample', '').split(';')[-1].strip()}",
                  [f"{e(cpu['value'])} ray-samples/s (GPU ×{B['c2']['value'] / cpu['value']:.0f})", "", "", ""]))
-hdr = (f"| quantity (one launch; round 3, bench `profiles/{tag}_bench_*.json`, rocprofv3 `profiles/{tag}_*`) | c2: 1920×1080, 8 spp, 8 b | "
+hdr = (f"| quantity (one launch; round 4, bench `profiles/{tag}_bench_*.json`, rocprofv3 `profiles/{tag}_*`) | c2: 1920×1080, 8 spp, 8 b | "
        "c3: 3840×2160, 64 spp | c4: 1080p, 16 spp, env | c5: 7680×4320, 256 spp (one GPU, whole image) |\n|---|---|---|---|---|\n")
 design = hdr + "".join(f"| {r} | " + " | ".join(v) + " |\n" for r, v in rows)
 v = B["v4"]
