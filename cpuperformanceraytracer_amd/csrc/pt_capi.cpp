@@ -147,6 +147,7 @@ struct State {
     // that it fires -- the error path's own GPU test (tests/test_gpu_state.py)
     uint32_t ring_guard_cap = ~0u;
     int32_t v4_ct_force = 0;   // PT_MI355_V4_CT=1 (read by pt_init): PtV4Job::ct_force (tests)
+    uint32_t ct_back_pct = 20;   // PT_MI355_BACK (read by pt_init): PtJob::ct_back_pct (0: none)
     uint32_t split = 2;   // PT_MI355_SPLIT (read by pt_init): tile split factor of the schedule (0: none)
     bool no_ct = false;   // PT_MI355_NO_CT=1 (read by pt_init): one-chunk launches on render_body (A/B)
 };
@@ -443,6 +444,7 @@ PtJob base_job(float* buf, int32_t w, int32_t h)
     j.guard_cap = g.ring_guard_cap;
     j.ct_slots = nullptr;
     j.ct_waves = 0;
+    j.ct_back_pct = 0;   // (launch(): launches of <= 16 frames)
     j.scene = nullptr;
     return j;
 }
@@ -651,6 +653,11 @@ int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
     j.cost = ls.cost;
     j.err = dv.derr;
     if ((rc = use_ct_slots(dv, ls, st, &j.ct_slots, &j.ct_waves))) return rc;
+    // the last-dispatched fifth of the grid (each CU's 5th block, the slowest under the SQ's
+    // oldest-first issue) claims the cheapest units, for launches of <= 16 frames, whose end is a
+    // large part of them (A/B, scripts/gpu_ab.sh, 20 % vs none: 1080p 8 spp 0.2533 vs 0.2561 ms,
+    // env 16 spp 0.4967 vs 0.5030, 4K 8 spp 0.8217 vs 0.8309; 4K 64 spp 5.913 vs 5.763: not there)
+    j.ct_back_pct = j.nframes <= 16 ? g.ct_back_pct : 0u;
     hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
     return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_render's early return)
@@ -1298,6 +1305,8 @@ int pt_init(const pt_config* cfg)
     g.ring_guard_cap = ~0u;
     g.no_ct = getenv("PT_MI355_NO_CT") && !strcmp(getenv("PT_MI355_NO_CT"), "1");
     g.v4_ct_force = getenv("PT_MI355_V4_CT") && !strcmp(getenv("PT_MI355_V4_CT"), "1");
+    g.ct_back_pct = 20;
+    if (const char* bk = getenv("PT_MI355_BACK")) g.ct_back_pct = (uint32_t)strtoul(bk, nullptr, 10);
     g.split = 2;
     if (const char* sp = getenv("PT_MI355_SPLIT")) g.split = (uint32_t)strtoul(sp, nullptr, 10);
     if (const char* cap = getenv("PT_MI355_RING_GUARD_CAP")) {

@@ -50,6 +50,8 @@ struct PtJob {
     uint32_t guard_cap;            // upper limit of the ring pool's iteration guard: ~0u (tests lower it)
     float* ct_slots;               // continuous-tiles pool (pt_kernel.hip render_body_ct): pt_ct_wave_floats()
     uint32_t ct_waves;             // f32 per wave for ct_waves waves; nullptr: one-chunk launches use render_body
+    uint32_t ct_back_pct;          // the continuous-tiles pool: the last-dispatched ct_back_pct % of the grid
+                                   // claims its units from the back of its queue group (pt_tile_queue.h)
     // mainImage's frame constants (scalar.cpp:338-347), set by pt_launch_render on the host with the
     // same correctly rounded f32 operations: W, H, 1/W, 1/H, W/H, 1/(W/H).  Kernel arguments are
     // scalar registers; computed in the kernel they were VGPRs that the tile loop spilled.

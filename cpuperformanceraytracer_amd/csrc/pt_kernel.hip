@@ -701,7 +701,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 
     // the next launch's queue counters start at zero: this launch clears them (pt_capi.cpp use_sched;
     // it saves the stream a 1-KiB fill before every launch)
-    if (job.queue_next && blockIdx.x == 0 && threadIdx.x < PT_NQUEUES) job.queue_next[threadIdx.x * 32u] = 0u;
+    pt_queue_zero_next(job.queue_next);   // (pt_tile_queue.h)
     // tiles from the launch's queue (pt_tile_queue.h)
     constexpr uint32_t kNone = PtTileQueue<kWavesPerBlock>::kNone;
     PtTileQueue<kWavesPerBlock> tq(job.queue, job.order, job.units, job.nunits, total_tiles, wv);
@@ -1291,9 +1291,14 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
         job.counters ? job.counters + 32 + 4 * 65536 + 96 * (size_t)(blockIdx.x * kWavesPerBlock + wv) : nullptr;
 #endif
 
-    if (job.queue_next && blockIdx.x == 0 && threadIdx.x < PT_NQUEUES) job.queue_next[threadIdx.x * 32u] = 0u;
+    pt_queue_zero_next(job.queue_next);   // (pt_tile_queue.h)
     constexpr uint32_t kNone = PtTileQueue<kWavesPerBlock>::kNone;
-    PtTileQueue<kWavesPerBlock>(job.queue, job.order, job.units, job.nunits, total_tiles, wv).save(s_tq[wv], lane);
+    {
+        PtTileQueue<kWavesPerBlock> q(job.queue, job.order, job.units, job.nunits, total_tiles, wv);
+        q.back = (uint64_t)blockIdx.x * 100u >= (uint64_t)gridDim.x * (100u - (job.ct_back_pct < 100u ? job.ct_back_pct : 100u)) &&
+                 job.ct_back_pct != 0;
+        q.save(s_tq[wv], lane);
+    }
 
     // Wave-uniform state.  What only the events (chunk start, retire, fold) use lives in LDS (s_ws),
     // not in scalar registers: the pool loop then keeps its constants in SGPRs instead of

@@ -57,16 +57,29 @@ __device__ __forceinline__ void pt_record_cost(uint32_t* cost, uint32_t e, uint3
     if (part == 0u) cost[ntiles + tile] = 0u;
 }
 
+// The next launch's queue counters, zeroed by the launch's block 0 (pt_capi.cpp use_sched)
+__device__ __forceinline__ void pt_queue_zero_next(unsigned int* queue_next)
+{
+    if (queue_next && blockIdx.x == 0 && threadIdx.x < PT_NQUEUES)
+        *reinterpret_cast<unsigned long long*>(queue_next + threadIdx.x * 32u) = 0ull;
+}
+
+// A group's counter is 64 bits: dynamic units taken from the front (low word: longest first) and
+// from the back (high word: the cheapest units).  A wave set to `back` (the continuous-tiles
+// kernels' last-dispatched blocks, which the SQ's oldest-first issue leaves the slowest) takes its
+// group's cheapest units, so the launch's last expensive units go to fast waves; a claim is valid
+// while front + back stays below the group's dynamic unit count.
 template <int WAVES_PER_BLOCK>
 struct PtTileQueue {
     static constexpr uint32_t kNone = 0xffffffffu;
-    unsigned int* base;       // PT_NQUEUES counters, 128 B apart (zeroed before the launch)
+    unsigned int* base;       // PT_NQUEUES 64-bit counters, 128 B apart (zeroed before the launch)
     const uint32_t* order;    // schedule position -> tile, or nullptr (raster order)
     const uint32_t* units;    // unit -> first schedule position (units[u + 1] its end), or nullptr
                               // (order: entries -- tile | part << PT_TILE_PART_SHIFT)
     uint32_t nunits, ntiles, ngroups, qg, wave;
     uint32_t dead = 0;        // groups known to be exhausted
     uint32_t c_pos = kNone, c_end = kNone;   // the current unit's remaining schedule positions
+    uint32_t back = 0;        // 1: claim from the back of the own group
 
     __device__ PtTileQueue(unsigned int* queue, const uint32_t* order_, const uint32_t* units_,
                            const uint32_t* nunits_, uint32_t total_tiles, int wv)
@@ -81,7 +94,7 @@ struct PtTileQueue {
     // The queue's state as kWords words (a wave's LDS copy: a kernel whose pool loop must not hold
     // the queue in scalar registers keeps it there between dequeues -- render_body_ct).  save: lane 0
     // stores; restore: uniform loads.
-    static constexpr int kWords = 14;
+    static constexpr int kWords = 15;
     __device__ PtTileQueue() = default;
     __device__ void save(uint32_t* w, int lane) const
     {
@@ -99,6 +112,7 @@ struct PtTileQueue {
         w[11] = dead;
         w[12] = c_pos;
         w[13] = c_end;
+        w[14] = back;
     }
     __device__ static PtTileQueue restore(const uint32_t* w)
     {
@@ -116,6 +130,7 @@ struct PtTileQueue {
         q.dead = u(11);
         q.c_pos = u(12);
         q.c_end = u(13);
+        q.back = u(14);
         return q;
     }
     __device__ uint32_t group_waves(uint32_t g) const
@@ -127,6 +142,18 @@ struct PtTileQueue {
         const uint32_t slot = g + ngroups * (group_waves(g) + c);
         return slot < nunits ? slot : kNone;
     }
+    __device__ uint32_t dyn_units(uint32_t g) const   // dynamic positions of group g
+    {
+        const uint32_t all = g < nunits ? (nunits - g + ngroups - 1) / ngroups : 0u, w = group_waves(g);
+        return all > w ? all - w : 0u;
+    }
+    // the slot of a claim whose counter read `old` (front or back), kNone past the group's units
+    __device__ uint32_t claimed(uint32_t g, unsigned long long old, bool from_back) const
+    {
+        const uint32_t f = (uint32_t)old, b = (uint32_t)(old >> 32), n = dyn_units(g);
+        if ((unsigned long long)f + b >= n) return kNone;
+        return slot_of(g, from_back ? n - 1u - b : f);
+    }
     __device__ uint32_t unit_lo(uint32_t u) const { return units ? __builtin_amdgcn_readfirstlane(units[u]) : u; }
     __device__ uint32_t unit_hi(uint32_t u) const { return units ? __builtin_amdgcn_readfirstlane(units[u + 1]) : u + 1; }
     // (defensive: a schedule entry outside the launch's tiles ends the wave instead of faulting)
@@ -136,29 +163,36 @@ struct PtTileQueue {
         return pt_entry_tile(e) < ntiles && pt_entry_part(e) < 3u ? e : kNone;
     }
 
+    __device__ unsigned long long* counter(uint32_t g) const
+    {
+        return reinterpret_cast<unsigned long long*>(base + g * 32u);
+    }
     // one returning atomic for the wave (its first active lane), the result broadcast
-    __device__ static uint32_t wave_atomic_add(unsigned int* c)
+    __device__ static unsigned long long wave_atomic_add(unsigned long long* c, unsigned long long inc)
     {
         const uint32_t me = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-        uint32_t r = 0;
-        if (me == (uint32_t)__builtin_amdgcn_readfirstlane(me)) r = atomicAdd(c, 1u);
-        return __builtin_amdgcn_readfirstlane(r);
+        unsigned long long r = 0;
+        if (me == (uint32_t)__builtin_amdgcn_readfirstlane(me)) r = atomicAdd(c, inc);
+        return ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(r >> 32)) << 32) |
+               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)r);
     }
-    __device__ static uint32_t wave_load(const unsigned int* c)
+    __device__ static unsigned long long wave_load(const unsigned long long* c)
     {
-        return __builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        const unsigned long long v = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
     }
     __device__ uint32_t steal()
     {
         for (uint32_t k = 1; k < ngroups; ++k) {
             const uint32_t g = (qg + 1 + (wave + k - 1) % (ngroups - 1)) % ngroups;
             if ((dead >> g) & 1u) continue;
-            unsigned int* const c = base + g * 32u;
-            if (slot_of(g, wave_load(c)) == kNone) {
+            unsigned long long* const c = counter(g);
+            if (claimed(g, wave_load(c), false) == kNone) {
                 dead |= 1u << g;
                 continue;
             }
-            const uint32_t slot = slot_of(g, wave_atomic_add(c));
+            const uint32_t slot = claimed(g, wave_atomic_add(c, 1ull), false);
             if (slot != kNone) return slot;
             dead |= 1u << g;
         }
@@ -178,7 +212,8 @@ struct PtTileQueue {
     __device__ uint32_t next()
     {
         if (c_pos >= c_end) {
-            uint32_t u = ((dead >> qg) & 1u) ? kNone : slot_of(qg, wave_atomic_add(base + qg * 32u));
+            uint32_t u = ((dead >> qg) & 1u) ? kNone
+                                             : claimed(qg, wave_atomic_add(counter(qg), back ? 1ull << 32 : 1ull), back != 0);
             if (u == kNone) {
                 dead |= 1u << qg;
                 u = steal();

@@ -773,7 +773,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     __syncthreads();
 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (job.queue_next && blockIdx.x == 0 && threadIdx.x < PT_NQUEUES) job.queue_next[threadIdx.x * 32u] = 0u;   // (as pt_kernel.hip)
+    pt_queue_zero_next(job.queue_next);   // (pt_tile_queue.h)
     const int tiles_x = (job.ncols + 7) >> 3;
     const int ntiles = tiles_x * ((job.nrows + 7) >> 3);
     float* const col = s_col[wv];
@@ -1039,7 +1039,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_ct_kernel(PtV4Job
 
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (job.queue_next && blockIdx.x == 0 && threadIdx.x < PT_NQUEUES) job.queue_next[threadIdx.x * 32u] = 0u;   // (as pt_kernel.hip)
+    pt_queue_zero_next(job.queue_next);   // (pt_tile_queue.h)
     const int tiles_x = (job.ncols + 7) >> 3;
     const uint32_t ntiles = (uint32_t)tiles_x * (uint32_t)((job.nrows + 7) >> 3);
     const int S = job.nframes;

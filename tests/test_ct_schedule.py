@@ -165,3 +165,30 @@ def test_ct_pool_keeps_lanes_busy():
     # path lengths are uniform in 1..9: mean 5 iterations per item
     util = sum(1 for _ in ended) * 5.0 / (64 * iters)
     assert util > 0.9, util
+
+
+def _claimed(n, old, from_back):
+    """pt_tile_queue.h PtTileQueue::claimed: the dynamic position of a claim whose 64-bit counter
+    read `old` (low word: front claims, high word: back claims), None past the group's n units."""
+    f, b = old & 0xFFFFFFFF, old >> 32
+    if f + b >= n:
+        return None
+    return n - 1 - b if from_back else f
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 7, 64])
+def test_front_back_claims_partition_the_group(n):
+    """Waves claiming a group's units from the front (atomicAdd 1) and from the back (atomicAdd
+    2^32) in any interleaving take every unit exactly once, and a claim past the meeting point gets
+    none (pt_tile_queue.h: the last-dispatched blocks take the cheapest units)."""
+    rng = random.Random(n)
+    for trial in range(50):
+        counter, taken = 0, []
+        for _ in range(n + 10):
+            back = rng.random() < 0.3
+            old = counter
+            counter += (1 << 32) if back else 1
+            pos = _claimed(n, old, back)
+            if pos is not None:
+                taken.append(pos)
+        assert sorted(taken) == list(range(n))
