@@ -148,7 +148,7 @@ struct State {
     uint32_t ring_guard_cap = ~0u;
     int32_t v4_ct_force = 0;   // PT_MI355_V4_CT=1 (read by pt_init): PtV4Job::ct_force (tests)
     uint32_t ct_back_pct = 20;   // PT_MI355_BACK (read by pt_init): PtJob::ct_back_pct (0: none)
-    uint32_t split = 2;   // PT_MI355_SPLIT (read by pt_init): tile split factor of the schedule (0: none)
+    uint32_t split = 1;   // PT_MI355_SPLIT (read by pt_init): tile split factor of the schedule (0: none)
     bool no_ct = false;   // PT_MI355_NO_CT=1 (read by pt_init): one-chunk launches on render_body (A/B)
 };
 
@@ -1307,7 +1307,7 @@ int pt_init(const pt_config* cfg)
     g.v4_ct_force = getenv("PT_MI355_V4_CT") && !strcmp(getenv("PT_MI355_V4_CT"), "1");
     g.ct_back_pct = 20;
     if (const char* bk = getenv("PT_MI355_BACK")) g.ct_back_pct = (uint32_t)strtoul(bk, nullptr, 10);
-    g.split = 2;
+    g.split = 1;
     if (const char* sp = getenv("PT_MI355_SPLIT")) g.split = (uint32_t)strtoul(sp, nullptr, 10);
     if (const char* cap = getenv("PT_MI355_RING_GUARD_CAP")) {
         const unsigned long v = strtoul(cap, nullptr, 10);

@@ -24,10 +24,8 @@
 // tripled the launch time).  Victims are visited in a per-wave rotation.
 //
 // A queue entry is a tile or one half of it: the schedule splits the few tiles that cost more than
-// half a wave's share of the launch (tiles whose paths all bounce to the last bounce: 64 pixels x S
-// frames x (B + 1) segments), so that a launch of about one such tile per wave -- 1080p at 8 spp is
-// 72 pool iterations per heavy tile against a mean of 69 per wave -- does not end on the waves that
-// drew two.  Part 1 is the tile's rows 0-3 (lanes 0-31), part 2 its rows 4-7 (lanes 32-63); the
+// a wave's share of the launch (pt_capi.cpp: split factor 1, PT_MI355_SPLIT), so that a launch of
+// about one such tile per wave does not end on the waves that drew two.  Part 1 is the tile's rows 0-3 (lanes 0-31), part 2 its rows 4-7 (lanes 32-63); the
 // other half's pixels are treated as outside the image.
 //
 // The whole wave runs the queue code (uniform control flow): every value is wave-uniform and lives
