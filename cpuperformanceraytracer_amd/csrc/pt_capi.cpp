@@ -1119,6 +1119,7 @@ int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count)
     // (the v4 pool's slots per wave: pt_v4_ct_wave_floats() <= pt_ct_wave_floats(), pt_v4.hip)
     if ((rc = use_ct_slots(dv, ls, st, &j.ct_slots, &j.ct_waves))) return rc;
     j.ct_force = g.v4_ct_force;
+    j.ct_back_pct = j.nframes <= 16 ? g.ct_back_pct : 0u;   // (as launch())
     hipError_t e = pt_launch_v4(j, g.v4scene, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "v4 render launch failed: %s", hipGetErrorString(e));
     return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_v4's early return)

@@ -67,6 +67,8 @@ struct PtV4Job {
     float* ct_slots;
     uint32_t ct_waves;
     int32_t ct_force;               // 1: the continuous-tiles kernel for every launch of >= 8 frames (tests)
+    uint32_t ct_back_pct;           // the CT kernel: the last-dispatched ct_back_pct % of the grid claims
+                                    // its units from the back of its queue group (pt_tile_queue.h)
 };
 
 // Scene description in AddQuad/Sphere/MaterialToScene order (v4 :1368-1401).

@@ -1054,7 +1054,12 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_ct_kernel(PtV4Job
     unsigned long long n_seg = 0, n_esc = 0, n_slots = 0, n_fb = 0, n_sky = 0;
 
     constexpr uint32_t kNone = PtTileQueue<kWaves>::kNone;
-    PtTileQueue<kWaves>(job.queue, job.order, job.units, job.nunits, ntiles, wv).save(s_tq[wv], lane);
+    {
+        PtTileQueue<kWaves> q(job.queue, job.order, job.units, job.nunits, ntiles, wv);
+        q.back = job.ct_back_pct != 0 &&
+                 (uint64_t)blockIdx.x * 100u >= (uint64_t)gridDim.x * (100u - (job.ct_back_pct < 100u ? job.ct_back_pct : 100u));
+        q.save(s_tq[wv], lane);
+    }
     // the events' wave-uniform state in LDS (as render_body_ct: the pool loop's SGPRs stay free)
     uint32_t* const ws = s_ws[wv];
     auto ws_ld = [&](int k) -> uint32_t { return __builtin_amdgcn_readfirstlane(ws[k]); };
