@@ -554,8 +554,13 @@ int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls, uin
         // then every kSchedRebuild launches (the costs of a fixed view barely change; the builder
         // is a one-workgroup kernel of ~57 us at 1080p)
         if (s->have_cost && (!s->built || s->launches % kSchedRebuild == 0)) {
+            // units of twice the adaptive cost for the diffuse kernels' continuous-tiles pool, whose
+            // lanes no longer idle in a unit's tail while the dequeues still cost (A/B, 60 launches:
+            // 1080p 8 spp 0.2497 vs 0.2525 ms, env 16 spp 0.4911 vs 0.4961, 4K 8 spp 0.8185 vs 0.8202;
+            // 3x: 0.2513 / 0.4965 / 0.8356)
+            const uint32_t unit_mult = key.kind == 0 && !g.no_ct ? 2u : 1u;
             hipError_t e = pt_launch_schedule(s->cost, s->order, s->units, s->units + 2 * s->key.ntiles + 1, s->key.ntiles,
-                                              split, st);
+                                              split, unit_mult, st);
             if (e != hipSuccess) return fail(PT_EHIP, "schedule launch failed: %s", hipGetErrorString(e));
             s->built = true;
         }

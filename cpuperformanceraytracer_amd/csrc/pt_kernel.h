@@ -88,5 +88,6 @@ inline uint32_t pt_job_tiles(const PtJob& j)
 // once, or as its two halves when it costs more than 1/split of a resident wave's share of the
 // launch; split 0: never), units = runs of about equal cost over it, *nunits = their number.
 // cost: 2 x ntiles words (pt_record_cost), order: up to 2 x ntiles entries, units: 2 x ntiles + 1.
+// unit_mult: a multiple of the adaptive unit cost (the continuous-tiles pools: 2).
 hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* units, uint32_t* nunits,
-                              uint32_t ntiles, uint32_t split, hipStream_t stream);
+                              uint32_t ntiles, uint32_t split, uint32_t unit_mult, hipStream_t stream);

@@ -1937,7 +1937,7 @@ __global__ __launch_bounds__(1024) void pt_schedule_kernel(const uint32_t* __res
 }  // namespace
 
 hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* units, uint32_t* nunits,
-                              uint32_t ntiles, uint32_t split, hipStream_t st)
+                              uint32_t ntiles, uint32_t split, uint32_t unit_mult, hipStream_t st)
 {
     if (ntiles == 0) return hipSuccess;
     if (!cost || !order || !units || !nunits) return hipErrorInvalidValue;
@@ -1949,7 +1949,7 @@ hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* u
             cus = 256;
         const uint32_t waves = (uint32_t)cus * 20u;
         unit_cost = (uint32_t)((2ull * ntiles) / (3ull * waves));
-        unit_cost = std::min(kUnitCostMax, std::max(kUnitCostMin, unit_cost));
+        unit_cost = std::min(kUnitCostMax, std::max(kUnitCostMin, unit_cost)) * (unit_mult ? unit_mult : 1u);
     }
     uint32_t split_div = 0;
     {   // tiles costing more than 1/split of a wave's share are split (pt_tile_queue.h)
