@@ -59,7 +59,14 @@ struct Sched {
     bool built = false;           // order/units hold a schedule
     unsigned long long launches = 0;
     unsigned long long last_use = 0;
+    // occupancy of the diffuse continuous-tiles kernel (PtJob::ct_wide): the first kTuneLaunches
+    // scheduled launches alternate 5 and 6 waves per SIMD between event pairs, the faster total is
+    // kept (A/B: 1080p 8 spp 0.243 vs 0.248 ms at 6, 720p 8 spp 0.145 vs 0.138 at 5)
+    hipEvent_t tune_ev[2 * 8] = {};
+    uint32_t tuned = 0;           // timed launches enqueued
+    int8_t wide = -1;             // the pick (-1: not yet)
 };
+constexpr uint32_t kTuneLaunches = 8;
 constexpr int kSchedSlots = 16;
 constexpr int kBands = 4;   // PT_FLAG_PIN_HOST: row bands of a pipelined frame
 constexpr uint32_t kSchedMinTiles = 512;   // smaller jobs (e.g. one RenderTile) are not scheduled
@@ -148,6 +155,7 @@ struct State {
     uint32_t ring_guard_cap = ~0u;
     int32_t v4_ct_force = 0;   // PT_MI355_V4_CT=1 (read by pt_init): PtV4Job::ct_force (tests)
     uint32_t ct_back_pct = 20;   // PT_MI355_BACK (read by pt_init): PtJob::ct_back_pct (0: none)
+    uint32_t ct_waves = 0;       // PT_MI355_CT_WAVES (read by pt_init): 5 or 6 (0: timed per geometry)
     uint32_t split = 1;   // PT_MI355_SPLIT (read by pt_init): tile split factor of the schedule (0: none)
     bool no_ct = false;   // PT_MI355_NO_CT=1 (read by pt_init): one-chunk launches on render_body (A/B)
 };
@@ -445,6 +453,7 @@ PtJob base_job(float* buf, int32_t w, int32_t h)
     j.ct_slots = nullptr;
     j.ct_waves = 0;
     j.ct_back_pct = 0;   // (launch(): launches of <= 16 frames)
+    j.ct_wide = 0;
     j.scene = nullptr;
     return j;
 }
@@ -454,6 +463,8 @@ void free_sched(Sched& s)
     if (s.cost) (void)hipFree(s.cost);
     if (s.order) (void)hipFree(s.order);
     if (s.units) (void)hipFree(s.units);
+    for (hipEvent_t e : s.tune_ev)
+        if (e) (void)hipEventDestroy(e);
     s = Sched{};
 }
 
@@ -544,6 +555,7 @@ struct LaunchSched {
     const uint32_t* units = nullptr;
     const uint32_t* nunits = nullptr;
     uint32_t* cost = nullptr;
+    Sched* sched = nullptr;
 };
 // split: the schedule builder's tile split factor (pt_launch_schedule; 0: whole tiles)
 int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls, uint32_t split)
@@ -565,6 +577,7 @@ int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls, uin
             s->built = true;
         }
         if (s->built) {
+            ls->sched = s;
             ls->order = s->order;
             ls->units = s->units;
             ls->nunits = s->units + 2 * s->key.ntiles + 1;
@@ -642,6 +655,38 @@ int use_ct_slots(Dev& dv, const LaunchSched& ls, hipStream_t st, float** slots, 
     return PT_OK;
 }
 
+// PtJob::ct_wide of a diffuse continuous-tiles launch: PT_MI355_CT_WAVES (5 or 6) when set, else the
+// faster of the two on the geometry's first scheduled launches; *tev: the event pair to record
+// around this launch while they are timed
+int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
+{
+    *tev = nullptr;
+    j.ct_wide = g.ct_waves == 6 ? 1u : 0u;
+    Sched* s = ls.sched;
+    if (g.ct_waves || !j.ct_slots || j.env || !s) return PT_OK;
+    if (s->wide >= 0) {
+        j.ct_wide = (uint32_t)s->wide;
+    } else if (s->tuned < kTuneLaunches) {
+        hipEvent_t* ev = &s->tune_ev[2 * s->tuned];
+        for (int i = 0; i < 2; ++i)
+            if (!ev[i]) HIP_TRY(hipEventCreate(&ev[i]));
+        j.ct_wide = s->tuned++ & 1u;
+        *tev = ev;
+    } else if (hipEventQuery(s->tune_ev[2 * kTuneLaunches - 1]) == hipSuccess) {
+        float t[2] = {0.f, 0.f};
+        for (uint32_t i = 0; i < kTuneLaunches; ++i) {
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, s->tune_ev[2 * i], s->tune_ev[2 * i + 1]));
+            t[i & 1] += ms;
+        }
+        s->wide = t[1] < t[0] ? 1 : 0;
+        j.ct_wide = (uint32_t)s->wide;
+    } else {
+        (void)hipGetLastError();   // (hipErrorNotReady: the timed launches are still running)
+    }
+    return PT_OK;
+}
+
 int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
 {
     LaunchSched ls;
@@ -663,8 +708,12 @@ int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
     // large part of them (A/B, scripts/gpu_ab.sh, 20 % vs none: 1080p 8 spp 0.2533 vs 0.2561 ms,
     // env 16 spp 0.4967 vs 0.5030, 4K 8 spp 0.8217 vs 0.8309; 4K 64 spp 5.913 vs 5.763: not there)
     j.ct_back_pct = j.nframes <= 16 ? g.ct_back_pct : 0u;
+    hipEvent_t* tev = nullptr;
+    if ((rc = ct_occupancy(ls, j, &tev))) return rc;
+    if (tev) HIP_TRY(hipEventRecord(tev[0], st));
     hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
+    if (tev) HIP_TRY(hipEventRecord(tev[1], st));
     return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_render's early return)
 }
 
@@ -1313,6 +1362,8 @@ int pt_init(const pt_config* cfg)
     g.v4_ct_force = getenv("PT_MI355_V4_CT") && !strcmp(getenv("PT_MI355_V4_CT"), "1");
     g.ct_back_pct = 20;
     if (const char* bk = getenv("PT_MI355_BACK")) g.ct_back_pct = (uint32_t)strtoul(bk, nullptr, 10);
+    g.ct_waves = 0;
+    if (const char* cw = getenv("PT_MI355_CT_WAVES")) g.ct_waves = (uint32_t)strtoul(cw, nullptr, 10);
     g.split = 1;
     if (const char* sp = getenv("PT_MI355_SPLIT")) g.split = (uint32_t)strtoul(sp, nullptr, 10);
     if (const char* cap = getenv("PT_MI355_RING_GUARD_CAP")) {

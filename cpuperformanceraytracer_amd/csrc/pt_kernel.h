@@ -52,6 +52,7 @@ struct PtJob {
     uint32_t ct_waves;             // f32 per wave for ct_waves waves; nullptr: one-chunk launches use render_body
     uint32_t ct_back_pct;          // the continuous-tiles pool: the last-dispatched ct_back_pct % of the grid
                                    // claims its units from the back of its queue group (pt_tile_queue.h)
+    uint32_t ct_wide;              // the diffuse continuous-tiles kernel at 6 waves per SIMD (0: 5)
     // mainImage's frame constants (scalar.cpp:338-347), set by pt_launch_render on the host with the
     // same correctly rounded f32 operations: W, H, 1/W, 1/H, W/H, 1/(W/H).  Kernel arguments are
     // scalar registers; computed in the kernel they were VGPRs that the tile loop spilled.

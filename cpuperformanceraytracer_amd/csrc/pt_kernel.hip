@@ -1718,8 +1718,10 @@ __global__ __launch_bounds__(64 * waves_per_block<true>()) void pt_render_env_ke
     render_body<LAYOUT, true, COUNT, MULTI, false>(job);
 }
 
-template <int LAYOUT, bool COUNT>
-__global__ __launch_bounds__(64 * waves_per_block<false>()) __attribute__((amdgpu_waves_per_eu(PT_AMBIENT_WAVES, PT_AMBIENT_WAVES))) void
+// WAVES per SIMD: 5 (96 VGPRs) or 6 (80 VGPRs, 29 SGPRs spilled to VGPR lanes); which one is faster
+// depends on the launch geometry (pt_capi.cpp launch(): timed on a geometry's first launches)
+template <int LAYOUT, bool COUNT, int WAVES>
+__global__ __launch_bounds__(64 * waves_per_block<false>()) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void
 pt_render_ct_kernel(PtJob job)
 {
     render_body_ct<LAYOUT, false, COUNT>(job);
@@ -1759,18 +1761,18 @@ constexpr int kRingMinFrames = PT_RING_MIN;
 
 // One-chunk ambient launches on the continuous-tiles pool (render_body_ct) when the caller provides
 // its slots for the whole grid; false: not launched (render_body then).
-template <int LAYOUT, bool ENV, bool COUNT>
+template <int LAYOUT, bool ENV, bool COUNT, bool WIDE>
 constexpr auto ct_kernel_of()
 {
     if constexpr (ENV) return pt_render_ct_env_kernel<LAYOUT, COUNT>;
-    else return pt_render_ct_kernel<LAYOUT, COUNT>;
+    else return pt_render_ct_kernel<LAYOUT, COUNT, WIDE ? 6 : 5>;
 }
 
 template <int LAYOUT, bool ENV, bool COUNT>
 bool launch_ct(const PtJob& job, hipStream_t st, unsigned tiles)
 {
     constexpr int wpb = waves_per_block<ENV>();
-    auto k = ct_kernel_of<LAYOUT, ENV, COUNT>();
+    auto k = job.ct_wide ? ct_kernel_of<LAYOUT, ENV, COUNT, true>() : ct_kernel_of<LAYOUT, ENV, COUNT, false>();
     const unsigned blocks = (unsigned)std::min<long>(pt_resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
     if (!job.ct_slots || (uint64_t)blocks * wpb > job.ct_waves) return false;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
@@ -1970,19 +1972,25 @@ uint32_t pt_ct_resident_waves()
 {
     static_assert(waves_per_block<false>() == waves_per_block<true>(), "one block shape for the CT kernels");
     constexpr int wpb = waves_per_block<false>();
-    const int r[12] = {pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, false>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, true>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, false>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, true>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, false>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, true>, 64 * wpb),
+    const int r[18] = {pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, false, 5>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, true, 5>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, false, 5>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, true, 5>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, false, 5>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, true, 5>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, false, 6>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, true, 6>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, false, 6>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, true, 6>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, false, 6>, 64 * wpb),
+                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, true, 6>, 64 * wpb),
                        pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_INTERLEAVED, false>, 64 * wpb),
                        pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_INTERLEAVED, true>, 64 * wpb),
                        pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_PLANAR8, false>, 64 * wpb),
                        pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_PLANAR8, true>, 64 * wpb),
                        pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_TILED_PLANAR8, false>, 64 * wpb),
                        pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_TILED_PLANAR8, true>, 64 * wpb)};
-    return (uint32_t)*std::max_element(r, r + 12) * (uint32_t)wpb;
+    return (uint32_t)*std::max_element(r, r + 18) * (uint32_t)wpb;
 }
 
 hipError_t pt_launch_render(const PtJob& job_in, hipStream_t st, bool count)

@@ -124,3 +124,25 @@ def test_split_schedules_match_oracle(monkeypatch, pool, env, frames):
     ref = pyoracle.render(W, H, nframes=K * frames, num_bounces=B, env=envmap)
     assert bits_equal(got, ref), mismatch_report(got, ref)
     pt.shutdown()
+
+
+@pytest.mark.parametrize("waves", ["5", "6", "0"])
+def test_ct_occupancy_variants_match_oracle(monkeypatch, waves):
+    """The diffuse continuous-tiles kernel at 5 and 6 waves per SIMD (PT_MI355_CT_WAVES, read by
+    pt_init; 0: pt_capi.cpp ct_occupancy times the two on a geometry's first 8 scheduled launches,
+    alternating, and keeps the faster) runs the same per-pixel code: 12 launches of 2 frames of one
+    scheduled geometry equal the oracle bit for bit."""
+    import torch
+    import cpuperformanceraytracer_amd as pt
+    from cpuperformanceraytracer_amd.device import render_device
+    monkeypatch.setenv("PT_MI355_CT_WAVES", waves)
+    W, H, B, K, frames = 256, 128, 8, 12, 2   # 512 tiles: scheduled
+    pt.init(num_bounces=B)
+    buf = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda:0")
+    for k in range(K):
+        render_device(buf, W, H, frame_first=1 + k * frames, nframes=frames, num_bounces=B)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy().reshape(H, W, 3)
+    ref = pyoracle.render(W, H, nframes=K * frames, num_bounces=B)
+    assert bits_equal(got, ref), mismatch_report(got, ref)
+    pt.shutdown()
