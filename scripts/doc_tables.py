@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Regenerate the measurement tables of DESIGN.md §4 and README.md from a profile tag's committed
 files (profiles/<TAG>_bench_*.json, profiles/<TAG>*_pmc.txt, *_kernel_stats.csv):
-    python3 scripts/doc_tables.py TAG
+    python3 scripts/doc_tables.py TAG [PMC_TAG]
+(PMC_TAG: the tag whose PMC / kernel-trace summaries stand in for a workload TAG did not profile --
+its kernel unchanged since.)
 Rewrites the blocks between the marker comments <!-- tables:design:begin/end --> and
 <!-- tables:readme:begin/end --> (README.md)."""
 import csv
@@ -13,6 +15,8 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 P = ROOT / "profiles"
 tag = sys.argv[1]
+pmc_tag = sys.argv[2] if len(sys.argv) > 2 else tag
+used_fallback = []
 
 
 def bench(w):
@@ -21,6 +25,9 @@ def bench(w):
 
 def pmc(short):
     f = P / f"{tag}{short}_pmc.txt"
+    if not f.exists() and (P / f"{pmc_tag}{short}_pmc.txt").exists():
+        f = P / f"{pmc_tag}{short}_pmc.txt"
+        used_fallback.append(short.strip("_"))
     out = {}
     if f.exists():
         for line in f.read_text().splitlines():
@@ -79,7 +86,8 @@ cpu = B["c2"].get("cpu_baseline") or {}
 if cpu:
     rows.append((f"CPU baseline: oracle port, {cpu.get('cores')} threads (the box's cgroup CPU quota), ~{cpu.get('sample', '').split(';')[-1].strip()}",
                  [f"{e(cpu['value'])} ray-samples/s (GPU ×{B['c2']['value'] / cpu['value']:.0f})", "", "", ""]))
-hdr = (f"| quantity (one launch; round 4, bench `profiles/{tag}_bench_*.json`, rocprofv3 `profiles/{tag}_*`) | c2: 1920×1080, 8 spp, 8 b | "
+fb = (f"; {', '.join(used_fallback)}: `profiles/{pmc_tag}_*`, kernel unchanged" if used_fallback else "")
+hdr = (f"| quantity (one launch; round 4, bench `profiles/{tag}_bench_*.json`, rocprofv3 `profiles/{tag}_*`{fb}) | c2: 1920×1080, 8 spp, 8 b | "
        "c3: 3840×2160, 64 spp | c4: 1080p, 16 spp, env | c5: 7680×4320, 256 spp (one GPU, whole image) |\n|---|---|---|---|---|\n")
 design = hdr + "".join(f"| {r} | " + " | ".join(v) + " |\n" for r, v in rows)
 v = B["v4"]
@@ -100,7 +108,7 @@ readme = ("| workload | kernel time per launch | ray-samples/s (px·spp·bounces
           f"| 1920×1080, 16 spp, env map (configs[3]) | {ms('c4'):.3f} ms | {e(B['c4']['value'])} | {B['c4']['roofline']['frac']:.3f} |\n"
           f"| 7680×4320, 256 spp, one GPU (configs[4]'s image) | {ms('c5'):.1f} ms | {e(B['c5']['value'])} | {B['c5']['roofline']['frac']:.3f} |\n"
           f"| v4 renderer, 1920×1080, 8 spp, equirect env | {ms('v4'):.3f} ms | {e(v['value'])} | {v['roofline']['frac']:.3f} |\n"
-          f"\n(`profiles/{tag}_bench_*.json`; rocprofv3 summaries `profiles/{tag}_*`"
+          f"\n(`profiles/{tag}_bench_*.json`; rocprofv3 summaries `profiles/{tag}_*`{fb}"
           + (f"; CPU baseline of the headline: {e(cpu['value'])} ray-samples/s on {cpu.get('cores')} host threads, GPU ×{B['c2']['value'] / cpu['value']:.0f}" if cpu else "")
           + ".)\n")
 
