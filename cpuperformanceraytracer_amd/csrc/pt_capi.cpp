@@ -59,9 +59,9 @@ struct Sched {
     bool built = false;           // order/units hold a schedule
     unsigned long long launches = 0;
     unsigned long long last_use = 0;
-    // occupancy of the diffuse continuous-tiles kernel (PtJob::ct_wide): the first kTuneLaunches
-    // scheduled launches alternate 5 and 6 waves per SIMD between event pairs, the faster total is
-    // kept (A/B: 1080p 8 spp 0.243 vs 0.248 ms at 6, 720p 8 spp 0.145 vs 0.138 at 5)
+    // occupancy of the diffuse continuous-tiles kernel (PtJob::ct_wide, PT_MI355_CT_WAVES=0 only): the
+    // first kTuneLaunches scheduled launches alternate 5 and 6 waves per SIMD between event pairs, the
+    // faster total is kept (A/B: 1080p 8 spp 0.245 vs 0.250 ms at 6, 720p 8 spp 0.147 vs 0.138 at 5)
     hipEvent_t tune_ev[2 * 8] = {};
     uint32_t tuned = 0;           // timed launches enqueued
     int8_t wide = -1;             // the pick (-1: not yet)
@@ -155,7 +155,8 @@ struct State {
     uint32_t ring_guard_cap = ~0u;
     int32_t v4_ct_force = 0;   // PT_MI355_V4_CT=1 (read by pt_init): PtV4Job::ct_force (tests)
     uint32_t ct_back_pct = 20;   // PT_MI355_BACK (read by pt_init): PtJob::ct_back_pct (0: none)
-    uint32_t ct_waves = 0;       // PT_MI355_CT_WAVES (read by pt_init): 5 or 6 (0: timed per geometry)
+    uint32_t ct_waves = 5;       // PT_MI355_CT_WAVES (read by pt_init): 5 or 6; 0: timed per geometry
+                                 // (experimental: DESIGN.md 3c, a known mismatch under two processes)
     uint32_t split = 1;   // PT_MI355_SPLIT (read by pt_init): tile split factor of the schedule (0: none)
     bool no_ct = false;   // PT_MI355_NO_CT=1 (read by pt_init): one-chunk launches on render_body (A/B)
 };
@@ -655,9 +656,10 @@ int use_ct_slots(Dev& dv, const LaunchSched& ls, hipStream_t st, float** slots, 
     return PT_OK;
 }
 
-// PtJob::ct_wide of a diffuse continuous-tiles launch: PT_MI355_CT_WAVES (5 or 6) when set, else the
-// faster of the two on the geometry's first scheduled launches; *tev: the event pair to record
-// around this launch while they are timed
+// PtJob::ct_wide of a diffuse continuous-tiles launch: PT_MI355_CT_WAVES (default 5, or 6), or with
+// PT_MI355_CT_WAVES=0 the faster of the two on the geometry's first scheduled launches (experimental:
+// a 2-process rehearsal on one GPU produced a mismatching row with it); *tev: the event
+// pair to record around this launch while they are timed
 int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
 {
     *tev = nullptr;
@@ -670,7 +672,11 @@ int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
         hipEvent_t* ev = &s->tune_ev[2 * s->tuned];
         for (int i = 0; i < 2; ++i)
             if (!ev[i]) HIP_TRY(hipEventCreate(&ev[i]));
+#ifdef PT_TUNE_SAME
+        j.ct_wide = (s->tuned++, 0u);   // (dev A/B: the timing without the alternation)
+#else
         j.ct_wide = s->tuned++ & 1u;
+#endif
         *tev = ev;
     } else if (hipEventQuery(s->tune_ev[2 * kTuneLaunches - 1]) == hipSuccess) {
         float t[2] = {0.f, 0.f};
@@ -1362,7 +1368,7 @@ int pt_init(const pt_config* cfg)
     g.v4_ct_force = getenv("PT_MI355_V4_CT") && !strcmp(getenv("PT_MI355_V4_CT"), "1");
     g.ct_back_pct = 20;
     if (const char* bk = getenv("PT_MI355_BACK")) g.ct_back_pct = (uint32_t)strtoul(bk, nullptr, 10);
-    g.ct_waves = 0;
+    g.ct_waves = 5;
     if (const char* cw = getenv("PT_MI355_CT_WAVES")) g.ct_waves = (uint32_t)strtoul(cw, nullptr, 10);
     g.split = 1;
     if (const char* sp = getenv("PT_MI355_SPLIT")) g.split = (uint32_t)strtoul(sp, nullptr, 10);

@@ -3,7 +3,7 @@
 # `bench.py --gpus 2` rehearsal through spawn_ranks.
 set -euo pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r04t
+OUT=${OUT:-gpurun_out/r04t}
 mkdir -p $OUT
 timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -rf > $OUT/gpu_tests.log 2>&1 || { tail -40 $OUT/gpu_tests.log; exit 1; }
 tail -2 $OUT/gpu_tests.log
