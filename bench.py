@@ -331,13 +331,28 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
     def gather():
         return gather_rows(buf.cpu() if rehearse else buf, Wg, Hg, rank, world)
 
+    def all_ranks(vals, op):
+        """vals reduced over the ranks (op: a torch.distributed ReduceOp); the values themselves when
+        world == 1.  Device tensors under RCCL, host tensors under gloo."""
+        if world == 1:
+            return list(vals)
+        t = torch.tensor(list(vals), dtype=torch.float64)
+        if not rehearse and ops.dev != "cpu" and dist.get_backend() == "nccl":
+            t = t.to(ops.dev)
+        dist.all_reduce(t, op=op)
+        return [float(v) for v in t.tolist()]
+
     # Device warm-up, untimed, before the W warmup steps: the MI355X reaches its steady clocks only
     # after ~25 ms of sustained load (per-launch time at 1080p, 8 spp: 0.46 ms over the first 20
     # launches, 0.379 over the next 20, 0.357 from the 60th on -- scripts/clock_ramp.py), and the
     # reference's progressive renderer runs continuously.  Reported as "device_warmup".
+    # Every rank accumulates the same frames: the decision to run another warm-up batch is taken by
+    # all ranks together (another batch while ANY rank is under the time budget).  Decided per rank,
+    # two ranks whose clocks crossed the budget in different batches accumulated different frame
+    # ranges -- the rows-763 mismatch of the round-4 two-process rehearsals (DESIGN.md 3c).
     dw_ms, dw_steps = 0.0, 0
     batch = 1 if strong else 10
-    while dw_ms < args.device_warmup_ms and dw_steps < 4000:
+    while all_ranks([float(dw_ms < args.device_warmup_ms and dw_steps < 4000)], dist.ReduceOp.MAX)[0] > 0:
         e0, e1 = ops.event(), ops.event()
         ops.record(e0)
         for _ in range(batch):
@@ -396,6 +411,9 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
     ops.sync()
     elapsed = time.perf_counter() - t0
     timed_end = frame
+    lo, hi = all_ranks([-timed_end, timed_end], dist.ReduceOp.MAX)
+    if -lo != hi:   # (the invariant the gathered image and its check rely on)
+        raise AssertionError(f"the ranks accumulated different frame ranges: ends {-lo:.0f} .. {hi:.0f}")
     if not strong:
         launch_ms_avg = ops.elapsed_ms(ev_a, ev_b) / K
         if world > 1:

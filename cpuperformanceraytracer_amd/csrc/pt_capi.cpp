@@ -40,11 +40,12 @@ struct SchedKey {
     int32_t width = 0, height = 0, col0 = 0, ncols = 0, row_start = 0, row_stride = 0, nrows = 0, bounces = 0;
     const float* env = nullptr;
     uint32_t ntiles = 0;
+    uint32_t split = 0;   // the schedule builder's split factor (launch(): one-chunk launches only)
     bool operator==(const SchedKey& o) const
     {
         return kind == o.kind && width == o.width && height == o.height && col0 == o.col0 && ncols == o.ncols &&
                row_start == o.row_start && row_stride == o.row_stride && nrows == o.nrows && bounces == o.bounces &&
-               env == o.env && ntiles == o.ntiles;
+               env == o.env && ntiles == o.ntiles && split == o.split;
     }
 };
 struct Sched {
@@ -156,7 +157,11 @@ struct State {
     int32_t v4_ct_force = 0;   // PT_MI355_V4_CT=1 (read by pt_init): PtV4Job::ct_force (tests)
     uint32_t ct_back_pct = 20;   // PT_MI355_BACK (read by pt_init): PtJob::ct_back_pct (0: none)
     uint32_t ct_waves = 5;       // PT_MI355_CT_WAVES (read by pt_init): 5 or 6; 0: timed per geometry
-                                 // (experimental: DESIGN.md 3c, a known mismatch under two processes)
+    // test hook: PT_MI355_CT_WAVES_SEQ (read by pt_init), a string of '5' / '6' cycled over the
+    // diffuse continuous-tiles launches -- forced changes of the grid between the launches of one
+    // accumulation (tests/test_gpu_configs.py); empty: off
+    char ct_seq[64] = {};
+    uint32_t ct_seq_len = 0, ct_seq_pos = 0;
     uint32_t split = 1;   // PT_MI355_SPLIT (read by pt_init): tile split factor of the schedule (0: none)
     bool no_ct = false;   // PT_MI355_NO_CT=1 (read by pt_init): one-chunk launches on render_body (A/B)
 };
@@ -289,9 +294,12 @@ int xfer(int d, const Geo& geo, float* host, bool to_device, const Region& rg)
 }
 
 // Synchronise every device stream and report what the kernels recorded in their error words since
-// the last synchronisation: a tile the ring pool's iteration guard abandoned mid-pool (pt_kernel.hip)
-// leaves a wrong accumulator, so no call that waited for such a launch returns PT_OK.  The words are
-// reset when reported.
+// the last synchronisation: a tile that a pool's guard abandoned (the ring pool's iteration guard or
+// the continuous-tiles pool's chunk / event guards, pt_kernel.hip, pt_v4.hip) leaves a wrong
+// accumulator, so no call that waited for such a launch returns PT_OK.  The words are reset when
+// reported.  Device jobs on callers' streams are covered once those streams have been synchronised
+// (pt_check_device_errors): a launch still running when the words are read and reset may record its
+// fault after the reset, and that fault is then reported by the next check.
 int sync_all()
 {
     int rc;
@@ -313,8 +321,8 @@ int sync_all()
         HIP_TRY(hipMemsetAsync(dv.derr + 1, 0xff, sizeof(uint32_t), dv.stream));
         HIP_TRY(hipStreamSynchronize(dv.stream));
         dv.herr[0] = 0;
-        return fail(PT_EKERNEL, "device %d: the ring pool's iteration guard abandoned %u tile(s) mid-pool (first: tile %u "
-                    "of its launch); the accumulator is invalid", dv.ordinal, n, tile);
+        return fail(PT_EKERNEL, "device %d: a pool guard (ring iterations or continuous-tiles chunks) abandoned %u "
+                    "tile(s) (first: tile %u of its launch); the accumulator is invalid", dv.ordinal, n, tile);
     }
     return PT_OK;
 }
@@ -664,6 +672,10 @@ int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
 {
     *tev = nullptr;
     j.ct_wide = g.ct_waves == 6 ? 1u : 0u;
+    if (g.ct_seq_len && j.ct_slots && !j.env) {   // (test hook: the forced sequence)
+        j.ct_wide = g.ct_seq[g.ct_seq_pos++ % g.ct_seq_len] == '6' ? 1u : 0u;
+        return PT_OK;
+    }
     Sched* s = ls.sched;
     if (g.ct_waves || !j.ct_slots || j.env || !s) return PT_OK;
     if (s->wide >= 0) {
@@ -672,11 +684,7 @@ int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
         hipEvent_t* ev = &s->tune_ev[2 * s->tuned];
         for (int i = 0; i < 2; ++i)
             if (!ev[i]) HIP_TRY(hipEventCreate(&ev[i]));
-#ifdef PT_TUNE_SAME
-        j.ct_wide = (s->tuned++, 0u);   // (dev A/B: the timing without the alternation)
-#else
         j.ct_wide = s->tuned++ & 1u;
-#endif
         *tev = ev;
     } else if (hipEventQuery(s->tune_ev[2 * kTuneLaunches - 1]) == hipSuccess) {
         float t[2] = {0.f, 0.f};
@@ -699,7 +707,9 @@ int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
     int rc;
     // split tiles: launches of one 8-frame chunk (a tile's half of several chunks is a short chunk
     // each, and the pool's two chunk contexts then wait on each other: 1080p 16 spp 0.452 vs 0.437 ms)
-    if ((rc = use_dev(dv)) || (rc = use_sched(dv, sched_key(j), st, &ls, j.nframes <= 8 ? g.split : 0u))) return rc;
+    SchedKey key = sched_key(j);
+    key.split = j.nframes <= 8 ? g.split : 0u;
+    if ((rc = use_dev(dv)) || (rc = use_sched(dv, key, st, &ls, key.split))) return rc;
     j.scene = dv.dscene;
     j.queue = ls.queue;
     j.queue_next = ls.queue_next;
@@ -1321,6 +1331,8 @@ int pt_init(const pt_config* cfg)
         c.device_count = 1;
         c.devices[0] = c.device;
     }
+    if (const char* cw = getenv("PT_MI355_CT_WAVES"); cw && strcmp(cw, "5") && strcmp(cw, "6") && strcmp(cw, "0"))
+        return fail(PT_EINVAL, "PT_MI355_CT_WAVES=%s: 5, 6 or 0 (timed per geometry)", cw);
     if (g.inited) pt_shutdown();
     DeviceGuard guard;
     int ndev = 0;
@@ -1370,6 +1382,11 @@ int pt_init(const pt_config* cfg)
     if (const char* bk = getenv("PT_MI355_BACK")) g.ct_back_pct = (uint32_t)strtoul(bk, nullptr, 10);
     g.ct_waves = 5;
     if (const char* cw = getenv("PT_MI355_CT_WAVES")) g.ct_waves = (uint32_t)strtoul(cw, nullptr, 10);
+    g.ct_seq_len = g.ct_seq_pos = 0;
+    if (const char* sq = getenv("PT_MI355_CT_WAVES_SEQ")) {
+        for (const char* c = sq; *c && g.ct_seq_len < sizeof(g.ct_seq); ++c)
+            if (*c == '5' || *c == '6') g.ct_seq[g.ct_seq_len++] = *c;
+    }
     g.split = 1;
     if (const char* sp = getenv("PT_MI355_SPLIT")) g.split = (uint32_t)strtoul(sp, nullptr, 10);
     if (const char* cap = getenv("PT_MI355_RING_GUARD_CAP")) {

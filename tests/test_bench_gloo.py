@@ -21,7 +21,24 @@ def _free_port() -> int:
     return p
 
 
-def _worker(rank, world, port, scaling, q):
+class _SkewedOps:
+    """bench.HostOps whose clock runs at a rank-dependent rate (rank 0: 5 ms per interval, rank 1:
+    25 ms): left to decide alone, the ranks would run different numbers of device warm-up batches."""
+
+    def __init__(self, rank):
+        import bench
+        self._h = bench.HostOps()
+        self.dev = "cpu"
+        self._ms = 5.0 if rank == 0 else 25.0
+
+    def __getattr__(self, name):
+        return getattr(self._h, name)
+
+    def elapsed_ms(self, a, b):
+        return self._ms
+
+
+def _worker(rank, world, port, scaling, q, skew=False):
     import sys
     from pathlib import Path
     root = str(Path(__file__).resolve().parents[1])
@@ -35,8 +52,8 @@ def _worker(rank, world, port, scaling, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         wl = Workload("tiny", 64, 36, 3, 8, scaling=scaling)   # configs[4]'s shape, scaled down
-        args = bench.parse(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--device-warmup-ms", "0",
-                            "--verify-rows", "2"])
+        args = bench.parse(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--device-warmup-ms",
+                            "20" if skew else "0", "--verify-rows", "2"])
 
         def render_fn(buf, W, H, f, n, rs, st, nr):
             pyoracle.render(W, H, frame_first=f, nframes=n, num_bounces=wl.num_bounces, row_start=rs,
@@ -49,7 +66,8 @@ def _worker(rank, world, port, scaling, q):
             return {"segments": c["segments"], "samples": c["samples"], "escaped": c["escaped"],
                     "lane_slots": c["segments"], "primary": c["samples"]}
 
-        res = bench.run(args, wl, rank, world, bench.HostOps(), render_fn, count_fn, roofline=False)
+        ops = _SkewedOps(rank) if skew else bench.HostOps()
+        res = bench.run(args, wl, rank, world, ops, render_fn, count_fn, roofline=False)
         if rank == 0:
             acc = res.pop("_accumulator")
             q.put((res, acc.numpy().copy()))
@@ -98,6 +116,37 @@ def test_bench_n_rank_path_gloo(scaling):
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
     # the verified frame range ends where the timed steps end (1 warm-up + 2 timed steps)
     assert res["verified"]["frames"] == [1, 3 * wl.spp]
+
+
+def test_bench_ranks_agree_on_the_device_warmup():
+    """The device warm-up runs batches until a time budget is spent; the ranks' clocks differ, so the
+    number of batches is agreed by all ranks (the largest any rank needs).  Rank 0 alone would stop
+    after 4 batches of 10 steps (20 ms at 5 ms each), rank 1 after 1 (25 ms): both run 4, every rank
+    accumulates the same frames, and the gathered image passes the bench's own row check.  (Decided
+    per rank, this was the row mismatch of the round-4 two-process rehearsals)"""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    from oracle import pyoracle
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, "weak", q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res, acc0 = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res["device_warmup"]["steps"] == 40
+    assert res["verified"]["bit_exact"]
+    Wg, Hg = res["config"]["image"]
+    frames = (40 + 1 + 2 + 2) * 3      # device warm-up + warm-up + timed + untimed steps of 3 frames
+    ref = pyoracle.render(Wg, Hg, frame_first=1, nframes=frames, num_bounces=8, row_start=0, row_stride=world,
+                          nrows=(Hg + 1) // 2, nthreads=2)
+    got = acc0[:ref.size].reshape(ref.shape)
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
 # ---- `python bench.py --gpus N` without a launcher: bench.spawn_ranks starts the N ranks itself ----

@@ -126,12 +126,13 @@ def test_split_schedules_match_oracle(monkeypatch, pool, env, frames):
     pt.shutdown()
 
 
-@pytest.mark.parametrize("waves", ["5", "6"])
+@pytest.mark.parametrize("waves", ["5", "6", "0"])
 def test_ct_occupancy_variants_match_oracle(monkeypatch, waves):
-    """The diffuse continuous-tiles kernel at 5 (default) and 6 waves per SIMD (PT_MI355_CT_WAVES,
-    read by pt_init) runs the same per-pixel code: 12 launches of 2 frames of one scheduled geometry
-    equal the oracle bit for bit.  (PT_MI355_CT_WAVES=0, the experimental per-geometry timing that
-    alternates the two, is not covered: DESIGN.md 3c.)"""
+    """The diffuse continuous-tiles kernel at 5 and 6 waves per SIMD (PT_MI355_CT_WAVES, read by
+    pt_init) runs the same per-pixel code, and "0" -- the per-geometry timing, which alternates the
+    two grids on a geometry's first 8 scheduled launches and then keeps the faster -- changes the
+    grid between the launches of one accumulation: 12 launches of 2 frames of one scheduled geometry
+    equal the oracle bit for bit in every mode (tests/test_gpu_regime.py: the same at bench sizes)."""
     import torch
     import cpuperformanceraytracer_amd as pt
     from cpuperformanceraytracer_amd.device import render_device
