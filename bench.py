@@ -56,6 +56,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2_1080p")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-configs4", action="store_true",
+                    help="default workload: skip the configs[4] strong-scaling leg (c5_8k, a few steps)")
     ap.add_argument("--device-warmup-ms", type=float, default=60.0,
                     help="untimed GPU work before the warmup steps (clock ramp; 0 = none)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
@@ -253,6 +255,39 @@ def measure_output_stage(buf, W: int, H: int, stream) -> dict:
     return {"kernel": "pt_tonemap_kernel<INTERLEAVED>", "pixels": W * H, "ms": ms,
             "bound": "hbm", "achieved_gbps": nbytes / (ms * 1e-3) / 1e9, "peak_gbps": RL.PEAK_HBM_GBPS,
             "frac": nbytes / (ms * 1e-3) / 1e9 / RL.PEAK_HBM_GBPS, "bytes": nbytes}
+
+
+def measure_fused_output(make_launcher, W: int, nrows: int, S: int, stream, frame0: int, reps: int = 20,
+                         rounds: int = 3) -> dict:
+    """The output stage fused into the render (pt_render_device_present: each pixel's 8-bit value
+    written by the continuous-tiles kernel at its last fold) -- its cost is the difference between
+    launches that present and launches that do not, interleaved (`rounds` x `reps` launches each) on
+    a scratch accumulator of the step's geometry.  make_launcher(buf, pixels) -> launch(frame)."""
+    import torch
+    buf = torch.zeros(nrows * W * 3, dtype=torch.float32, device=stream.device)
+    pix = torch.zeros(nrows * W, dtype=torch.int32, device=stream.device)
+    plain, fused = make_launcher(buf, None), make_launcher(buf, pix)
+    t = {"plain": 0.0, "fused": 0.0}
+    frame = frame0
+    for _ in range(2):   # (the scratch geometry's schedule: built from the 2nd launch on)
+        plain(frame)
+        frame += S
+    for _ in range(rounds):
+        for name, fn in (("plain", plain), ("fused", fused)):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fn(frame)
+                frame += S
+            e1.record(stream)
+            torch.cuda.synchronize()
+            t[name] += e0.elapsed_time(e1)
+    n = rounds * reps
+    plain_ms, fused_ms = t["plain"] / n, t["fused"] / n
+    return {"launch_ms": plain_ms, "presenting_launch_ms": fused_ms, "extra_ms": fused_ms - plain_ms,
+            "pixels": W * nrows, "launches": n,
+            "note": "pt_render_device_present vs pt_render_device, interleaved launches of the step's geometry; "
+                    "extra_ms = the fused output stage's cost per presented frame (the standalone pass: ms above)"}
 
 
 class DeviceOps:
@@ -587,6 +622,31 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
     return res
 
 
+def strong_leg(wl4, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: bool = False,
+               steps: int = 3) -> dict | None:
+    """BASELINE configs[4] beside the default line: the FIXED image of the strong-scaling workload
+    (c5_8k: 7680x4320, 256 spp, 8 bounces), rows r::N per rank, each step one render + the RCCL
+    gather of the sub-images to rank 0 (both timed, reported separately), a few steps -- so the
+    driver's N = 1, 2, 4, 8 runs of the default line also trace configs[4]'s scaling curve.  The
+    gathered image is checked against a single-rank render of two rows.  Rank 0 returns a summary."""
+    a4 = parse(["--gpus", str(world), "--steps", str(steps), "--warmup", "1", "--device-warmup-ms", "0",
+                "--verify-rows", "2" if world > 1 else "0"])
+    r = run(a4, wl4, rank, world, ops, render_fn, count_fn, rehearse=rehearse, roofline=False)
+    if r is None:
+        return None
+    r.pop("_accumulator", None)
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "ms_per_step", "scaling", "config", "kernel_ms_avg",
+            "render_ms_per_step", "gather_ms", "gather_bytes", "verified", "primary_samples_per_s")
+    out = {k: r[k] for k in keep if k in r}
+    if world == 1:   # one GPU renders the whole image: the step is the render alone
+        out["render_ms_per_step"] = r["kernel_ms_avg"]
+        out["gather_ms"] = 0.0
+    out["note"] = ("BASELINE configs[4] (the fixed 7680x4320 image, 256 spp, 8 bounces), strong scaling: every "
+                   "step renders the whole image over the N ranks (rows r::N) and gathers it to rank 0 over "
+                   "RCCL; value = ray-samples/s of the whole job, render and gather per step reported apart")
+    return out
+
+
 def spawn_ranks(n: int, argv: list[str], script: str | None = None) -> int:
     """`--gpus N` without a launcher: start N rank processes of `script` (default: this file) with
     the environment torch.distributed.run gives each rank (RANK, LOCAL_RANK, WORLD_SIZE,
@@ -640,6 +700,7 @@ def main() -> None:
     import torch.distributed as dist
 
     from cpuperformanceraytracer_amd.config import CONFIGS, synthetic_env
+    from cpuperformanceraytracer_amd.shard import rows_of
     from cpuperformanceraytracer_amd.device import (JobLauncher, check_device_errors, count_device, count_v4_device,
                                                     ensure_backend, set_env_map)
 
@@ -692,6 +753,11 @@ def main() -> None:
     ops = DeviceOps(dev, stream)
     res = run(args, wl, rank, world, ops, render_fn, count_fn, rehearse=rehearse)
     check_device_errors()   # no launch of the run abandoned a tile (PT_EKERNEL otherwise)
+    # configs[4] beside the default workload's line (its scaling curve from the driver's N-GPU runs)
+    configs4 = None
+    if args.workload == "c2_1080p" and not args.no_configs4:
+        configs4 = strong_leg(CONFIGS["c5_8k"], rank, world, ops, render_fn, count_fn, rehearse=rehearse)
+        check_device_errors()
     if rank == 0:
         # the presented frame: rank 0's rendered accumulator (its first W x H pixels when sharded)
         W, H = wl.width, wl.height
@@ -700,6 +766,15 @@ def main() -> None:
         if acc is not buf:
             acc[:buf.numel()].copy_(buf)
         res["output_stage"] = measure_output_stage(acc, W, H, stream)
+        if not v4:
+            Wg, Hg = job_image(wl, world)
+            rs, st, nr = rows_of(rank, world, Hg)
+            res["output_stage"]["fused"] = measure_fused_output(
+                lambda b, px: JobLauncher(b, Wg, Hg, nframes=wl.spp, num_bounces=B, row_start=rs, row_stride=st,
+                                          nrows=nr, use_env=wl.env, stream=stream, pixels=px),
+                Wg, nr, wl.spp, stream, frame0=1)
+        if configs4 is not None:
+            res["configs4"] = configs4
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, env)
         print(json.dumps(res))

@@ -1709,6 +1709,21 @@ int pt_render_device(const pt_device_job* dj, void* stream)
 #endif
 }
 
+int pt_render_device_present(const pt_device_job* dj, uint32_t* pixels, int32_t format, void* stream)
+{
+    int rc;
+    PtJob j;
+    Dev* dv = nullptr;
+    DeviceGuard guard;
+    if (!pixels) return fail(PT_EINVAL, "null pixel buffer");
+    if (format != PT_PIXEL_RGBA8 && format != PT_PIXEL_XRGB8) return fail(PT_EINVAL, "unknown pixel format %d", format);
+    if ((rc = ensure_init()) || (rc = device_job(dj, &j)) || (rc = dev_of(dj->buf, &dv))) return rc;
+    if (dj->use_env) j.env = dv->denv;
+    j.pix_out = pixels;
+    j.pix_xrgb = format == PT_PIXEL_XRGB8;
+    return launch(*dv, j, (hipStream_t)stream, false);
+}
+
 int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
 {
     int rc;

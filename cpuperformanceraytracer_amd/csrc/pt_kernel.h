@@ -53,6 +53,11 @@ struct PtJob {
     uint32_t ct_back_pct;          // the continuous-tiles pool: the last-dispatched ct_back_pct % of the grid
                                    // claims its units from the back of its queue group (pt_tile_queue.h)
     uint32_t ct_wide;              // the diffuse continuous-tiles kernel at 6 waves per SIMD (0: 5)
+    // fused output stage (pt_render_device_present): each pixel's 8-bit value (pt_tonemap.h, the
+    // reference's default fast ACES / gamma) at pix_out[row * ncols + col] of the job's rows, written
+    // where its final accumulator value is (the continuous-tiles kernels; nullptr: none)
+    uint32_t* pix_out;
+    int32_t pix_xrgb;              // PT_PIXEL_XRGB8 (OutputToScreen) else RGBA8 (OutputToFile)
     // mainImage's frame constants (scalar.cpp:338-347), set by pt_launch_render on the host with the
     // same correctly rounded f32 operations: W, H, 1/W, 1/H, W/H, 1/(W/H).  Kernel arguments are
     // scalar registers; computed in the kernel they were VGPRs that the tile loop spilled.
@@ -71,7 +76,9 @@ struct PtJob {
 #define PT_TILE_MASK 0x3fffffffu
 #define PT_TILE_PART_SHIFT 30
 
-// Enqueue one render launch on `stream`.  Returns hipSuccess or the launch error.
+// Enqueue one render launch on `stream`.  Returns hipSuccess or the launch error.  With job.pix_out
+// the pixels are written by the render kernel itself when it is a continuous-tiles one, else by the
+// standalone output pass enqueued after it (pt_output.hip).
 hipError_t pt_launch_render(const PtJob& job, hipStream_t stream, bool count);
 
 // The continuous-tiles pool's scratch: f32 per wave, and the waves of its resident grid on the

@@ -47,6 +47,8 @@
 #define PT_EC_SQRT(x) pt::sqrt_rn(x)                     // t >= 2^-21 where the value is used
 #include "pt_envcert.h"
 #include "pt_tile_queue.h"
+#include "pt_tonemap.h"
+#include "pt_output.h"
 #include "pt_wave.h"
 #include <math.h>
 #include <algorithm>
@@ -1208,7 +1210,9 @@ enum : int {
 // radiance so far (s_envq, 32 B), and the queue is drained 64 at a time by the whole wave -- the
 // coherent texel gathers of render_body's env kernel; a drain writes the items' radiance + texel
 // (render_body's `cp + c`) to their slots.  D's fold drains the whole queue first.
-template <int LAYOUT, bool ENV, bool COUNT>
+// PRESENT: the fused output stage (job.pix_out; pt_render_device_present) -- its own instances, so
+// the plain kernels' register allocation is untouched.
+template <int LAYOUT, bool ENV, bool COUNT, bool PRESENT>
 __device__ __forceinline__ void render_body_ct(const PtJob& job)
 {
     const PtScene* __restrict__ sc = job.scene;
@@ -1266,10 +1270,22 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     const uint32_t total_tiles = (uint32_t)tiles_x * (uint32_t)((job.nrows + 7) >> 3);
     const int S = job.nframes, B = job.num_bounces;
     const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;   // channel stride
+#if PT_CT_SLOT_ALIAS   // timing-only A/B build (wrong images): every XCD's waves share 32 waves' slots,
+                      // which stay in its L2 -- what the slot area's fabric traffic costs
+    float* const slots = job.ct_slots + (size_t)((blockIdx.x % 8u) * kWavesPerBlock + wv) * kCtWaveFloats;
+#else
     float* const slots = job.ct_slots + (size_t)(blockIdx.x * kWavesPerBlock + wv) * kCtWaveFloats;
+#endif
     // lerp weight of frame f of the launch: the table, or its correctly rounded reciprocal (:812)
     auto weight = [&](int f) {
         return f < kMaxWeights ? s_w[f] : pt::rcp_rn((float)(job.frame_first + (uint32_t)f) + 1.0f);
+    };
+    // the fused output stage: a pixel's final accumulator value -> its 8-bit pixel (OutputToScreen /
+    // OutputToFile, v4 :1260-1331; pt_tonemap.h), at the point the launch writes that value
+    auto present = [&](int lc, int lr, const V3& acc) {
+        if constexpr (PRESENT)
+            job.pix_out[(size_t)lr * (uint32_t)job.ncols + (uint32_t)lc] =
+                pt_tone::pack<true, true>(acc.x, acc.y, acc.z, job.pix_xrgb != 0);
     };
 
     Camera cam;
@@ -1414,6 +1430,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                     px[0] = acc.x;
                     px[cs] = acc.y;
                     px[2 * cs] = acc.z;
+                    present(lc, lr, acc);
                 }
             }
             const uint64_t hm = pt_ballot(items);
@@ -1495,6 +1512,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 px[0] = acc.x;
                 px[cs] = acc.y;
                 px[2 * cs] = acc.z;
+                present(lc, lr, acc);
             } else {
                 s_acc[wv][0][lane] = acc.x;
                 s_acc[wv][1][lane] = acc.y;
@@ -1720,17 +1738,17 @@ __global__ __launch_bounds__(64 * waves_per_block<true>()) void pt_render_env_ke
 
 // WAVES per SIMD: 5 (96 VGPRs) or 6 (80 VGPRs, 29 SGPRs spilled to VGPR lanes); which one is faster
 // depends on the launch geometry (pt_capi.cpp launch(): timed on a geometry's first launches)
-template <int LAYOUT, bool COUNT, int WAVES>
+template <int LAYOUT, bool COUNT, int WAVES, bool PRESENT = false>
 __global__ __launch_bounds__(64 * waves_per_block<false>()) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void
 pt_render_ct_kernel(PtJob job)
 {
-    render_body_ct<LAYOUT, false, COUNT>(job);
+    render_body_ct<LAYOUT, false, COUNT, PRESENT>(job);
 }
 
-template <int LAYOUT, bool COUNT>
+template <int LAYOUT, bool COUNT, bool PRESENT = false>
 __global__ __launch_bounds__(64 * waves_per_block<true>()) __attribute__((amdgpu_waves_per_eu(5, 5))) void pt_render_ct_env_kernel(PtJob job)
 {
-    render_body_ct<LAYOUT, true, COUNT>(job);
+    render_body_ct<LAYOUT, true, COUNT, PRESENT>(job);
 }
 
 template <int LAYOUT, bool ENV, bool COUNT, bool MULTI, bool RING>
@@ -1761,32 +1779,60 @@ constexpr int kRingMinFrames = PT_RING_MIN;
 
 // One-chunk ambient launches on the continuous-tiles pool (render_body_ct) when the caller provides
 // its slots for the whole grid; false: not launched (render_body then).
-template <int LAYOUT, bool ENV, bool COUNT, bool WIDE>
+template <int LAYOUT, bool ENV, bool COUNT, bool WIDE, bool PRESENT = false>
 constexpr auto ct_kernel_of()
 {
-    if constexpr (ENV) return pt_render_ct_env_kernel<LAYOUT, COUNT>;
-    else return pt_render_ct_kernel<LAYOUT, COUNT, WIDE ? 6 : 5>;
+    if constexpr (ENV) return pt_render_ct_env_kernel<LAYOUT, COUNT, PRESENT>;
+    else return pt_render_ct_kernel<LAYOUT, COUNT, WIDE ? 6 : 5, PRESENT>;
 }
 
+// *presented: the kernel wrote job.pix_out (the presenting instances: row layouts, uncounted launches,
+// 5 waves per SIMD)
 template <int LAYOUT, bool ENV, bool COUNT>
-bool launch_ct(const PtJob& job, hipStream_t st, unsigned tiles)
+bool launch_ct(const PtJob& job, hipStream_t st, unsigned tiles, bool* presented)
 {
     constexpr int wpb = waves_per_block<ENV>();
+    *presented = false;
     auto k = job.ct_wide ? ct_kernel_of<LAYOUT, ENV, COUNT, true>() : ct_kernel_of<LAYOUT, ENV, COUNT, false>();
+    bool pres = false;
+    if constexpr (!COUNT && LAYOUT != PT_LAYOUT_TILED_PLANAR8) {
+        if (job.pix_out) {
+            k = ct_kernel_of<LAYOUT, ENV, false, false, true>();
+            pres = true;
+        }
+    }
     const unsigned blocks = (unsigned)std::min<long>(pt_resident_blocks(k, 64 * wpb), (tiles + wpb - 1) / wpb);
     if (!job.ct_slots || (uint64_t)blocks * wpb > job.ct_waves) return false;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
+    *presented = pres;
     return true;
 }
+
+template <int LAYOUT, bool ENV>
+hipError_t launch_pools(const PtJob& job, hipStream_t st, bool count, unsigned tiles);
 
 template <int LAYOUT, bool ENV>
 hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
 {
     const unsigned tiles = (unsigned)((job.ncols + 7) / 8) * (unsigned)((job.nrows + 7) / 8);
+    // the continuous-tiles pool when its slots are provided (its presenting instances write
+    // job.pix_out themselves)
+    bool presented = false;
+    hipError_t e;
+    if (count ? launch_ct<LAYOUT, ENV, true>(job, st, tiles, &presented) : launch_ct<LAYOUT, ENV, false>(job, st, tiles, &presented))
+        e = hipGetLastError();
+    else
+        e = launch_pools<LAYOUT, ENV>(job, st, count, tiles);
+    if (e != hipSuccess || !job.pix_out || presented) return e;
+    // the other pools do not present: the standalone output pass over the job's rows
+    PtToneJob tj{job.buf, job.ncols, job.nrows, LAYOUT, 0, 0, job.pix_out, job.pix_xrgb ? PT_PIXEL_XRGB8 : PT_PIXEL_RGBA8, 1, 1};
+    return pt_launch_tonemap(tj, st);
+}
+
+template <int LAYOUT, bool ENV>
+hipError_t launch_pools(const PtJob& job, hipStream_t st, bool count, unsigned tiles)
+{
     const bool multi = job.nframes > kChunk;
-    // the continuous-tiles pool when its slots are provided
-    if (count ? launch_ct<LAYOUT, ENV, true>(job, st, tiles) : launch_ct<LAYOUT, ENV, false>(job, st, tiles))
-        return hipGetLastError();
     const bool ring = !ENV && job.nframes >= kRingMinFrames && job.nframes > kChunk;
     if (count) {
         if (ring) launch_k<LAYOUT, ENV, true, true, !ENV>(job, st, tiles);
@@ -1995,7 +2041,13 @@ uint32_t pt_ct_resident_waves()
 
 hipError_t pt_launch_render(const PtJob& job_in, hipStream_t st, bool count)
 {
-    if (job_in.ncols <= 0 || job_in.nrows <= 0 || job_in.nframes <= 0) return hipSuccess;
+    if (job_in.ncols <= 0 || job_in.nrows <= 0) return hipSuccess;
+    if (job_in.nframes <= 0) {   // nothing to render; a presenting job still converts the accumulator
+        if (!job_in.pix_out) return hipSuccess;
+        const PtToneJob tj{job_in.buf, job_in.ncols, job_in.nrows, job_in.layout, 0, 0, job_in.pix_out,
+                           job_in.pix_xrgb ? PT_PIXEL_XRGB8 : PT_PIXEL_RGBA8, 1, 1};
+        return pt_launch_tonemap(tj, st);
+    }
     if (!job_in.scene || !job_in.buf || !job_in.queue) return hipErrorInvalidValue;
     // mainImage's frame constants (scalar.cpp:338-347): IEEE f32 '/' here (host, -ffp-contract=off)
     // == the kernel's correctly rounded div_x / rcp_rn

@@ -72,6 +72,38 @@ def render_device(buf, width: int, height: int, *, frame_first: int, nframes: in
     N.check(N.load().pt_render_device(ctypes.byref(job), _stream(stream)), "pt_render_device")
 
 
+def render_device_present(buf, pixels, width: int, height: int, *, frame_first: int, nframes: int,
+                          num_bounces: int, row_start: int = 0, row_stride: int = 1, nrows: int | None = None,
+                          layout: int = N.PT_LAYOUT_INTERLEAVED, use_env: bool = False,
+                          pixel_format: int = N.PT_PIXEL_RGBA8, stream=None) -> None:
+    """render_device with the output stage fused into the render (pt_render_device_present): also
+    writes the job's rows as packed 8-bit pixels (nrows x width int32/uint32 device tensor `pixels`,
+    PT_PIXEL_RGBA8 = OutputToFile, PT_PIXEL_XRGB8 = OutputToScreen) -- equal to render_device followed
+    by the standalone output stage on those rows.  Asynchronous on `stream`."""
+    nrows = height if nrows is None else nrows
+    job = _job(buf, width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces, layout, use_env)
+    _check_pixels(pixels, width * nrows, buf)
+    N.check(N.load().pt_render_device_present(ctypes.byref(job), pixels.data_ptr(), pixel_format, _stream(stream)),
+            "pt_render_device_present")
+
+
+def tonemap_device(buf, width: int, nrows: int, pixels, *, layout: int = N.PT_LAYOUT_INTERLEAVED,
+                   pixel_format: int = N.PT_PIXEL_RGBA8, stream=None) -> None:
+    """The standalone output stage (pt_tonemap_device) on an HBM accumulator of nrows x width pixels
+    into `pixels` (nrows x width 32-bit words).  Asynchronous on `stream`."""
+    _check_pixels(pixels, width * nrows, buf)
+    N.check(N.load().pt_tonemap_device(buf.data_ptr(), width, nrows, layout, 0, 0, pixels.data_ptr(), pixel_format,
+                                       _stream(stream)), "pt_tonemap_device")
+
+
+def _check_pixels(pixels, n: int, buf) -> None:
+    import torch
+    if not isinstance(pixels, torch.Tensor) or pixels.device != buf.device:
+        raise N.PtError(N.PT_EINVAL, "render_device_present", "pixels must be a tensor on the buffer's device")
+    if pixels.element_size() != 4 or not pixels.is_contiguous() or pixels.numel() < n:
+        raise N.PtError(N.PT_EINVAL, "render_device_present", f"pixels must hold >= {n} contiguous 32-bit words")
+
+
 def count_device(buf, width: int, height: int, *, frame_first: int, nframes: int, num_bounces: int,
                  row_start: int = 0, row_stride: int = 1, nrows: int | None = None,
                  layout: int = N.PT_LAYOUT_INTERLEAVED, use_env: bool = False, stream=None) -> dict:
@@ -93,21 +125,32 @@ class JobLauncher:
 
     def __init__(self, buf, width: int, height: int, *, nframes: int, num_bounces: int, row_start: int = 0,
                  row_stride: int = 1, nrows: int | None = None, layout: int = N.PT_LAYOUT_INTERLEAVED,
-                 use_env: bool = False, stream=None, v4: bool = False):
+                 use_env: bool = False, stream=None, v4: bool = False, pixels=None,
+                 pixel_format: int = N.PT_PIXEL_RGBA8):
         nrows = height if nrows is None else nrows
         self._buf = buf   # (kept alive with the job that points at it)
         self.job = _job(buf, width, height, row_start, row_stride, nrows, 1, nframes, num_bounces, layout, use_env)
         L = N.load()
-        self._fn = L.pt_v4_render_device if v4 else L.pt_render_device
-        self._what = "pt_v4_render_device" if v4 else "pt_render_device"
         self._ref = ctypes.byref(self.job)
         self._stream = _stream(stream)
+        if pixels is not None:   # the fused output stage (pt_render_device_present)
+            if v4:
+                raise N.PtError(N.PT_EINVAL, "JobLauncher", "pixels: diffuse renderer only")
+            _check_pixels(pixels, width * nrows, buf)
+            self._pixels = pixels
+            fn, args = L.pt_render_device_present, (self._ref, pixels.data_ptr(), pixel_format, self._stream)
+            self._what = "pt_render_device_present"
+        else:
+            fn = L.pt_v4_render_device if v4 else L.pt_render_device
+            args = (self._ref, self._stream)
+            self._what = "pt_v4_render_device" if v4 else "pt_render_device"
+        self._fn, self._args = fn, args
 
     def __call__(self, frame_first: int) -> None:
         if frame_first < 1:
             raise N.PtError(N.PT_EINVAL, self._what, "frame_first must be >= 1")
         self.job.frame_first = frame_first
-        rc = self._fn(self._ref, self._stream)
+        rc = self._fn(*self._args)
         if rc != N.PT_OK:
             N.check(rc, self._what)
 

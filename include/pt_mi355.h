@@ -318,6 +318,14 @@ void pt_free_work_queue(pt_work_queue* q);
 int pt_render_device(const pt_device_job* job, void* hip_stream);      /* async on hip_stream     */
 int pt_count_device(const pt_device_job* job, void* hip_stream, pt_work_counts* out); /* sync;    */
                                   /* renders like pt_render_device AND counts the work it did     */
+/* pt_render_device with the output stage fused into the render (the
+ * per-frame OutputToScreen / OutputToFile of demofox_path_tracing_optimization_v4.cpp :1260-1331 with
+ * the reference's default USE_FAST_APPROXIMATE_ACES_TONEMAP / _GAMMA 1): besides accumulating, every
+ * pixel of the job's rows is converted to its packed 8-bit value (PT_PIXEL_*) in `pixels` (device
+ * memory on the job's device, nrows x width u32, row k = the job's row k) by the render kernel itself,
+ * where the pixel's final accumulator value is -- no second pass over the accumulator.  Equal bit for
+ * bit to pt_render_device followed by pt_tonemap_device on the job's rows.  Async on hip_stream. */
+int pt_render_device_present(const pt_device_job* job, uint32_t* pixels, int32_t format, void* hip_stream);
 
 #ifdef __cplusplus
 }

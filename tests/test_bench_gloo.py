@@ -149,6 +149,65 @@ def test_bench_ranks_agree_on_the_device_warmup():
     assert np.array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
+def _worker_leg(rank, world, port, q):
+    """bench.strong_leg (the configs[4] leg of the default line) on a tiny fixed image."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import torch.distributed as dist
+    import bench
+    from cpuperformanceraytracer_amd.config import Workload
+    from oracle import pyoracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        wl4 = Workload("tiny_c5", 48, 28, 4, 8, scaling="strong")
+
+        def render_fn(buf, W, H, f, n, rs, st, nr):
+            pyoracle.render(W, H, frame_first=f, nframes=n, num_bounces=8, row_start=rs, row_stride=st, nrows=nr,
+                            nthreads=2, buf=buf.numpy())
+
+        def count_fn(buf, W, H, f, n, rs, st, nr):
+            render_fn(buf, W, H, f, n, rs, st, nr)
+            _, c = pyoracle.render_counted(W, H, frame_first=f, nframes=n, num_bounces=8, row_start=rs,
+                                           row_stride=st, nrows=nr)
+            return {"segments": c["segments"], "samples": c["samples"], "escaped": c["escaped"],
+                    "lane_slots": c["segments"], "primary": c["samples"]}
+
+        out = bench.strong_leg(wl4, rank, world, bench.HostOps(), render_fn, count_fn, steps=2)
+        if rank == 0:
+            q.put(out)
+        else:
+            assert out is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_configs4_leg_of_the_default_line(world):
+    """The default line's `configs4` object (bench.strong_leg): the fixed image does not grow with N,
+    every step's render and gather are reported apart, and with N > 1 the gathered image passes the
+    bench's row check; N = 1 reports the whole-image render alone."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_leg, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert out["scaling"] == "strong" and out["n_gpus"] == world
+    assert out["config"]["image"] == [48, 28] and out["steps"] == 2
+    assert out["value"] > 0 and out["render_ms_per_step"] > 0 and "gather_ms" in out
+    if world > 1:
+        assert out["verified"]["bit_exact"]
+    else:
+        assert out["gather_ms"] == 0.0
+
+
 # ---- `python bench.py --gpus N` without a launcher: bench.spawn_ranks starts the N ranks itself ----
 def test_spawn_ranks_runs_the_n_rank_path(capfd):
     """The driver's plain invocation with N > 1 (no torch.distributed.run): spawn_ranks gives each

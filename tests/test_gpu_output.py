@@ -92,3 +92,71 @@ def test_tonemap_errors():
     with pytest.raises(N.PtError):
         pt.tonemap(np.zeros((8, 16, 3), np.float32), 16, 8, layout=N.PT_LAYOUT_TILED_PLANAR8, tile_width=12,
                    tile_height=8)
+
+
+# ---- the output stage fused into the render (pt_render_device_present) ----
+def _present_series(W, H, B, S, launches, fmt, *, use_env=False, pool_env=None, **rows):
+    """`launches` fused launches of S frames (frames 1 .. launches*S); returns (accumulator, pixels)."""
+    import torch
+    from cpuperformanceraytracer_amd.device import JobLauncher
+    nrows = rows.get("nrows", H)
+    buf = torch.zeros(nrows * W * 3, dtype=torch.float32, device="cuda:0")
+    pix = torch.zeros(nrows * W, dtype=torch.int32, device="cuda:0")
+    launch = JobLauncher(buf, W, H, nframes=S, num_bounces=B, use_env=use_env, pixels=pix, pixel_format=fmt,
+                         **rows)
+    for k in range(launches):
+        launch(1 + k * S)
+    torch.cuda.synchronize()
+    return buf.cpu().numpy().reshape(nrows, W, 3), pix.cpu().numpy().view(np.uint32).reshape(nrows, W)
+
+
+@pytest.mark.parametrize("fmt", [N.PT_PIXEL_RGBA8, N.PT_PIXEL_XRGB8])
+def test_fused_present_c2_matches_oracle(fmt):
+    """configs[1] (1920x1080, 8 spp, 8 bounces) with the output stage fused into the continuous-tiles
+    kernel: after 3 fused launches (the 2nd and 3rd scheduled, with split tiles) every pixel equals the
+    standalone pass over the same accumulator, and rows 0::54 equal the oracle (render, then
+    OutputToFile / OutputToScreen of v4 :1260-1331) bit for bit."""
+    import torch
+    pt.init(num_bounces=8)
+    W, H, B, S = 1920, 1080, 8, 8
+    acc, pix = _present_series(W, H, B, S, 3, fmt)
+    from cpuperformanceraytracer_amd.device import tonemap_device
+    sep = torch.zeros(W * H, dtype=torch.int32, device="cuda:0")
+    dbuf = torch.from_numpy(acc.reshape(-1).copy()).to("cuda:0")
+    tonemap_device(dbuf, W, H, sep, pixel_format=fmt)
+    torch.cuda.synchronize()
+    assert np.array_equal(pix, sep.cpu().numpy().view(np.uint32).reshape(H, W))
+    ref = pyoracle.render(W, H, nframes=3 * S, num_bounces=B, row_start=0, row_stride=54, nrows=20)
+    assert np.array_equal(acc[0::54].view(np.uint32), ref.view(np.uint32))
+    assert np.array_equal(pix[0::54], pyoracle.tonemap(ref, fmt))
+
+
+def test_fused_present_env_shard_and_fallback_pools(monkeypatch):
+    """The env kernel (configs[3] miss term) and a row shard present in the fused kernel; with
+    PT_MI355_NO_CT=1 (the per-tile / ring pools, which do not present) the standalone pass runs after
+    the launch -- the same pixels either way, equal to the oracle's."""
+    import torch
+    from cpuperformanceraytracer_amd.device import set_env_map
+    W, H, B = 256, 144, 8
+    rng = np.random.default_rng(21)
+    env = (rng.random((32, 64, 3), dtype=np.float32) * 3.0 + 0.01).astype(np.float32)
+    rows = dict(row_start=1, row_stride=3, nrows=48)
+    ref = pyoracle.render(W, H, nframes=2 * 16, num_bounces=B, env=env, **rows)
+    for no_ct in ("0", "1"):
+        monkeypatch.setenv("PT_MI355_NO_CT", no_ct)
+        pt.init(num_bounces=B)
+        set_env_map(env, 0, B)
+        acc, pix = _present_series(W, H, B, 16, 2, N.PT_PIXEL_RGBA8, use_env=True, **rows)
+        assert np.array_equal(acc.view(np.uint32), ref.view(np.uint32)), no_ct
+        assert np.array_equal(pix, pyoracle.tonemap(ref, N.PT_PIXEL_RGBA8)), no_ct
+        pt.shutdown()
+    # 0 frames: nothing rendered, the accumulator is still converted
+    monkeypatch.setenv("PT_MI355_NO_CT", "0")
+    pt.init(num_bounces=B)
+    from cpuperformanceraytracer_amd.device import render_device_present
+    buf = torch.from_numpy(ref.reshape(-1).copy()).to("cuda:0")
+    pix = torch.zeros(W * 48, dtype=torch.int32, device="cuda:0")
+    render_device_present(buf, pix, W, H, frame_first=1, nframes=0, num_bounces=B, **rows)
+    torch.cuda.synchronize()
+    assert np.array_equal(pix.cpu().numpy().view(np.uint32).reshape(48, W), pyoracle.tonemap(ref, N.PT_PIXEL_RGBA8))
+    pt.shutdown()
