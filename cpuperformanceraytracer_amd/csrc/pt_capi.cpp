@@ -156,7 +156,8 @@ struct State {
     uint32_t ring_guard_cap = ~0u;
     int32_t v4_ct_force = 0;   // PT_MI355_V4_CT=1 (read by pt_init): PtV4Job::ct_force (tests)
     uint32_t ct_back_pct = 20;   // PT_MI355_BACK (read by pt_init): PtJob::ct_back_pct (0: none)
-    uint32_t ct_waves = 5;       // PT_MI355_CT_WAVES (read by pt_init): 5 or 6; 0: timed per geometry
+    uint32_t ct_waves = 0;       // PT_MI355_CT_WAVES (read by pt_init): 5 or 6 waves per SIMD; 0 (default):
+                                 // the faster of the two, timed on each geometry's first launches
     // test hook: PT_MI355_CT_WAVES_SEQ (read by pt_init), a string of '5' / '6' cycled over the
     // diffuse continuous-tiles launches -- forced changes of the grid between the launches of one
     // accumulation (tests/test_gpu_configs.py); empty: off
@@ -664,10 +665,11 @@ int use_ct_slots(Dev& dv, const LaunchSched& ls, hipStream_t st, float** slots, 
     return PT_OK;
 }
 
-// PtJob::ct_wide of a diffuse continuous-tiles launch: PT_MI355_CT_WAVES (default 5, or 6), or with
-// PT_MI355_CT_WAVES=0 the faster of the two on the geometry's first scheduled launches (experimental:
-// a 2-process rehearsal on one GPU produced a mismatching row with it); *tev: the event
-// pair to record around this launch while they are timed
+// PtJob::ct_wide of a diffuse continuous-tiles launch: 5 or 6 waves per SIMD -- PT_MI355_CT_WAVES=5|6,
+// or by default (0) the faster of the two, timed on the geometry's first kTuneLaunches scheduled
+// launches (per stream: a geometry's Sched).  The grid may change between the launches of one
+// accumulation; no pixel depends on it (tests/test_gpu_regime.py forces every change).
+// *tev: the event pair to record around this launch while they are timed
 int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
 {
     *tev = nullptr;
@@ -684,14 +686,18 @@ int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
         hipEvent_t* ev = &s->tune_ev[2 * s->tuned];
         for (int i = 0; i < 2; ++i)
             if (!ev[i]) HIP_TRY(hipEventCreate(&ev[i]));
-        j.ct_wide = s->tuned++ & 1u;
+        // ABBA order (5 6 6 5 5 6 6 5): the launches of a fresh process run while the clocks ramp up
+        // (DESIGN.md 4), and plain alternation timed the 6-wave arm always second, i.e. faster --
+        // it then picked 6 waves for 4K 8 spp (0.852 vs 0.829 ms at 5, profiles/r05/r05b_ab.jsonl)
+        const uint32_t t = s->tuned++;
+        j.ct_wide = (t ^ (t >> 1)) & 1u;
         *tev = ev;
     } else if (hipEventQuery(s->tune_ev[2 * kTuneLaunches - 1]) == hipSuccess) {
         float t[2] = {0.f, 0.f};
         for (uint32_t i = 0; i < kTuneLaunches; ++i) {
             float ms = 0.f;
             HIP_TRY(hipEventElapsedTime(&ms, s->tune_ev[2 * i], s->tune_ev[2 * i + 1]));
-            t[i & 1] += ms;
+            t[(i ^ (i >> 1)) & 1u] += ms;
         }
         s->wide = t[1] < t[0] ? 1 : 0;
         j.ct_wide = (uint32_t)s->wide;
@@ -1380,7 +1386,7 @@ int pt_init(const pt_config* cfg)
     g.v4_ct_force = getenv("PT_MI355_V4_CT") && !strcmp(getenv("PT_MI355_V4_CT"), "1");
     g.ct_back_pct = 20;
     if (const char* bk = getenv("PT_MI355_BACK")) g.ct_back_pct = (uint32_t)strtoul(bk, nullptr, 10);
-    g.ct_waves = 5;
+    g.ct_waves = 0;
     if (const char* cw = getenv("PT_MI355_CT_WAVES")) g.ct_waves = (uint32_t)strtoul(cw, nullptr, 10);
     g.ct_seq_len = g.ct_seq_pos = 0;
     if (const char* sq = getenv("PT_MI355_CT_WAVES_SEQ")) {
