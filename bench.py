@@ -524,11 +524,12 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
         flops_launch_ref = flops_launch
         flop_model = (f"segments x V4_F_SEGMENT + samples x V4_F_SAMPLE; F = {RL.V4_F_SEGMENT}/{RL.V4_F_SAMPLE} "
                       "(roofline.py, counted by oracle/pt_oracle_v4.c)")
-        # pt_v4.hip launch_t: the continuous-tiles kernel for launches of >= 12 8-frame chunks per
-        # resident wave (5120 on MI355X), the per-tile pool kernel else (this label mirrors that rule)
+        # pt_v4.hip launch_t: the continuous-tiles kernel for launches of >= 4 8-frame chunks per
+        # resident wave (6144 at its 6 waves per SIMD on MI355X), the per-tile pool kernel else (this
+        # label mirrors that rule)
         tiles = ((Wg + 7) // 8) * (((Hg + world - 1) // world + 7) // 8)
         v4_ct = os.environ.get("PT_MI355_NO_CT") != "1" and S >= 8 and (
-            os.environ.get("PT_MI355_V4_CT") == "1" or S * tiles >= 12 * 8 * 5120)
+            os.environ.get("PT_MI355_V4_CT") == "1" or S * tiles >= 4 * 8 * 6144)
         kernel_name = "pt_v4_ct_kernel<EQUIRECT, INTERLEAVED>" if v4_ct else "pt_v4_kernel<EQUIRECT, INTERLEAVED>"
     else:
         env_esc = escaped if wl.env else 0

@@ -740,10 +740,18 @@ __device__ __forceinline__ void v4_segment(const PtV4Job& job, const PtV4Scene& 
 
 #ifdef PT_V4_WAVES   // A/B builds: force the occupancy (waves per SIMD)
 #define PT_V4_OCC __attribute__((amdgpu_waves_per_eu(PT_V4_WAVES, PT_V4_WAVES)))
+#define PT_V4_CT_OCC PT_V4_OCC
 #else
 // render instances: at least 5 waves per SIMD (<= 96 VGPRs; the exact-exp instance needs 97
 // otherwise and compiles spill-free at 96); the diagnostic COUNT instances are left unconstrained
 #define PT_V4_OCC __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : 5)))
+// the continuous-tiles kernel at 6 waves per SIMD (80 VGPRs -- its pool loop needs no more, the one
+// spilled register is in the event code; 16 KiB of LDS per block: 6 blocks per CU).  Against 5
+// waves (interleaved A/B, profiles/r05/r05g_v4_ab.jsonl): 1080p 8 spp 0.3591 vs 0.3652 ms, 1080p
+// 32 spp 1.247 vs 1.261, 4K 8 spp 1.272 vs 1.296 -- and ahead of the per-tile kernel (0.3602,
+// 1.260, 1.298) at all three.  The instance with the reference's default flags (DFL) only: the
+// others spill in their pool loops at 80 VGPRs and keep 5 waves.
+#define PT_V4_CT_OCC __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : (DFL ? 6 : 5))))
 #endif
 // FEXP: USE_FAST_APPROXIMATE_EXP as a compile-time switch (1 fast, 0 exact) for the render
 // instances -- the exact expf's registers in the Beer branch would otherwise raise the kernel from
@@ -1013,7 +1021,7 @@ enum : int {   // per-wave LDS words of the events (pt_kernel.hip kWs*)
 };
 
 template <int ENV, int LAYOUT, bool COUNT, bool DEF, int FEXP, bool DFL = false>
-__global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_ct_kernel(PtV4Job job, PtV4Scene sc)
+__global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4Job job, PtV4Scene sc)
 {
     __shared__ PtV4Mat s_mat[PT_V4_MAX_OBJECTS];
     __shared__ float4 s_sc[DEF ? pt_v4_default::kSpheres : 1];   // default scene: sphere centre, radius
@@ -1422,16 +1430,17 @@ hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool 
     const int tiles = ((j.ncols + 7) / 8) * ((j.nrows + 7) / 8);
     const dim3 block(64 * kWaves);
     // persistent grid: the resident blocks, at most one tile per wave.  The continuous-tiles kernel
-    // when the caller provides its slots for the whole grid and the launch holds >= 12 full chunks
-    // (8 frames x tile) per wave, else the per-tile pool kernel.  Measured (scripts/gpu_v4_ab.sh, CT
-    // vs per-tile): 1080p 32 spp 1.257 vs 1.320 ms (51 chunks per wave), 4K 8 spp 1.308 vs 1.328 (25),
+    // when the caller provides its slots for the whole grid and the launch holds >= 4 full chunks
+    // (8 frames x tile) per wave, else the per-tile pool kernel.  Measured (round 4, 5-wave CT vs
+    // per-tile): 1080p 32 spp 1.257 vs 1.320 ms (51 chunks per wave), 4K 8 spp 1.308 vs 1.328 (25),
     // 1080p 8 spp 0.3602 vs 0.3589 (6), 1 spp 0.133 vs 0.115 (one item per pixel and chunk: the
-    // chunk events, claim and fold, dominate).
+    // chunk events, claim and fold, dominate); round 5, the 6-wave CT kernel: 1080p 8 spp (5.3 chunks
+    // per wave) 0.3591 vs 0.3602.
     const auto go = [&](auto kern, auto ct_kern) {
         const long ct_blocks = std::min<long>(pt_resident_blocks(ct_kern, 64 * kWaves), (tiles + kWaves - 1) / kWaves);
         const uint64_t ct_waves = (uint64_t)ct_blocks * kWaves;
         if (j.ct_slots && ct_waves <= j.ct_waves && j.nframes >= kChunk &&
-            (j.ct_force || (uint64_t)j.nframes * (uint64_t)tiles >= 12ull * kChunk * ct_waves)) {
+            (j.ct_force || (uint64_t)j.nframes * (uint64_t)tiles >= 4ull * kChunk * ct_waves)) {
             hipLaunchKernelGGL(ct_kern, dim3((unsigned)ct_blocks), block, 0, st, j, sc);
             return;
         }
