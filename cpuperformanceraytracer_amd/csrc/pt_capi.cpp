@@ -60,14 +60,14 @@ struct Sched {
     bool built = false;           // order/units hold a schedule
     unsigned long long launches = 0;
     unsigned long long last_use = 0;
-    // occupancy of the diffuse continuous-tiles kernel (PtJob::ct_wide, PT_MI355_CT_WAVES=0 only): the
-    // first kTuneLaunches scheduled launches alternate 5 and 6 waves per SIMD between event pairs, the
-    // faster total is kept (A/B: 1080p 8 spp 0.245 vs 0.250 ms at 6, 720p 8 spp 0.147 vs 0.138 at 5)
-    hipEvent_t tune_ev[2 * 8] = {};
+    // launch variant of the diffuse continuous-tiles kernel (PT_MI355_CT_WAVES=0, the default): the
+    // first scheduled launches time the arms (ct_occupancy) between event pairs, the fastest is kept
+    hipEvent_t tune_ev[2 * 18] = {};
     uint32_t tuned = 0;           // timed launches enqueued
-    int8_t wide = -1;             // the pick (-1: not yet)
+    uint32_t narms = 0;           // arms timed (2 or 3; 0: not started)
+    int8_t wide = -1;             // the pick: arm index (-1: not yet)
 };
-constexpr uint32_t kTuneLaunches = 8;
+constexpr uint32_t kTuneRounds = 3;   // rounds of the palindromic arm order timed; the first is discarded
 constexpr int kSchedSlots = 16;
 constexpr int kBands = 4;   // PT_FLAG_PIN_HOST: row bands of a pipelined frame
 constexpr uint32_t kSchedMinTiles = 512;   // smaller jobs (e.g. one RenderTile) are not scheduled
@@ -156,6 +156,7 @@ struct State {
     uint32_t ring_guard_cap = ~0u;
     int32_t v4_ct_force = 0;   // PT_MI355_V4_CT=1 (read by pt_init): PtV4Job::ct_force (tests)
     uint32_t ct_back_pct = 20;   // PT_MI355_BACK (read by pt_init): PtJob::ct_back_pct (0: none)
+    bool back_set = false;       // PT_MI355_BACK given: the occupancy timing keeps it
     uint32_t ct_waves = 0;       // PT_MI355_CT_WAVES (read by pt_init): 5 or 6 waves per SIMD; 0 (default):
                                  // the faster of the two, timed on each geometry's first launches
     // test hook: PT_MI355_CT_WAVES_SEQ (read by pt_init), a string of '5' / '6' cycled over the
@@ -665,11 +666,23 @@ int use_ct_slots(Dev& dv, const LaunchSched& ls, hipStream_t st, float** slots, 
     return PT_OK;
 }
 
-// PtJob::ct_wide of a diffuse continuous-tiles launch: 5 or 6 waves per SIMD -- PT_MI355_CT_WAVES=5|6,
-// or by default (0) the faster of the two, timed on the geometry's first kTuneLaunches scheduled
-// launches (per stream: a geometry's Sched).  The grid may change between the launches of one
-// accumulation; no pixel depends on it (tests/test_gpu_regime.py forces every change).
-// *tev: the event pair to record around this launch while they are timed
+// The launch variant of a diffuse continuous-tiles launch: PtJob::ct_wide (5 or 6 waves per SIMD) and
+// PtJob::ct_back_pct.  PT_MI355_CT_WAVES=5|6 fixes the occupancy; by default (0) the geometry's first
+// scheduled launches time the ARMS and the fastest is kept (per stream: a geometry's Sched):
+//   arm 0: 5 waves, arm 1: 6 waves -- each with the default back-claim share (20 %) -- and, for
+//   launches that take back claims (<= 16 frames) unless PT_MI355_BACK is given, arm 2: 6 waves with
+//   kBackWide % of the grid claiming from the back.  Measured (profiles/r05/r05i_back_sweep_ab.jsonl,
+//   r05h_back_ab.jsonl): at 6 waves 45 % gave 1080p 8 spp 0.2392 vs 0.2440 ms and 4K 8 spp 0.8015 vs
+//   0.8395 (55-90 %: 0.249 / 0.80), but 720p 0.1490 vs 0.1462 and, at 5 waves, 1080p 0.2526 vs 0.2488 --
+//   so it is one more timed arm, not a new default.
+// The arms are timed in a palindromic order (ABBA, ABCCBA), three rounds of which the first is not
+// counted: the clocks of a fresh process ramp up over its first launches -- a plain
+// alternation favoured the later arm, and one round of ABCCBA still picked 5 waves for 4K 8 spp in
+// one of two runs (0.8242 vs 0.8023 ms, profiles/r05/r05j_timing3_ab.jsonl).  Until the pick: 6
+// waves for launches of several chunks (ahead at 16 and 64 spp), 5 for one-chunk launches.  No pixel
+// depends on the variant (tests/test_gpu_regime.py forces grid changes).
+// *tev: the event pair to record around this launch while it is timed.
+constexpr uint32_t kBackWide = 45;
 int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
 {
     *tev = nullptr;
@@ -680,29 +693,37 @@ int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
     }
     Sched* s = ls.sched;
     if (g.ct_waves || !j.ct_slots || j.env || !s) return PT_OK;
+    const auto apply = [&](int arm) {
+        j.ct_wide = arm != 0 ? 1u : 0u;
+        if (arm == 2 && j.ct_back_pct != 0) j.ct_back_pct = kBackWide;   // (launches that take back claims)
+    };
+    if (!s->narms) s->narms = (j.ct_back_pct != 0 && !g.back_set) ? 3u : 2u;
+    const uint32_t per_round = s->narms == 3 ? 6u : 4u, nt = kTuneRounds * per_round;
+    static constexpr int kOrder3[6] = {0, 1, 2, 2, 1, 0};
+    const auto arm_of = [&](uint32_t t) { return s->narms == 3 ? kOrder3[t % 6] : (int)((t ^ (t >> 1)) & 1u); };
     if (s->wide >= 0) {
-        j.ct_wide = (uint32_t)s->wide;
-    } else if (s->tuned < kTuneLaunches) {
+        apply(s->wide);
+    } else if (s->tuned < nt) {
         hipEvent_t* ev = &s->tune_ev[2 * s->tuned];
         for (int i = 0; i < 2; ++i)
             if (!ev[i]) HIP_TRY(hipEventCreate(&ev[i]));
-        // ABBA order (5 6 6 5 5 6 6 5): the launches of a fresh process run while the clocks ramp up
-        // (DESIGN.md 4), and plain alternation timed the 6-wave arm always second, i.e. faster --
-        // it then picked 6 waves for 4K 8 spp (0.852 vs 0.829 ms at 5, profiles/r05/r05b_ab.jsonl)
-        const uint32_t t = s->tuned++;
-        j.ct_wide = (t ^ (t >> 1)) & 1u;
+        apply(arm_of(s->tuned++));
         *tev = ev;
-    } else if (hipEventQuery(s->tune_ev[2 * kTuneLaunches - 1]) == hipSuccess) {
-        float t[2] = {0.f, 0.f};
-        for (uint32_t i = 0; i < kTuneLaunches; ++i) {
+    } else if (hipEventQuery(s->tune_ev[2 * nt - 1]) == hipSuccess) {
+        float t[3] = {0.f, 0.f, 0.f};
+        for (uint32_t i = per_round; i < nt; ++i) {
             float ms = 0.f;
             HIP_TRY(hipEventElapsedTime(&ms, s->tune_ev[2 * i], s->tune_ev[2 * i + 1]));
-            t[(i ^ (i >> 1)) & 1u] += ms;
+            t[arm_of(i)] += ms;
         }
-        s->wide = t[1] < t[0] ? 1 : 0;
-        j.ct_wide = (uint32_t)s->wide;
+        int best = 0;
+        for (int a = 1; a < (int)s->narms; ++a)
+            if (t[a] < t[best]) best = a;
+        s->wide = (int8_t)best;
+        apply(best);
     } else {
         (void)hipGetLastError();   // (hipErrorNotReady: the timed launches are still running)
+        apply(j.nframes > 8 ? 1 : 0);
     }
     return PT_OK;
 }
@@ -1385,7 +1406,8 @@ int pt_init(const pt_config* cfg)
     g.no_ct = getenv("PT_MI355_NO_CT") && !strcmp(getenv("PT_MI355_NO_CT"), "1");
     g.v4_ct_force = getenv("PT_MI355_V4_CT") && !strcmp(getenv("PT_MI355_V4_CT"), "1");
     g.ct_back_pct = 20;
-    if (const char* bk = getenv("PT_MI355_BACK")) g.ct_back_pct = (uint32_t)strtoul(bk, nullptr, 10);
+    g.back_set = false;
+    if (const char* bk = getenv("PT_MI355_BACK")) g.ct_back_pct = (uint32_t)strtoul(bk, nullptr, 10), g.back_set = true;
     g.ct_waves = 0;
     if (const char* cw = getenv("PT_MI355_CT_WAVES")) g.ct_waves = (uint32_t)strtoul(cw, nullptr, 10);
     g.ct_seq_len = g.ct_seq_pos = 0;

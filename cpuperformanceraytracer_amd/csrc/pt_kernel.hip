@@ -1206,6 +1206,16 @@ enum : int {
     kWsTileSeg, kWsSegA, kWsSegD, kWsFlags, kWsChunks, kWsWords
 };
 
+// The env CT kernel runs 6 waves per SIMD: its pool loop fits 80 VGPRs (the spills of that build
+// are in the event code), and a block's LDS fits 6 per CU with a 96-entry miss queue per wave
+// (128 entries: 30 KiB per block, 5 per CU).  PT_ENV_WAVES / PT_ENV_Q: A/B builds.
+#ifndef PT_ENV_WAVES
+#define PT_ENV_WAVES 6
+#endif
+#ifndef PT_ENV_Q
+#define PT_ENV_Q 96
+#endif
+static_assert(PT_ENV_Q >= 64 && PT_ENV_Q <= 128, "the env miss queue holds 64 .. 128 entries per wave");
 // ENV (config 4, the env-map miss term): a missed segment's item is queued with its direction and
 // radiance so far (s_envq, 32 B), and the queue is drained 64 at a time by the whole wave -- the
 // coherent texel gathers of render_body's env kernel; a drain writes the items' radiance + texel
@@ -1230,7 +1240,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     __shared__ uint32_t s_seed[kWavesPerBlock][64];   // the item pixels' seed terms (x, y) of :332
     __shared__ uint32_t s_ws[kWavesPerBlock][kWsWords];   // the events' wave-uniform state (below)
     __shared__ uint32_t s_tq[kWavesPerBlock][PtTileQueue<kWavesPerBlock>::kWords];   // the wave's tile queue
-    constexpr int kQ = ENV ? 128 : 1;   // queued misses: direction + slot, radiance so far
+    constexpr int kQ = ENV ? PT_ENV_Q : 1;   // queued misses: direction + slot, radiance so far
     __shared__ float4 s_envq[ENV ? kWavesPerBlock : 1][kQ][2];
     {
         const int t = threadIdx.x;
@@ -1653,12 +1663,20 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             }
             if (ENV) {
                 const uint64_t qm = pt_ballot(queued);
+                const int nq = __popcll(qm);
+                // room for this iteration's misses (<= 64): the queue holds kQ; after the drain below
+                // qn < 64, so with kQ < 128 a queue of more than kQ - 64 entries is evaluated first
+                // (all of them: < 64 lanes busy, rare -- most iterations queue a few misses)
+                if (kQ < 128 && qn + nq > kQ) {
+                    drain(0, qn);
+                    qn = 0;
+                }
                 if (queued) {
                     const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
                     s_envq[ENV ? wv : 0][qn + r][0] = make_float4(D.x, D.y, D.z, __builtin_bit_cast(float, it_addr));
                     s_envq[ENV ? wv : 0][qn + r][1] = make_float4(ret.x, ret.y, ret.z, 0.0f);
                 }
-                qn += __popcll(qm);
+                qn += nq;
                 if (qn >= 64) {   // a full wave of misses: evaluate the last 64
                     qn -= 64;
                     drain(qn, 64);
@@ -1746,7 +1764,7 @@ pt_render_ct_kernel(PtJob job)
 }
 
 template <int LAYOUT, bool COUNT, bool PRESENT = false>
-__global__ __launch_bounds__(64 * waves_per_block<true>()) __attribute__((amdgpu_waves_per_eu(5, 5))) void pt_render_ct_env_kernel(PtJob job)
+__global__ __launch_bounds__(64 * waves_per_block<true>()) __attribute__((amdgpu_waves_per_eu(PT_ENV_WAVES, PT_ENV_WAVES))) void pt_render_ct_env_kernel(PtJob job)
 {
     render_body_ct<LAYOUT, true, COUNT, PRESENT>(job);
 }

@@ -11,7 +11,8 @@ STEPS=${STEPS:-10}
 OUT=$PWD/gpurun_out/prof/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-CMD=(python3 "$PWD/bench.py" --workload "$WORKLOAD" --steps "$STEPS" --warmup 2 --no-cpu-baseline)
+# (--no-configs4: the default line's configs[4] leg would add 8K launches of the same kernel instance)
+CMD=(python3 "$PWD/bench.py" --workload "$WORKLOAD" --steps "$STEPS" --warmup 2 --no-cpu-baseline --no-configs4)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- "${CMD[@]}" > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- "${CMD[@]}" > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- "${CMD[@]}" > "$OUT/write.log" 2>&1

@@ -38,7 +38,9 @@ if os.environ.get("PT_PROFILE_PER_TILE") == "1":
 else:
     KERNEL = "pt_render_ct_env_kernel<0, false" if ENV else "pt_render_ct_kernel<0, false"
 if workload.startswith("v4"):
-    KERNEL = "pt_v4_kernel<1, 0, false, true,"   # <EQUIRECT, INTERLEAVED, COUNT = false, default-scene literals, FEXP>
+    # <EQUIRECT, INTERLEAVED, COUNT = false, default-scene literals, FEXP>: the continuous-tiles kernel at
+    # the bench's 1080p 8 spp since round 5 (launches of >= 4 chunks per wave), the per-tile one else
+    KERNEL = os.environ.get("PT_PROFILE_V4_KERNEL", "pt_v4_ct_kernel<1, 0, false, true,")
 SUMMARY = "pmc_summary.json" if workload == "c2_1080p" else f"pmc_summary_{workload}.json"
 
 stats = glob.glob(str(src / "trace" / "**" / "*kernel_stats.csv"), recursive=True)
