@@ -1804,8 +1804,7 @@ constexpr auto ct_kernel_of()
     else return pt_render_ct_kernel<LAYOUT, COUNT, WIDE ? 6 : 5, PRESENT>;
 }
 
-// *presented: the kernel wrote job.pix_out (the presenting instances: row layouts, uncounted launches,
-// 5 waves per SIMD)
+// *presented: the kernel wrote job.pix_out (the presenting instances: row layouts, uncounted launches)
 template <int LAYOUT, bool ENV, bool COUNT>
 bool launch_ct(const PtJob& job, hipStream_t st, unsigned tiles, bool* presented)
 {
@@ -1815,7 +1814,7 @@ bool launch_ct(const PtJob& job, hipStream_t st, unsigned tiles, bool* presented
     bool pres = false;
     if constexpr (!COUNT && LAYOUT != PT_LAYOUT_TILED_PLANAR8) {
         if (job.pix_out) {
-            k = ct_kernel_of<LAYOUT, ENV, false, false, true>();
+            k = job.ct_wide ? ct_kernel_of<LAYOUT, ENV, false, true, true>() : ct_kernel_of<LAYOUT, ENV, false, false, true>();
             pres = true;
         }
     }
