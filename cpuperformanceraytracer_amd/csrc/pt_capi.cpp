@@ -666,8 +666,8 @@ int use_ct_slots(Dev& dv, const LaunchSched& ls, hipStream_t st, float** slots, 
     return PT_OK;
 }
 
-// The launch variant of a diffuse continuous-tiles launch: PtJob::ct_wide (5 or 6 waves per SIMD) and
-// PtJob::ct_back_pct.  PT_MI355_CT_WAVES=5|6 fixes the occupancy; by default (0) the geometry's first
+// The launch variant of a continuous-tiles launch (diffuse and env kernels): PtJob::ct_wide (5 or 6 waves per SIMD) and
+// PtJob::ct_back_pct.  PT_MI355_CT_WAVES=5|6 fixes the occupancy (and the env share); by default (0) the geometry's first
 // scheduled launches time the ARMS and the fastest is kept (per stream: a geometry's Sched):
 //   arm 0: 5 waves, arm 1: 6 waves -- each with the default back-claim share (20 %) -- and, for
 //   launches that take back claims (<= 16 frames) unless PT_MI355_BACK is given, arm 2: 6 waves with
@@ -675,6 +675,10 @@ int use_ct_slots(Dev& dv, const LaunchSched& ls, hipStream_t st, float** slots, 
 //   r05h_back_ab.jsonl): at 6 waves 45 % gave 1080p 8 spp 0.2392 vs 0.2440 ms and 4K 8 spp 0.8015 vs
 //   0.8395 (55-90 %: 0.249 / 0.80), but 720p 0.1490 vs 0.1462 and, at 5 waves, 1080p 0.2526 vs 0.2488 --
 //   so it is one more timed arm, not a new default.
+// The env kernel has one occupancy (PT_ENV_WAVES); its arms, for launches that take back claims unless
+//   PT_MI355_BACK is given, are the back-claim shares 20 (default), 33 and 45 %: measured
+//   (profiles/r05/r05k_env_back_ab.jsonl) 1080p 8 frames 0.2786 / 0.2809 / 0.2738 ms, 16 frames
+//   0.4821 / 0.4770 / 0.4885 -- the best share depends on the launch, as for the diffuse kernel.
 // The arms are timed in a palindromic order (ABBA, ABCCBA), three rounds of which the first is not
 // counted: the clocks of a fresh process ramp up over its first launches -- a plain
 // alternation favoured the later arm, and one round of ABCCBA still picked 5 waves for 4K 8 spp in
@@ -683,6 +687,7 @@ int use_ct_slots(Dev& dv, const LaunchSched& ls, hipStream_t st, float** slots, 
 // depends on the variant (tests/test_gpu_regime.py forces grid changes).
 // *tev: the event pair to record around this launch while it is timed.
 constexpr uint32_t kBackWide = 45;
+constexpr uint32_t kEnvBack[3] = {0, 33, 45};   // env arms 1, 2 (arm 0: the default share)
 int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
 {
     *tev = nullptr;
@@ -692,12 +697,17 @@ int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
         return PT_OK;
     }
     Sched* s = ls.sched;
-    if (g.ct_waves || !j.ct_slots || j.env || !s) return PT_OK;
+    const bool env_arms = j.env && j.ct_back_pct != 0 && !g.back_set;
+    if (g.ct_waves || !j.ct_slots || !s || (j.env && !env_arms)) return PT_OK;
     const auto apply = [&](int arm) {
+        if (j.env) {   // (one occupancy: the arms are back-claim shares)
+            if (arm) j.ct_back_pct = kEnvBack[arm];
+            return;
+        }
         j.ct_wide = arm != 0 ? 1u : 0u;
         if (arm == 2 && j.ct_back_pct != 0) j.ct_back_pct = kBackWide;   // (launches that take back claims)
     };
-    if (!s->narms) s->narms = (j.ct_back_pct != 0 && !g.back_set) ? 3u : 2u;
+    if (!s->narms) s->narms = (j.env || (j.ct_back_pct != 0 && !g.back_set)) ? 3u : 2u;
     const uint32_t per_round = s->narms == 3 ? 6u : 4u, nt = kTuneRounds * per_round;
     static constexpr int kOrder3[6] = {0, 1, 2, 2, 1, 0};
     const auto arm_of = [&](uint32_t t) { return s->narms == 3 ? kOrder3[t % 6] : (int)((t ^ (t >> 1)) & 1u); };
@@ -723,7 +733,7 @@ int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
         apply(best);
     } else {
         (void)hipGetLastError();   // (hipErrorNotReady: the timed launches are still running)
-        apply(j.nframes > 8 ? 1 : 0);
+        apply(j.env || j.nframes <= 8 ? 0 : 1);
     }
     return PT_OK;
 }

@@ -37,6 +37,11 @@ def pmc(short):
             m = re.match(r"kernel_trace_average_ns\s+(\S+)", line)
             if m:
                 out["avg_ns"] = float(m.group(1))
+            m = re.match(r"kernel_trace_steady_average_ns\s+(\S+)", line)
+            if m:   # the dispatches after the clock ramp (summarize_profile.py, round 5)
+                out["steady_ns"] = float(m.group(1))
+    if "steady_ns" in out:
+        out["avg_ns"] = out["steady_ns"]
     return out
 
 
@@ -68,7 +73,7 @@ def roc(k):
 
 
 rows = [
-    ("kernel time (HIP events bracketing the timed launches, interval / K; rocprofv3 kernel-trace average)",
+    (f"kernel time (HIP events bracketing the timed launches, interval / K; rocprofv3 kernel-trace average{' after the clock ramp' if M['c2'].get('steady_ns') else ''})",
      [f"**{ms('c2'):.4f} ms**{roc('c2')}", f"{ms('c3'):.3f} ms{roc('c3')}", f"{ms('c4'):.4f} ms{roc('c4')}", f"{ms('c5'):.1f} ms"]),
     ("ray-samples/s (BASELINE metric, px·spp·bounces)", [f"**{e(B['c2']['value'])}**"] + [e(B[k]["value"]) for k in ("c3", "c4", "c5")]),
     ("primary samples/s (north-star target ≥ 10⁹)", [e(B[k]["primary_samples_per_s"]) for k in ("c2", "c3", "c4", "c5")]),
@@ -78,8 +83,8 @@ rows = [
     ("reference-equivalent FLOP/s", [f"{B[k]['roofline']['achieved_ref_equivalent']:.1f} TF/s" for k in ("c2", "c3", "c4", "c5")]),
     ("fabric bytes per launch (rocprofv3 FETCH+WRITE: L2 misses and write-backs, Infinity-Cache hits included; with the continuous-tiles slot area, §3c) vs algorithmic",
      [f"{hbm(k):.1f} MB vs {B[k]['roofline']['algorithmic_bytes_per_launch'] / 1e6:.1f} MB" if hbm(k) else "—" for k in ("c2", "c3", "c4", "c5")]),
-    ("VALU wave-instructions per launch (PMC)",
-     [f"{e(M[k]['SQ_INSTS_VALU'])}" + (f" = {M[k]['SQ_INSTS_VALU'] / (M[k]['avg_ns'] * 1024):.2f} per SIMD per ns" if k == "c2" else "")
+    ("VALU / SALU wave-instructions per launch (PMC)",
+     [f"{e(M[k]['SQ_INSTS_VALU'])} / {e(M[k]['SQ_INSTS_SALU'])}" + (f" (VALU {M[k]['SQ_INSTS_VALU'] / (M[k]['avg_ns'] * 1024):.2f} per SIMD per ns)" if k == "c2" else "")
       if "SQ_INSTS_VALU" in M.get(k, {}) else "" for k in ("c2", "c3", "c4", "c5")]),
 ]
 cpu = B["c2"].get("cpu_baseline") or {}
@@ -87,7 +92,8 @@ if cpu:
     rows.append((f"CPU baseline: oracle port, {cpu.get('cores')} threads (the box's cgroup CPU quota), ~{cpu.get('sample', '').split(';')[-1].strip()}",
                  [f"{e(cpu['value'])} ray-samples/s (GPU ×{B['c2']['value'] / cpu['value']:.0f})", "", "", ""]))
 fb = (f"; {', '.join(used_fallback)}: `profiles/{pmc_tag}_*`, kernel unchanged" if used_fallback else "")
-hdr = (f"| quantity (one launch; round 4, bench `profiles/{tag}_bench_*.json`, rocprofv3 `profiles/{tag}_*`{fb}) | c2: 1920×1080, 8 spp, 8 b | "
+rnd = int(re.match(r"r0*(\d+)", tag).group(1)) if re.match(r"r\d+", tag) else "?"
+hdr = (f"| quantity (one launch; round {rnd}, bench `profiles/{tag}_bench_*.json`, rocprofv3 `profiles/{tag}_*`{fb}) | c2: 1920×1080, 8 spp, 8 b | "
        "c3: 3840×2160, 64 spp | c4: 1080p, 16 spp, env | c5: 7680×4320, 256 spp (one GPU, whole image) |\n|---|---|---|---|---|\n")
 design = hdr + "".join(f"| {r} | " + " | ".join(v) + " |\n" for r, v in rows)
 v = B["v4"]
