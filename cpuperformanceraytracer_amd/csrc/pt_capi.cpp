@@ -1209,7 +1209,7 @@ int v4_use_env(PtV4Job& j)
     return PT_OK;
 }
 
-int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count)
+int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count, bool* presented = nullptr)
 {
     LaunchSched ls;
     int rc;
@@ -1227,7 +1227,7 @@ int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count)
     if ((rc = use_ct_slots(dv, ls, st, &j.ct_slots, &j.ct_waves))) return rc;
     j.ct_force = g.v4_ct_force;
     j.ct_back_pct = j.nframes <= 16 ? g.ct_back_pct : 0u;   // (as launch())
-    hipError_t e = pt_launch_v4(j, g.v4scene, st, count);
+    hipError_t e = pt_launch_v4(j, g.v4scene, st, count, presented);
     if (e != hipSuccess) return fail(PT_EHIP, "v4 render launch failed: %s", hipGetErrorString(e));
     return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_v4's early return)
 }
@@ -1976,14 +1976,29 @@ int pt_render_opt_v4(float* buf, int32_t w, int32_t h, int32_t ntx, int32_t nty,
                            &banded)))
         return rc;
     const Geo geo = geo_of(w, h, PT_LAYOUT_TILED_PLANAR8, tw, th);
+    bool presented = false;   // the render launch wrote the screen pixels (fused OutputToScreen)
     if (!banded) {
         if ((rc = stage_in(buf, geo, Region{}))) return rc;
-        for (int d = 0; d < g.ndev; ++d)
-            if ((rc = v4_launch(g.dev[d], shard_job(j, d), g.dev[d].stream, false))) return rc;
+        for (int d = 0; d < g.ndev; ++d) {
+            PtV4Job jd = shard_job(j, d);
+            // RenderTile + OutputToScreen in one pass, as the reference's worker does per tile (v4
+            // :1562-1564): one device, the presenting configuration (pt_launch_v4 decides)
+            if (screen && g.v4cfg.output_to_screen && g.ndev == 1) {
+                Dev& dv = g.dev[d];
+                if ((rc = grow(dv, (void**)&dv.dtone_out, &dv.dtone_out_cap, (size_t)w * h * sizeof(uint32_t)))) return rc;
+                jd.pix_out = dv.dtone_out;
+                jd.pix_xrgb = 1;
+                jd.pix_fast_tone = g.v4cfg.fast_aces && g.v4cfg.fast_gamma ? 1 : 0;
+            }
+            if ((rc = v4_launch(g.dev[d], jd, g.dev[d].stream, false, &presented))) return rc;
+        }
     }
     g.v4_frame += 1;   // iFrame += 1.0f (v4 :1703), before rendering
     if (screen && g.v4cfg.output_to_screen) {   // OutputToScreen per tile (v4 :1562-1564)
-        if (banded) {
+        if (presented) {
+            Dev& dv = g.dev[0];
+            HIP_TRY(hipMemcpyAsync(screen, dv.dtone_out, (size_t)w * h * sizeof(uint32_t), hipMemcpyDeviceToHost, dv.stream));
+        } else if (banded) {
             Dev& dv = g.dev[0];
             const size_t out_bytes = (size_t)w * h * sizeof(uint32_t);
             if ((rc = grow(dv, (void**)&dv.dtone_out, &dv.dtone_out_cap, out_bytes))) return rc;

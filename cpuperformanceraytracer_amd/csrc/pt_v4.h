@@ -69,6 +69,13 @@ struct PtV4Job {
     int32_t ct_force;               // 1: the continuous-tiles kernel for every launch of >= 8 frames (tests)
     uint32_t ct_back_pct;           // the CT kernel: the last-dispatched ct_back_pct % of the grid claims
                                     // its units from the back of its queue group (pt_tile_queue.h)
+    // fused output stage (OutputToScreen / OutputToFile after RenderTile, v4 :1562-1564): each
+    // pixel's 8-bit value at pix_out[Y * width + X] (full-image rows, the screen's layout), written
+    // with its final accumulator value; nullptr: none.  pix_fast_tone: the tonemap flags are the
+    // default fast ACES / gamma (the only ones the presenting kernels carry)
+    uint32_t* pix_out;
+    int32_t pix_xrgb;               // PT_PIXEL_XRGB8 (OutputToScreen) else RGBA8 (OutputToFile)
+    int32_t pix_fast_tone;
 };
 
 // Scene description in AddQuad/Sphere/MaterialToScene order (v4 :1368-1401).
@@ -82,4 +89,7 @@ struct PtV4SceneDesc {
 void pt_v4_default_scene_desc(PtV4SceneDesc* d);                   // InitializeScene, v4 :1403-1496
 int pt_v4_build_scene(const PtV4SceneDesc* d, PtV4Scene* out);     // PrecomputeQuadData + AddMaterialToScene
 bool pt_v4_is_default_geometry(const PtV4Scene& s);                // geometry == pt_v4_default_scene.h
-hipError_t pt_launch_v4(const PtV4Job& job, const PtV4Scene& scene, hipStream_t stream, bool count);
+// *presented (optional): the launch also wrote job.pix_out (the fused output stage; only for the
+// presenting configuration, pt_v4.hip pt_launch_v4 -- otherwise the caller converts separately)
+hipError_t pt_launch_v4(const PtV4Job& job, const PtV4Scene& scene, hipStream_t stream, bool count,
+                        bool* presented = nullptr);

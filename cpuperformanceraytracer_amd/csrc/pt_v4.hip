@@ -36,6 +36,7 @@
 #include "pt_v4_default_scene.h"
 #include "pt_tile_queue.h"
 #include "pt_wave.h"
+#include "pt_tonemap.h"
 #include <algorithm>
 
 namespace {
@@ -760,7 +761,20 @@ __device__ __forceinline__ void v4_segment(const PtV4Job& job, const PtV4Scene& 
 // DFL: the reference's default sampling flags (USE_RANDOM_JITTER_TEXTURE_SAMPLING 1,
 // USE_UNIT_VECTOR_REJECTION_SAMPLING 1) compiled in -- the default scene's render instance only
 // (0.3950 -> 0.3924 ms at 1080p equirect, profiles/r03r_ab_v4_flags.txt).
-template <int ENV, int LAYOUT, bool COUNT, bool DEF, int FEXP, bool DFL = false>
+// PRESENT: the fused OutputToScreen (v4 :1562-1564 calls it right after RenderTile, per tile): each
+// pixel's 8-bit value (pt_tonemap.h, the default fast ACES / gamma) is written with its final
+// accumulator value at job.pix_out[Y * width + X] -- the presenting instances (pt_launch_v4: the
+// drop-in's one-frame calls in the tiled layout, default scene and flags), so the plain kernels'
+// register allocation is untouched.
+template <bool PRESENT>
+__device__ __forceinline__ void v4_present(const PtV4Job& job, int X, int Y, V3 acc)
+{
+    if constexpr (PRESENT)
+        job.pix_out[(size_t)(uint32_t)Y * (uint32_t)job.width + (uint32_t)X] =
+            pt_tone::pack<true, true>(acc.x, acc.y, acc.z, job.pix_xrgb != 0);
+}
+
+template <int ENV, int LAYOUT, bool COUNT, bool DEF, int FEXP, bool DFL = false, bool PRESENT = false>
 __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job job, PtV4Scene sc)
 {
     __shared__ float s_col[kWaves][kChunk * 64 * 3];
@@ -979,6 +993,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
         acc_p[0] = acc.x;
         acc_p[cs] = acc.y;
         acc_p[2 * cs] = acc.z;
+        v4_present<PRESENT>(job, px, job.row_start + pr * job.row_stride, acc);
     }
     if (job.cost && lane == 0) pt_record_cost(job.cost, tile, (uint32_t)ntiles, tile_work);
     tile = __builtin_amdgcn_readfirstlane(next_tile);
@@ -1447,6 +1462,14 @@ hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool 
         const long blocks = std::min<long>(pt_resident_blocks(kern, 64 * kWaves), (tiles + kWaves - 1) / kWaves);
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), block, 0, st, j, sc);
     };
+    if constexpr (LAYOUT == PT_LAYOUT_TILED_PLANAR8) {   // the presenting instances (pt_launch_v4: one frame)
+        if (j.pix_out && !count) {
+            auto k = pt_v4_kernel<ENV, LAYOUT, false, true, 1, true, true>;
+            const long blocks = std::min<long>(pt_resident_blocks(k, 64 * kWaves), (tiles + kWaves - 1) / kWaves);
+            hipLaunchKernelGGL(k, dim3((unsigned)blocks), block, 0, st, j, sc);
+            return hipGetLastError();
+        }
+    }
     if (j.default_scene) {
         if (count) go(pt_v4_kernel<ENV, LAYOUT, true, true, 2>, pt_v4_ct_kernel<ENV, LAYOUT, true, true, 2>);
         else if (j.fast_exp && j.random_jitter && j.rejection)
@@ -1474,9 +1497,18 @@ hipError_t launch_env(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, boo
 
 }  // namespace
 
-hipError_t pt_launch_v4(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool count)
+hipError_t pt_launch_v4(const PtV4Job& j_in, const PtV4Scene& sc, hipStream_t st, bool count, bool* presented)
 {
-    if (j.ncols <= 0 || j.nrows <= 0 || j.nframes <= 0) return hipSuccess;
+    if (presented) *presented = false;
+    if (j_in.ncols <= 0 || j_in.nrows <= 0 || j_in.nframes <= 0) return hipSuccess;
+    // the fused output stage (j.pix_out) runs in the presenting instances only: the drop-in's calls
+    // (DemofoxRenderOptV4: the tiled layout, one frame -- the per-tile pool kernel), the default scene
+    // and sampling flags, fast exp, and the default fast ACES / gamma
+    PtV4Job j = j_in;
+    if (j.pix_out && !(j.layout == PT_LAYOUT_TILED_PLANAR8 && j.nframes < kChunk && j.default_scene && j.fast_exp &&
+                       j.random_jitter && j.rejection && j.pix_fast_tone && !count))
+        j.pix_out = nullptr;
+    if (presented) *presented = j.pix_out != nullptr;
     if (sc.nquads < 0 || sc.nspheres < 0 || sc.nquads + sc.nspheres > PT_V4_MAX_OBJECTS) return hipErrorInvalidValue;
     if (j.env_mode != PT_V4_ENV_NONE_ && (!j.env || j.env_w <= 0 || j.env_h <= 0)) return hipErrorInvalidValue;
     if (count && !j.counters) return hipErrorInvalidValue;
