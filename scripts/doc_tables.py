@@ -103,7 +103,7 @@ v4rows = [
     ("primary samples/s", e(v["primary_samples_per_s"])),
     ("traced segments per sample", f"{v['segments_per_sample']:.2f} (99.8 % of paths end on the env map)"),
     ("algorithmic FLOP/s (frac of 157.3 TF)", f"{v['roofline']['achieved']:.1f} TF/s ({100 * v['roofline']['frac']:.1f} %; algorithmic = reference-equivalent: every frame traces its own jittered camera ray)"),
-    ("HBM bytes per launch (rocprofv3) vs algorithmic", f"{hbm('v4'):.1f} MB vs {v['roofline']['algorithmic_bytes_per_launch'] / 1e6:.1f} MB (24 B/px + 12 B per env texel gather)"),
+    ("fabric bytes per launch (rocprofv3 FETCH+WRITE, with the continuous-tiles kernel's slot area, §3c) vs algorithmic", f"{hbm('v4'):.1f} MB vs {v['roofline']['algorithmic_bytes_per_launch'] / 1e6:.1f} MB (24 B/px + 12 B per env texel gather)"),
     ("VALU / SALU wave-instructions per launch (PMC)", f"{e(M['v4']['SQ_INSTS_VALU'])} / {e(M['v4']['SQ_INSTS_SALU'])}"),
 ]
 design += "\nThe v4 renderer (`bench.py --workload v4_1080p`: 1920×1080, 8 spp, 8 bounces, default glass scene, 2k synthetic equirect map):\n\n"
