@@ -1111,7 +1111,8 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
 
     // a deferred miss: env(d) with the rng state r, fma'd with throughput t onto the radiance so far,
     // into slot k (pt_v4_kernel's resolve, its slot read replaced by the entry's radiance)
-    auto resolve = [&](V3 d, uint32_t r, V3 t, V3 rs, int k) {
+    // (always_inline: without it the non-default-flag equirect instances called it out of line)
+    auto resolve = [&](V3 d, uint32_t r, V3 t, V3 rs, int k) __attribute__((always_inline)) {
         V3 amb = v3(0.0f, 0.0f, 0.0f);
         if (ENV == PT_V4_ENV_EQUIRECT_) amb = equirect(tex, d, random, r);
         if (ENV == PT_V4_ENV_CUBEMAP_) amb = cubemap(tex, d, random, r);

@@ -11,7 +11,7 @@ W, H, S, B = 1920, 1080, 8, 8
 if len(sys.argv) > 4:
     W, H, S, B = map(int, sys.argv[1:5])
 set_env_map(synthetic_env(), 0, B)
-v4_config(num_bounces=B)
+v4_config(num_bounces=B, random_jitter=os.environ.get("PT_QP_RJ", "1") == "1")
 buf = torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")
 kw = dict(frame_first=1, nframes=S, num_bounces=B, use_env=True)
 cnt = count_v4_device(buf, W, H, **kw)

@@ -245,6 +245,30 @@ def test_drop_in_opt_v4_tiled_and_screen(pin_host):
     assert bits_equal(got, ref), mismatch_report(got, ref)
 
 
+@pytest.mark.parametrize("env_mode", [N.PT_V4_ENV_NONE, N.PT_V4_ENV_CUBEMAP])
+@pytest.mark.parametrize("random_jitter", [True, False])
+def test_drop_in_opt_v4_fused_screen_env_modes(env_mode, random_jitter):
+    """OutputToScreen fused into the v4 render launch (the reference's worker runs it right after
+    RenderTile, v4 :1562-1564) for the other env kinds; without random-jitter texel sampling the
+    launch is not the presenting configuration and the separate pass must give the same pixels."""
+    pt.init()
+    pt.v4_config(env_mode=env_mode, random_jitter=random_jitter)
+    pt.InitializeGlobalRenderResources()
+    w, h, ntx, nty = 160, 96, 4, 6
+    tw, th = w // ntx, h // nty
+    env = _tex(6 * 16, 16, seed=23) if env_mode == N.PT_V4_ENV_CUBEMAP else None
+    tex = pt.texture(env, env.shape[1], env.shape[0], 3) if env is not None else None
+    buf = np.zeros(w * h * 3, np.float32)
+    screen = np.zeros(w * h, np.uint32)
+    for _ in range(2):
+        pt.DemofoxRenderOptV4(buf, w, h, ntx, nty, tw, th, 3, tex, screen)
+    kw = dict(env=env, env_mode=po.ENV_CUBEMAP) if env is not None else dict(env=None)
+    ref = po.render4(w, h, nframes=2, random_jitter=random_jitter, **kw)
+    got = tiled_to_interleaved(buf, w, h, tw, th)
+    assert bits_equal(got, ref), mismatch_report(got, ref)
+    assert np.array_equal(screen.reshape(h, w), po.tonemap(ref, po.PIXEL_XRGB8))
+
+
 def test_drop_in_opt_v4_accumulates_host_buffer():
     """The host buffer is the accumulator (ACCUMULATE_FRAMES): a non-zero start is blended in."""
     pt.init()
