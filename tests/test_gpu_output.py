@@ -189,3 +189,32 @@ def test_fused_present_accumulator_equals_plain_every_occupancy(monkeypatch, wav
         monkeypatch.delenv("PT_MI355_CT_WAVES")
         pt.init()
     assert bits_equal(out[1], out[0]), mismatch_report(out[1], out[0])
+
+
+def test_fused_present_env_full_size_equals_plain():
+    """configs[3] at full size (1920x1080, 16 spp, the synthetic 2k env map): the presenting env
+    kernel's whole accumulator after 3 launches equals the plain env kernel's bit for bit, and its
+    pixels equal the standalone conversion of that accumulator."""
+    import torch
+    from cpuperformanceraytracer_amd.config import synthetic_env
+    from cpuperformanceraytracer_amd.device import JobLauncher, set_env_map, tonemap_device
+    W, H, B, S = 1920, 1080, 8, 16
+    out, pix = [], None
+    for present in (False, True):
+        pt.init(num_bounces=B)
+        set_env_map(synthetic_env(), 0, B)
+        buf = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda:0")
+        p = torch.zeros(H * W, dtype=torch.int32, device="cuda:0")
+        kw = dict(pixels=p, pixel_format=N.PT_PIXEL_XRGB8) if present else {}
+        launch = JobLauncher(buf, W, H, nframes=S, num_bounces=B, use_env=True, **kw)
+        for k in range(3):
+            launch(1 + k * S)
+        torch.cuda.synchronize()
+        out.append(buf.cpu().numpy().reshape(H, W, 3))
+        if present:
+            sep = torch.zeros(H * W, dtype=torch.int32, device="cuda:0")
+            tonemap_device(buf, W, H, sep, pixel_format=N.PT_PIXEL_XRGB8)
+            torch.cuda.synchronize()
+            assert np.array_equal(p.cpu().numpy(), sep.cpu().numpy())
+    pt.init()
+    assert bits_equal(out[1], out[0]), mismatch_report(out[1], out[0])
