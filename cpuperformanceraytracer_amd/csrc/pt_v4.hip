@@ -752,7 +752,10 @@ __device__ __forceinline__ void v4_segment(const PtV4Job& job, const PtV4Scene& 
 // 32 spp 1.247 vs 1.261, 4K 8 spp 1.272 vs 1.296 -- and ahead of the per-tile kernel (0.3602,
 // 1.260, 1.298) at all three.  The instance with the reference's default flags (DFL) only: the
 // others spill in their pool loops at 80 VGPRs and keep 5 waves.
-#define PT_V4_CT_OCC __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : (DFL ? 6 : 5))))
+#ifndef PT_V4_CT_DFL_WAVES
+#define PT_V4_CT_DFL_WAVES 6   // (A/B builds: -DPT_V4_CT_DFL_WAVES=k)
+#endif
+#define PT_V4_CT_OCC __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : (DFL ? PT_V4_CT_DFL_WAVES : 5))))
 #endif
 // FEXP: USE_FAST_APPROXIMATE_EXP as a compile-time switch (1 fast, 0 exact) for the render
 // instances -- the exact expf's registers in the Beer branch would otherwise raise the kernel from
@@ -1497,6 +1500,22 @@ hipError_t launch_env(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, boo
 }
 
 }  // namespace
+
+uint32_t pt_v4_ct_resident_waves()
+{
+    // the continuous-tiles instances above 5 waves per SIMD: the default-flags ones (PT_V4_CT_OCC)
+    const int r[9] = {
+        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_NONE_, PT_LAYOUT_INTERLEAVED, false, true, 1, true>, 64 * kWaves),
+        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_NONE_, PT_LAYOUT_PLANAR8, false, true, 1, true>, 64 * kWaves),
+        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_NONE_, PT_LAYOUT_TILED_PLANAR8, false, true, 1, true>, 64 * kWaves),
+        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_EQUIRECT_, PT_LAYOUT_INTERLEAVED, false, true, 1, true>, 64 * kWaves),
+        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_EQUIRECT_, PT_LAYOUT_PLANAR8, false, true, 1, true>, 64 * kWaves),
+        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_EQUIRECT_, PT_LAYOUT_TILED_PLANAR8, false, true, 1, true>, 64 * kWaves),
+        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_CUBEMAP_, PT_LAYOUT_INTERLEAVED, false, true, 1, true>, 64 * kWaves),
+        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_CUBEMAP_, PT_LAYOUT_PLANAR8, false, true, 1, true>, 64 * kWaves),
+        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_CUBEMAP_, PT_LAYOUT_TILED_PLANAR8, false, true, 1, true>, 64 * kWaves)};
+    return (uint32_t)*std::max_element(r, r + 9) * (uint32_t)kWaves;
+}
 
 hipError_t pt_launch_v4(const PtV4Job& j_in, const PtV4Scene& sc, hipStream_t st, bool count, bool* presented)
 {
