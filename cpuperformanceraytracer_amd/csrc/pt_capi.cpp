@@ -652,7 +652,7 @@ int use_ct_slots(Dev& dv, const LaunchSched& ls, hipStream_t st, float** slots, 
     *waves = 0;
     if (g.no_ct) return PT_OK;
     if (!dv.dct) {   // once per device: 12 KiB per wave of the resident grid (~60 MB)
-        const uint32_t w = std::max(pt_ct_resident_waves(), pt_v4_ct_resident_waves());   // (both pools' grids)
+        const uint32_t w = pt_ct_resident_waves();
         if (hipMalloc(&dv.dct, (size_t)w * pt_ct_wave_floats() * sizeof(float)) == hipSuccess) dv.dct_waves = w;
         else dv.dct = nullptr, (void)hipGetLastError();   // (the per-tile pools then: correct, slower)
     }

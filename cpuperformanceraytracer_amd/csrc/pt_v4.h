@@ -89,9 +89,6 @@ struct PtV4SceneDesc {
 void pt_v4_default_scene_desc(PtV4SceneDesc* d);                   // InitializeScene, v4 :1403-1496
 int pt_v4_build_scene(const PtV4SceneDesc* d, PtV4Scene* out);     // PrecomputeQuadData + AddMaterialToScene
 bool pt_v4_is_default_geometry(const PtV4Scene& s);                // geometry == pt_v4_default_scene.h
-// Waves of the largest resident grid of the v4 continuous-tiles kernels (the slot area must hold it
-// as well as the diffuse kernels', pt_ct_resident_waves)
-uint32_t pt_v4_ct_resident_waves();
 // *presented (optional): the launch also wrote job.pix_out (the fused output stage; only for the
 // presenting configuration, pt_v4.hip pt_launch_v4 -- otherwise the caller converts separately)
 hipError_t pt_launch_v4(const PtV4Job& job, const PtV4Scene& scene, hipStream_t stream, bool count,

@@ -1501,22 +1501,6 @@ hipError_t launch_env(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, boo
 
 }  // namespace
 
-uint32_t pt_v4_ct_resident_waves()
-{
-    // the continuous-tiles instances above 5 waves per SIMD: the default-flags ones (PT_V4_CT_OCC)
-    const int r[9] = {
-        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_NONE_, PT_LAYOUT_INTERLEAVED, false, true, 1, true>, 64 * kWaves),
-        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_NONE_, PT_LAYOUT_PLANAR8, false, true, 1, true>, 64 * kWaves),
-        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_NONE_, PT_LAYOUT_TILED_PLANAR8, false, true, 1, true>, 64 * kWaves),
-        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_EQUIRECT_, PT_LAYOUT_INTERLEAVED, false, true, 1, true>, 64 * kWaves),
-        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_EQUIRECT_, PT_LAYOUT_PLANAR8, false, true, 1, true>, 64 * kWaves),
-        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_EQUIRECT_, PT_LAYOUT_TILED_PLANAR8, false, true, 1, true>, 64 * kWaves),
-        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_CUBEMAP_, PT_LAYOUT_INTERLEAVED, false, true, 1, true>, 64 * kWaves),
-        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_CUBEMAP_, PT_LAYOUT_PLANAR8, false, true, 1, true>, 64 * kWaves),
-        pt_resident_blocks(pt_v4_ct_kernel<PT_V4_ENV_CUBEMAP_, PT_LAYOUT_TILED_PLANAR8, false, true, 1, true>, 64 * kWaves)};
-    return (uint32_t)*std::max_element(r, r + 9) * (uint32_t)kWaves;
-}
-
 hipError_t pt_launch_v4(const PtV4Job& j_in, const PtV4Scene& sc, hipStream_t st, bool count, bool* presented)
 {
     if (presented) *presented = false;
