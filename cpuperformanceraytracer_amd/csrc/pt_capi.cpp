@@ -1762,6 +1762,40 @@ int pt_render_device_present(const pt_device_job* dj, uint32_t* pixels, int32_t 
     return launch(*dv, j, (hipStream_t)stream, false);
 }
 
+int pt_launch_variant(const pt_device_job* dj, int32_t* waves, int32_t* back_pct)
+{
+    int rc;
+    PtJob j;
+    Dev* dv = nullptr;
+    if (!waves || !back_pct) return fail(PT_EINVAL, "null output");
+    *waves = 0;
+    *back_pct = 0;
+    if ((rc = ensure_init()) || (rc = device_job(dj, &j)) || (rc = dev_of(dj->buf, &dv))) return rc;
+    if (dj->use_env) j.env = dv->denv;
+    if (g.no_ct) return PT_OK;   // (the per-tile pools)
+    const bool back = j.nframes <= 16;
+    const uint32_t dflt = back ? g.ct_back_pct : 0u;
+    if (g.ct_waves) {   // fixed (launch(), ct_occupancy)
+        *waves = j.env ? pt_ct_env_waves() : (int32_t)g.ct_waves;
+        *back_pct = (int32_t)dflt;
+        return PT_OK;
+    }
+    SchedKey key = sched_key(j);
+    key.split = j.nframes <= 8 ? g.split : 0u;
+    for (const Sched& s : dv->sched) {
+        if (!s.used || !(s.key == key) || s.wide < 0) continue;
+        if (j.env) {
+            *waves = pt_ct_env_waves();
+            *back_pct = (int32_t)(s.wide && back && !g.back_set ? kEnvBack[s.wide] : dflt);
+        } else {
+            *waves = s.wide ? 6 : 5;
+            *back_pct = (int32_t)(s.wide == 2 && back ? kBackWide : dflt);
+        }
+        return PT_OK;
+    }
+    return PT_OK;   // (undecided)
+}
+
 int pt_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)
 {
     int rc;

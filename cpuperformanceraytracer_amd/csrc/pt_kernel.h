@@ -85,6 +85,7 @@ hipError_t pt_launch_render(const PtJob& job, hipStream_t stream, bool count);
 // current device (the most a launch uses).
 uint32_t pt_ct_wave_floats();
 uint32_t pt_ct_resident_waves();
+int32_t pt_ct_env_waves();   // the env continuous-tiles kernel's waves per SIMD (PT_ENV_WAVES)
 
 // Tiles of a job (8x8 pixel tiles over ncols x nrows).
 inline uint32_t pt_job_tiles(const PtJob& j)

@@ -2031,6 +2031,8 @@ hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* u
 
 uint32_t pt_ct_wave_floats() { return kCtWaveFloats; }
 
+int32_t pt_ct_env_waves() { return PT_ENV_WAVES; }
+
 uint32_t pt_ct_resident_waves()
 {
     static_assert(waves_per_block<false>() == waves_per_block<true>(), "one block shape for the CT kernels");

@@ -87,6 +87,18 @@ def render_device_present(buf, pixels, width: int, height: int, *, frame_first: 
             "pt_render_device_present")
 
 
+def launch_variant(buf, width: int, height: int, *, nframes: int, num_bounces: int, row_start: int = 0,
+                   row_stride: int = 1, nrows: int | None = None, layout: int = N.PT_LAYOUT_INTERLEAVED,
+                   use_env: bool = False) -> dict:
+    """The continuous-tiles launch variant of this job's geometry (pt_launch_variant): waves per SIMD
+    (0: not decided yet) and the back-claim share in percent."""
+    nrows = height if nrows is None else nrows
+    job = _job(buf, width, height, row_start, row_stride, nrows, 1, nframes, num_bounces, layout, use_env)
+    w, b = ctypes.c_int32(0), ctypes.c_int32(0)
+    N.check(N.load().pt_launch_variant(ctypes.byref(job), ctypes.byref(w), ctypes.byref(b)), "pt_launch_variant")
+    return {"waves_per_simd": int(w.value), "back_claim_pct": int(b.value)}
+
+
 def tonemap_device(buf, width: int, nrows: int, pixels, *, layout: int = N.PT_LAYOUT_INTERLEAVED,
                    pixel_format: int = N.PT_PIXEL_RGBA8, stream=None) -> None:
     """The standalone output stage (pt_tonemap_device) on an HBM accumulator of nrows x width pixels

@@ -326,6 +326,12 @@ int pt_count_device(const pt_device_job* job, void* hip_stream, pt_work_counts* 
  * where the pixel's final accumulator value is -- no second pass over the accumulator.  Equal bit for
  * bit to pt_render_device followed by pt_tonemap_device on the job's rows.  Async on hip_stream. */
 int pt_render_device_present(const pt_device_job* job, uint32_t* pixels, int32_t format, void* hip_stream);
+/* The launch variant the continuous-tiles pool runs for `job`'s geometry (its buffer's device): waves
+ * per SIMD (5 or 6) and the share of the grid that claims units from the back (percent; 0 for
+ * launches of more than 16 frames).  Fixed by PT_MI355_CT_WAVES / PT_MI355_BACK, else the pick of the
+ * geometry's timed launches; *waves = 0 while it is undecided (no scheduled launch timed yet), or for a
+ * job that does not run the continuous-tiles pool.  Host state only, no GPU work. */
+int pt_launch_variant(const pt_device_job* job, int32_t* waves, int32_t* back_pct);
 
 #ifdef __cplusplus
 }

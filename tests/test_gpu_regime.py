@@ -155,3 +155,24 @@ def test_v4_bench_regime_matches_oracle(fresh):
     for k in range(5, H, 90):
         ref = pyoracle.render4(W, H, nframes=frames, num_bounces=B, row_start=k, row_stride=1, nrows=1, env=env)
         assert bits_equal(img[k:k + 1], ref), (k, mismatch_report(img[k:k + 1], ref))
+
+
+def test_launch_variant_reports_the_pick(fresh):
+    """pt_launch_variant: undecided before the geometry's timed launches, then the pick they made (5 or
+    6 waves per SIMD; 20 or 45 % back claims for these one-chunk launches); with PT_MI355_CT_WAVES
+    fixed, that occupancy and the default share at once.  bench.py reports it as launch_variant."""
+    import torch
+    from cpuperformanceraytracer_amd.device import launch_variant
+    W, H, B, S = 1920, 1080, 8, 8
+    buf = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda:0")
+    fresh(B)
+    assert launch_variant(buf, W, H, nframes=S, num_bounces=B)["waves_per_simd"] == 0
+    _launch_series(W, H, B, S, 24)   # (ends synchronised: the timed launches' events are complete)
+    # the pick is taken by the first launch that finds the timing events complete
+    from cpuperformanceraytracer_amd.device import JobLauncher
+    JobLauncher(buf, W, H, nframes=S, num_bounces=B, stream=torch.cuda.current_stream())(1)
+    torch.cuda.synchronize()
+    v = launch_variant(buf, W, H, nframes=S, num_bounces=B)
+    assert (v["waves_per_simd"], v["back_claim_pct"]) in ((5, 20), (6, 20), (6, 45)), v
+    fresh(B, PT_MI355_CT_WAVES="6")
+    assert launch_variant(buf, W, H, nframes=S, num_bounces=B) == {"waves_per_simd": 6, "back_claim_pct": 20}
