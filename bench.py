@@ -47,6 +47,12 @@ sys.path.insert(0, str(ROOT))
 METRIC = "ray-samples/sec (pixels×spp×bounces) at 1920×1080; ms/frame"
 
 
+def metric_label(W: int, H: int) -> str:
+    """BASELINE.json's metric string for the headline 1920x1080 workloads; other images (c3's 4K, the
+    configs[4] leg's 7680x4320) name their own size in the same form."""
+    return METRIC if (W, H) == (1920, 1080) else METRIC.replace("1920×1080", f"{W}×{H}")
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -558,7 +564,7 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
                         "2-cycle f32 ops issue at ~1.0 per SIMD per ns, the 4-cycle class (compares, selects, "
                         "min/max, f64, conversions) at ~0.58 (DESIGN.md §3)"}
     res = {
-        "metric": METRIC,
+        "metric": metric_label(wl.width, wl.height),
         "value": value,
         "unit": "ray-samples/s",
         "n_gpus": world,
@@ -646,6 +652,59 @@ def strong_leg(wl4, rank: int, world: int, ops, render_fn, count_fn, *, rehearse
                    "step renders the whole image over the N ranks (rows r::N) and gathers it to rank 0 over "
                    "RCCL; value = ray-samples/s of the whole job, render and gather per step reported apart")
     return out
+
+
+class Hooks:
+    """What `drive` needs beyond bench.run's render/count functions: check_errors() raises on a device
+    error the run left (PT_EKERNEL); launch_variant(buf, Wg, Hg, rs, st, nr) -> dict, the
+    continuous-tiles variant the timed launches picked (None: not reported); output_stage(buf, res)
+    -> dict, rank 0's output-stage measurement on its accumulator (None: skipped); cpu_baseline()
+    -> dict (None: skipped)."""
+
+    def __init__(self, check_errors=None, launch_variant=None, output_stage=None, cpu_baseline=None):
+        self.check_errors = check_errors or (lambda: None)
+        self.launch_variant = launch_variant
+        self.output_stage = output_stage
+        self.cpu_baseline = cpu_baseline
+
+
+def drive(args, wl, rank: int, world: int, ops, render_fn, count_fn, hooks: Hooks, *,
+          rehearse: bool = False, leg_workload=None) -> dict | None:
+    """Everything main() does after the device is set up, on every rank: the timed job (run), the
+    reports that need only the rank's own state, the configs[4] strong leg of the default line (all
+    ranks take part: it gathers), then rank 0's output stage and CPU baseline.  Returns rank 0's JSON
+    object, None on the other ranks -- whose only duty after run() is to take part in the leg's
+    collectives (a report that assumed a result dict there crashed ranks 1..N-1 before the leg and
+    left rank 0 waiting in its all-reduce: ADVICE round 5).  leg_workload: the strong leg's workload
+    (default configs[4], c5_8k; tests pass a tiny one)."""
+    from cpuperformanceraytracer_amd.shard import rows_of
+    res = run(args, wl, rank, world, ops, render_fn, count_fn, rehearse=rehearse)
+    hooks.check_errors()   # no launch of the run abandoned a tile (PT_EKERNEL otherwise)
+    acc = None
+    if res is not None:
+        acc = res.pop("_accumulator")
+        if hooks.launch_variant is not None:   # the continuous-tiles launch variant (pt_launch_variant)
+            Wg, Hg = job_image(wl, world)
+            rs, st, nr = rows_of(rank, world, Hg)
+            try:   # (a report: it never costs the line)
+                res["launch_variant"] = hooks.launch_variant(acc, Wg, Hg, rs, st, nr)
+            except Exception as e:   # noqa: BLE001
+                res["launch_variant"] = {"error": str(e)}
+    # configs[4] beside the default workload's line (its scaling curve from the driver's N-GPU runs)
+    configs4 = None
+    if args.workload == "c2_1080p" and not args.no_configs4:
+        from cpuperformanceraytracer_amd.config import CONFIGS
+        configs4 = strong_leg(leg_workload or CONFIGS["c5_8k"], rank, world, ops, render_fn, count_fn, rehearse=rehearse)
+        hooks.check_errors()
+    if rank != 0:
+        return None
+    if hooks.output_stage is not None:
+        res["output_stage"] = hooks.output_stage(acc, res)
+    if configs4 is not None:
+        res["configs4"] = configs4
+    if world == 1 and not args.no_cpu_baseline and hooks.cpu_baseline is not None:
+        res["cpu_baseline"] = hooks.cpu_baseline()
+    return res
 
 
 def spawn_ranks(n: int, argv: list[str], script: str | None = None) -> int:
@@ -752,40 +811,32 @@ def main() -> None:
                    use_env=wl.env, stream=stream)
 
     ops = DeviceOps(dev, stream)
-    res = run(args, wl, rank, world, ops, render_fn, count_fn, rehearse=rehearse)
-    check_device_errors()   # no launch of the run abandoned a tile (PT_EKERNEL otherwise)
-    if not v4:   # the continuous-tiles launch variant the timed launches ran (pt_launch_variant)
-        Wg, Hg = job_image(wl, world)
-        rs, st, nr = rows_of(rank, world, Hg)
-        try:   # (a report: it never costs the line)
-            res["launch_variant"] = launch_variant(res["_accumulator"], Wg, Hg, nframes=wl.spp, num_bounces=B,
-                                                   row_start=rs, row_stride=st, nrows=nr, use_env=wl.env)
-        except Exception as e:   # noqa: BLE001
-            res["launch_variant"] = {"error": str(e)}
-    # configs[4] beside the default workload's line (its scaling curve from the driver's N-GPU runs)
-    configs4 = None
-    if args.workload == "c2_1080p" and not args.no_configs4:
-        configs4 = strong_leg(CONFIGS["c5_8k"], rank, world, ops, render_fn, count_fn, rehearse=rehearse)
-        check_device_errors()
-    if rank == 0:
+
+    def output_stage(buf, res):
         # the presented frame: rank 0's rendered accumulator (its first W x H pixels when sharded)
         W, H = wl.width, wl.height
-        buf = res.pop("_accumulator")
         acc = buf if buf.numel() >= W * H * 3 else torch.zeros(W * H * 3, dtype=torch.float32, device=dev)
         if acc is not buf:
             acc[:buf.numel()].copy_(buf)
-        res["output_stage"] = measure_output_stage(acc, W, H, stream)
+        out = measure_output_stage(acc, W, H, stream)
         if not v4:
             Wg, Hg = job_image(wl, world)
             rs, st, nr = rows_of(rank, world, Hg)
-            res["output_stage"]["fused"] = measure_fused_output(
+            out["fused"] = measure_fused_output(
                 lambda b, px: JobLauncher(b, Wg, Hg, nframes=wl.spp, num_bounces=B, row_start=rs, row_stride=st,
                                           nrows=nr, use_env=wl.env, stream=stream, pixels=px),
                 Wg, nr, wl.spp, stream, frame0=1)
-        if configs4 is not None:
-            res["configs4"] = configs4
-        if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(wl, args.cpu_seconds, env)
+        return out
+
+    hooks = Hooks(check_errors=check_device_errors,
+                  launch_variant=None if v4 else (
+                      lambda buf, Wg, Hg, rs, st, nr: launch_variant(buf, Wg, Hg, nframes=wl.spp, num_bounces=B,
+                                                                     row_start=rs, row_stride=st, nrows=nr,
+                                                                     use_env=wl.env)),
+                  output_stage=output_stage,
+                  cpu_baseline=lambda: cpu_baseline(wl, args.cpu_seconds, env))
+    res = drive(args, wl, rank, world, ops, render_fn, count_fn, hooks, rehearse=rehearse)
+    if rank == 0:
         print(json.dumps(res))
     if world > 1:
         dist.destroy_process_group()

@@ -270,3 +270,75 @@ def test_main_dispatches_to_spawn_ranks(monkeypatch):
     with pytest.raises(SystemExit) as ei:
         bench.main()
     assert ei.value.code == 7 and seen == {"n": 4, "argv": ["--gpus", "4", "--steps", "3"]}
+
+
+def _worker_drive(rank, world, port, q):
+    """bench.drive -- main()'s whole post-setup flow (run, launch-variant report, the configs[4]
+    strong leg, rank 0's output stage and CPU baseline) -- on CPU with host hooks."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import torch.distributed as dist
+    import bench
+    from cpuperformanceraytracer_amd.config import Workload
+    from oracle import pyoracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        wl = Workload("tiny", 64, 36, 3, 8, scaling="weak")
+        wl4 = Workload("tiny_c5", 48, 28, 4, 8, scaling="strong")
+        args = bench.parse(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--device-warmup-ms", "0"])
+
+        def render_fn(buf, W, H, f, n, rs, st, nr):
+            pyoracle.render(W, H, frame_first=f, nframes=n, num_bounces=8, row_start=rs, row_stride=st, nrows=nr,
+                            nthreads=2, buf=buf.numpy())
+
+        def count_fn(buf, W, H, f, n, rs, st, nr):
+            render_fn(buf, W, H, f, n, rs, st, nr)
+            _, c = pyoracle.render_counted(W, H, frame_first=f, nframes=n, num_bounces=8, row_start=rs,
+                                           row_stride=st, nrows=nr)
+            return {"segments": c["segments"], "samples": c["samples"], "escaped": c["escaped"],
+                    "lane_slots": c["segments"], "primary": c["samples"]}
+
+        calls = []
+        hooks = bench.Hooks(
+            check_errors=lambda: calls.append("check"),
+            launch_variant=lambda buf, W, H, rs, st, nr: {"rows": [rs, st, nr], "n": int(buf.numel())},
+            output_stage=lambda buf, res: {"pixels": int(buf.numel()) // 3},
+            cpu_baseline=lambda: {"value": 1.0})
+        out = bench.drive(args, wl, rank, world, bench.HostOps(), render_fn, count_fn, hooks, leg_workload=wl4)
+        q.put((rank, out, calls))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_drive_completes_on_every_rank(world):
+    """main()'s post-run flow on N ranks: ranks 1..N-1 (whose run() result is None) pass the reports
+    and take part in the configs[4] leg's gathers; rank 0's object carries launch_variant, the leg,
+    the output stage, and (N = 1 only) the CPU baseline.  Round 5's main() crashed every rank but 0
+    here, so rank 0 waited in the leg's all-reduce and no N-GPU line was ever printed."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_drive, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (o, c)) for r, o, c in (q.get(timeout=240) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(1, world):
+        assert got[r][0] is None and got[r][1] == ["check", "check"]
+    res, calls = got[0]
+    assert calls == ["check", "check"]
+    assert "_accumulator" not in res
+    assert res["launch_variant"]["rows"][1] == world
+    assert res["configs4"]["scaling"] == "strong" and res["configs4"]["n_gpus"] == world
+    assert res["configs4"]["metric"].endswith("at 48×28; ms/frame")
+    assert res["metric"].endswith("at 64×36; ms/frame")
+    assert res["output_stage"]["pixels"] > 0
+    assert ("cpu_baseline" in res) == (world == 1)
+    if world > 1:
+        assert res["configs4"]["verified"]["bit_exact"]
