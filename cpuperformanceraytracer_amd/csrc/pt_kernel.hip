@@ -142,7 +142,7 @@ __device__ __forceinline__ bool facing(V3 n, V3 D)
 }
 
 // Per-quad, per-axis vertex components (A_k, B_k, C_k, D_k): indexed by the lane's axis.
-struct AxisRow {
+struct alignas(16) AxisRow {   // (16-byte aligned: one ds_read_b128 per row)
     float a, b, c, d;
 };
 // The per-axis rows of a quad, s_axis[(q * 2 + fl) * 3 + k], for both vertex orders: row (q, fl, k)
@@ -390,26 +390,23 @@ struct Hit {
     int fb;       // the culled quad stage fell back to the six exact tests (counted by COUNT builds)
 };
 
-// The six exact quad tests in the reference's order (TestSceneTrace :192-261) into h.
+// The six exact quad tests in the reference's order (TestSceneTrace :192-261) into h.  Plain LDS
+// loads of the per-quad rows: the compiler's waitcnt insertion places each wait before the row's
+// first use.  (Until round 5 this was a software pipeline of inline-asm ds_read_b128 with its
+// s_waitcnt in a separate asm statement: the compiler treats an asm output as defined when the
+// load's statement ends and may copy or spill it before the data returns -- a hazard that depends on
+// each template instance's register allocation.  The plain loads also spill less: the 6-wave
+// presenting instance 2 VGPRs instead of 3, the counting instances 18-31 instead of 25-31, and four
+// env per-tile instances reach 4 waves instead of 3.  tests/test_isa_lgkm.py checks every kernel of
+// the built library for LDS return hazards.)
 template <class SC, bool QV>
 __device__ __forceinline__ void quads_exact(const AxisRow* s_axis, V3 P, V3 D, V3 pq, int axis, float dP, float dD,
                                             float yD, Hit& h)
 {
-    // software pipeline of the per-quad LDS rows: row q+1 is read while quad q is tested, so the
-    // LDS latency hides under a quad test instead of stalling inside its divergent tail
-    typedef __attribute__((address_space(3))) const AxisRow lds_row_t;
-    const uint32_t base = (uint32_t)(uintptr_t)(lds_row_t*)s_axis + (uint32_t)axis * (uint32_t)sizeof(AxisRow);
-    typedef float f32x4 __attribute__((ext_vector_type(4)));
-    f32x4 row;
-    asm volatile("ds_read_b128 %0, %1" : "=v"(row) : "v"(base));
+    const AxisRow* rows = s_axis + axis;
 #pragma unroll
-    for (int q = 0; q < PT_NQUADS; ++q) {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(row));
-        const AxisRow cur{row.x, row.y, row.z, row.w};
-        if (q + 1 < PT_NQUADS)
-            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(row) : "v"(base), "i"((q + 1) * kAxisRowsPerQuad<QV> * (int)sizeof(AxisRow)));
-        quad_test<SC>(q, P, D, pq, dP, dD, yD, h.best, h.id, h.flag, cur);
-    }
+    for (int q = 0; q < PT_NQUADS; ++q)
+        quad_test<SC>(q, P, D, pq, dP, dD, yD, h.best, h.id, h.flag, rows[q * kAxisRowsPerQuad<QV>]);
 }
 
 // Per (quad, flip): the vertices in the reference's order after its facing flip (a, b, c, d or
