@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
-# Round 5, end: the final tree's whole -m gpu suite, smoke() and the default bench line.
+# Round-end check: the tree's whole -m gpu suite, smoke() and the default bench line.
 set -euo pipefail
-TAG=${1:-r05end}; OUT=gpurun_out/$TAG
+TAG=${1:-round_check}; OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rf -p no:cacheprovider > "$OUT/gpu_tests.log" 2>&1 || { tail -40 "$OUT/gpu_tests.log"; exit 1; }
