@@ -36,7 +36,7 @@ PT_PIXEL_XRGB8 = 1
 EXPORTED_SYMBOLS = (
     "pt_init", "pt_shutdown", "pt_last_error", "pt_default_config", "pt_set_frame", "pt_get_frame",
     "pt_render_scalar", "pt_render_simd", "pt_render_simd_tiled", "pt_render_tile", "pt_begin_frame",
-    "pt_readback", "pt_gather_root", "pt_unpin_host", "pt_release_buffer", "pt_initialized_device", "pt_check_device_errors", "pt_device_count",
+    "pt_readback", "pt_gather_root", "pt_unpin_host", "pt_release_buffer", "pt_initialized_device", "pt_check_device_errors", "pt_build_checked", "pt_device_count",
     "pt_device_ordinal", "pt_render_device", "pt_count_device", "pt_render_device_present", "pt_launch_variant",
     "pt_load_texture", "pt_decode_hdr", "pt_free_texture", "pt_set_env_map", "pt_render_simt_textured",
     "pt_tonemap", "pt_tonemap_device", "pt_write_bmp", "pt_load_cubemap_texture",
@@ -159,6 +159,7 @@ def load() -> ctypes.CDLL:
         "pt_release_buffer": (i32, [vp]),
         "pt_initialized_device": (i32, []),
         "pt_check_device_errors": (i32, []),
+        "pt_build_checked": (i32, []),
         "pt_device_count": (i32, []),
         "pt_device_ordinal": (i32, [i32]),
         "pt_render_device": (i32, [ctypes.POINTER(PtDeviceJob), vp]),

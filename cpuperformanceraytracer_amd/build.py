@@ -26,7 +26,8 @@ ARCH = os.environ.get("PT_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["pt_kernel.hip", "pt_output.hip", "pt_v4.hip", "pt_scene.cpp", "pt_v4_scene.cpp", "pt_capi.cpp",
            "pt_dropin.cpp", "pt_texture.cpp"]
 HEADERS = ["pt_kernel.h", "pt_output.h", "pt_v4.h", "pt_v4_default_scene.h", "pt_scene.h", "pt_sincosf.h", "pt_exactmath.h",
-           "pt_invtrig.h", "pt_envcert.h", "pt_tile_queue.h", "pt_quadcull.h", "pt_libmf.h", "pt_wave.h"]
+           "pt_invtrig.h", "pt_envcert.h", "pt_tile_queue.h", "pt_quadcull.h", "pt_libmf.h", "pt_wave.h", "pt_guard.h"]
+CHECKED_LIB = ROOT / "build" / "libpt_checked.so"
 PARITY_FLAGS = [
     "-ffp-contract=off",
     "-fhip-fp32-correctly-rounded-divide-sqrt",
@@ -83,6 +84,24 @@ def build_variant(name: str, defines=(), extra=()) -> Path:
     return out
 
 
+def build_checked(force: bool = False, verbose: bool = False) -> Path:
+    """The checked build (-DPT_CHECKED=1, pt_guard.h): every global index the continuous-tiles pools and
+    the schedule builder compute is bounds-tested and a failure is reported as PT_EKERNEL naming the
+    guard.  build/libpt_checked.so, selected with PT_MI355_LIB (a diagnostic library, not the product)."""
+    deps = [CSRC / s for s in SOURCES + HEADERS] + [ROOT / "include" / "pt_mi355.h", Path(__file__)]
+    if not force and not _stale(CHECKED_LIB, deps):
+        return CHECKED_LIB
+    CHECKED_LIB.parent.mkdir(exist_ok=True)
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *PARITY_FLAGS, *PERF_FLAGS,
+           "-DPT_CHECKED=1", f"-I{ROOT / 'include'}", f"-I{CSRC}", "-Wall", "-Wno-unused-function",
+           *[str(CSRC / s) for s in SOURCES], "-o", str(CHECKED_LIB) + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(str(CHECKED_LIB) + ".tmp", CHECKED_LIB)
+    return CHECKED_LIB
+
+
 def build_examples(verbose: bool = False) -> Path:
     """examples/reference_host: a reference-shaped C++ host linked against libpt_mi355.so through
     the reference-named header only (the drop-in boundary exercised as a real link)."""
@@ -109,6 +128,8 @@ def build_oracle(verbose: bool = False) -> None:
 
 if __name__ == "__main__":
     build_lib(force="--force" in sys.argv, verbose=True)
+    if "--checked" in sys.argv:
+        build_checked(verbose=True)
     build_examples(verbose=True)
     build_oracle(verbose=True)
     print(LIB)

@@ -18,6 +18,7 @@
 // full-size buffer of which it owns the rows for the tiled layout (whose rows are not contiguous in
 // the host buffer); transfers move only the owned rows (pitched 2D copies).
 #include "pt_kernel.h"
+#include "pt_guard.h"
 #include "pt_output.h"
 #include "pt_v4.h"
 #include "../../include/pt_mi355.h"
@@ -165,6 +166,7 @@ struct State {
     char ct_seq[64] = {};
     uint32_t ct_seq_len = 0, ct_seq_pos = 0;
     uint32_t split = 1;   // PT_MI355_SPLIT (read by pt_init): tile split factor of the schedule (0: none)
+    int64_t test_bad_entry = -1;   // PT_MI355_TEST_BAD_ENTRY (test hook, pt_init)
     bool no_ct = false;   // PT_MI355_NO_CT=1 (read by pt_init): one-chunk launches on render_body (A/B)
 };
 
@@ -302,6 +304,25 @@ int xfer(int d, const Geo& geo, float* host, bool to_device, const Region& rg)
 // reported.  Device jobs on callers' streams are covered once those streams have been synchronised
 // (pt_check_device_errors): a launch still running when the words are read and reset may record its
 // fault after the reset, and that fault is then reported by the next check.
+const char* guard_name(uint32_t id)
+{
+    switch (id) {
+        case PT_G_QUEUE_ENTRY: return "schedule entry outside the launch's tiles";
+        case PT_G_NUNITS: return "schedule unit count beyond its entries";
+        case PT_G_UNIT_RANGE: return "unit positions outside the schedule";
+        case PT_G_SLOT_BASE: return "wave slot area beyond the allocation";
+        case PT_G_ITEM_SLOT: return "item radiance slot outside its wave's area";
+        case PT_G_PIXEL: return "accumulator element outside the buffer";
+        case PT_G_PIXOUT: return "presented pixel outside the pixel buffer";
+        case PT_G_ENVQ: return "env miss-queue entry outside the queue";
+        case PT_G_SCHED_ORDER: return "schedule builder: order position out of range";
+        case PT_G_SCHED_UNIT: return "schedule builder: unit index out of range";
+        case PT_G_RECORD: return "item record slot >= 64";
+        case PT_G_QUEUE_GROUP: return "queue group out of range";
+        default: return "unknown";
+    }
+}
+
 int sync_all()
 {
     int rc;
@@ -316,13 +337,20 @@ int sync_all()
     }
     for (int d = 0; d < g.ndev; ++d) {
         Dev& dv = g.dev[d];
-        if (dv.herr[0] == 0) continue;
+        const uint32_t guards = dv.herr[PT_ERR_GUARD_COUNT];
+        if (dv.herr[0] == 0 && guards == 0) continue;
         const uint32_t n = dv.herr[0], tile = dv.herr[1];
+        const unsigned long long first =
+            (unsigned long long)dv.herr[PT_ERR_GUARD_FIRST] | ((unsigned long long)dv.herr[PT_ERR_GUARD_FIRST + 1] << 32);
         if ((rc = use_dev(dv))) return rc;
-        HIP_TRY(hipMemsetAsync(dv.derr, 0, sizeof(uint32_t), dv.stream));
-        HIP_TRY(hipMemsetAsync(dv.derr + 1, 0xff, sizeof(uint32_t), dv.stream));
+        const uint32_t init[PT_ERR_WORDS] = {0u, ~0u, 0u, 0u, ~0u, ~0u};
+        memcpy(dv.herr, init, sizeof(init));
+        HIP_TRY(hipMemcpyAsync(dv.derr, dv.herr, sizeof(init), hipMemcpyHostToDevice, dv.stream));
         HIP_TRY(hipStreamSynchronize(dv.stream));
-        dv.herr[0] = 0;
+        if (guards)
+            return fail(PT_EKERNEL, "device %d: %u kernel bounds guard failure(s), the first: guard %u (%s), value %u; "
+                        "the accumulator is invalid", dv.ordinal, guards, (uint32_t)(first >> 32),
+                        guard_name((uint32_t)(first >> 32)), (uint32_t)first);
         return fail(PT_EKERNEL, "device %d: a pool guard (ring iterations or continuous-tiles chunks) abandoned %u "
                     "tile(s) (first: tile %u of its launch); the accumulator is invalid", dv.ordinal, n, tile);
     }
@@ -583,9 +611,11 @@ int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls, uin
             // 3x: 0.2513 / 0.4965 / 0.8356)
             const uint32_t unit_mult = key.kind == 0 && !g.no_ct ? 2u : 1u;
             hipError_t e = pt_launch_schedule(s->cost, s->order, s->units, s->units + 2 * s->key.ntiles + 1, s->key.ntiles,
-                                              split, unit_mult, st);
+                                              split, unit_mult, st, dv.derr);
             if (e != hipSuccess) return fail(PT_EHIP, "schedule launch failed: %s", hipGetErrorString(e));
             s->built = true;
+            if (g.test_bad_entry >= 0 && (uint32_t)g.test_bad_entry < 2u * s->key.ntiles)   // (test hook, below)
+                HIP_TRY(hipMemsetAsync(s->order + g.test_bad_entry, 0xff, sizeof(uint32_t), st));
         }
         if (s->built) {
             ls->sched = s;
@@ -1223,6 +1253,7 @@ int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count, bool* presented = 
     j.units = ls.units;
     j.nunits = ls.nunits;
     j.cost = ls.cost;
+    j.err = dv.derr;
     // (the v4 pool's slots per wave: pt_v4_ct_wave_floats() <= pt_ct_wave_floats(), pt_v4.hip)
     if ((rc = use_ct_slots(dv, ls, st, &j.ct_slots, &j.ct_waves))) return rc;
     j.ct_force = g.v4_ct_force;
@@ -1313,10 +1344,11 @@ int init_dev(Dev& dv, int32_t ordinal)
     if (hipMalloc(&dv.derr, PT_ERR_WORDS * sizeof(uint32_t)) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc(err) failed");
     if (hipHostMalloc(&dv.herr, PT_ERR_WORDS * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess)
         return fail(PT_ENOMEM, "hipHostMalloc(err) failed");
-    HIP_TRY(hipMemset(dv.derr, 0, sizeof(uint32_t)));
-    HIP_TRY(hipMemset(dv.derr + 1, 0xff, sizeof(uint32_t)));
-    dv.herr[0] = 0;
-    dv.herr[1] = ~0u;
+    {
+        const uint32_t init[PT_ERR_WORDS] = {0u, ~0u, 0u, 0u, ~0u, ~0u};   // (pt_kernel.h: the words' meaning)
+        HIP_TRY(hipMemcpy(dv.derr, init, sizeof(init), hipMemcpyHostToDevice));
+        memcpy(dv.herr, init, sizeof(init));
+    }
     if (hipMalloc(&dv.dqueue, (size_t)kQueueRing * PT_QUEUE_WORDS * sizeof(unsigned)) != hipSuccess)
         return fail(PT_ENOMEM, "hipMalloc(queue) failed");
     if (hipMalloc(&dv.dscene, sizeof(PtScene)) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc(scene) failed");
@@ -1425,6 +1457,10 @@ int pt_init(const pt_config* cfg)
         for (const char* c = sq; *c && g.ct_seq_len < sizeof(g.ct_seq); ++c)
             if (*c == '5' || *c == '6') g.ct_seq[g.ct_seq_len++] = *c;
     }
+    // test hook: PT_MI355_TEST_BAD_ENTRY=<position> overwrites that entry of every schedule built with
+    // ~0u (a tile outside the launch) -- the queue's entry guard must report it (tests/test_gpu_guards.py)
+    g.test_bad_entry = -1;
+    if (const char* be = getenv("PT_MI355_TEST_BAD_ENTRY")) g.test_bad_entry = (int64_t)strtoll(be, nullptr, 10);
     g.split = 1;
     if (const char* sp = getenv("PT_MI355_SPLIT")) g.split = (uint32_t)strtoul(sp, nullptr, 10);
     if (const char* cap = getenv("PT_MI355_RING_GUARD_CAP")) {
@@ -1839,6 +1875,8 @@ int pt_check_device_errors(void)
 }
 
 int32_t pt_initialized_device(void) { return g.inited ? g.dev[0].ordinal : -1; }
+
+int32_t pt_build_checked(void) { return PT_CHECKED ? 1 : 0; }
 
 int32_t pt_device_count(void) { return g.inited ? g.ndev : 0; }
 

@@ -45,8 +45,7 @@ struct PtJob {
     const uint32_t* units;         // schedule runs: unit k = positions [units[k], units[k+1]), nullptr = one tile each
     const uint32_t* nunits;        // device word: number of units (with units)
     uint32_t* cost;                // per-tile work of this launch (trace iterations), nullptr = not recorded
-    uint32_t* err;                 // PT_ERR_WORDS: [0] tiles abandoned by the ring pool's iteration guard,
-                                   // [1] the smallest such tile index (~0u: none); nullptr = not recorded
+    uint32_t* err;                 // PT_ERR_WORDS error words (below); nullptr = not recorded
     uint32_t guard_cap;            // upper limit of the ring pool's iteration guard: ~0u (tests lower it)
     float* ct_slots;               // continuous-tiles pool (pt_kernel.hip render_body_ct): pt_ct_wave_floats()
     uint32_t ct_waves;             // f32 per wave for ct_waves waves; nullptr: one-chunk launches use render_body
@@ -64,7 +63,28 @@ struct PtJob {
     float cam_W, cam_H, cam_yW, cam_yH, cam_aspect, cam_yAspect;
 };
 
-#define PT_ERR_WORDS 2
+// Kernel error words (PtJob::err, PtV4Job::err; reset by the host after it reports them, pt_capi.cpp
+// sync_all): [0] tiles abandoned by a pool guard (the ring pool's iteration guard, the
+// continuous-tiles pools' chunk / event guards), [1] the smallest such tile index (~0u: none),
+// [2] failed bounds guards (pt_guard.h), [3] 0, [4..5] the smallest (guard id << 32 | detail) of
+// them (~0: none).
+#define PT_ERR_WORDS 6
+#define PT_ERR_GUARD_COUNT 2
+#define PT_ERR_GUARD_FIRST 4
+enum PtGuardId : uint32_t {
+    PT_G_QUEUE_ENTRY = 1,   // a schedule entry outside the launch's tiles (tile_at; every build)
+    PT_G_NUNITS = 2,        // the schedule's unit count beyond its order (2 x tiles entries)
+    PT_G_UNIT_RANGE = 3,    // a unit's schedule positions outside order[]
+    PT_G_SLOT_BASE = 4,     // a wave's continuous-tiles slot area beyond ct_waves
+    PT_G_ITEM_SLOT = 5,     // an item's radiance slot outside its wave's area
+    PT_G_PIXEL = 6,         // an accumulator element outside the job's buffer
+    PT_G_PIXOUT = 7,        // a presented pixel outside the job's pixel buffer
+    PT_G_ENVQ = 8,          // an env miss-queue entry outside the wave's queue
+    PT_G_SCHED_ORDER = 9,   // the schedule builder: an order position >= 2 x tiles
+    PT_G_SCHED_UNIT = 10,   // the schedule builder: a unit index > 2 x tiles
+    PT_G_RECORD = 11,       // a tile's item record slot >= 64
+    PT_G_QUEUE_GROUP = 12,  // a queue group counter beyond PT_NQUEUES
+};
 
 // Tile queues: one counter per XCD group, 128 B apart (PT_QUEUE_WORDS u32 per launch).
 #ifndef PT_NQUEUES
@@ -98,5 +118,7 @@ inline uint32_t pt_job_tiles(const PtJob& j)
 // launch; split 0: never), units = runs of about equal cost over it, *nunits = their number.
 // cost: 2 x ntiles words (pt_record_cost), order: up to 2 x ntiles entries, units: 2 x ntiles + 1.
 // unit_mult: a multiple of the adaptive unit cost (the continuous-tiles pools: 2).
+// err: the device's error words (the checked build's guards; nullptr: none).
 hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* units, uint32_t* nunits,
-                              uint32_t ntiles, uint32_t split, uint32_t unit_mult, hipStream_t stream);
+                              uint32_t ntiles, uint32_t split, uint32_t unit_mult, hipStream_t stream,
+                              uint32_t* err = nullptr);

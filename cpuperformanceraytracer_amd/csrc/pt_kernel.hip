@@ -47,6 +47,7 @@
 #define PT_EC_SQRT(x) pt::sqrt_rn(x)                     // t >= 2^-21 where the value is used
 #include "pt_envcert.h"
 #include "pt_tile_queue.h"
+#include "pt_guard.h"
 #include "pt_tonemap.h"
 #include "pt_output.h"
 #include "pt_wave.h"
@@ -324,6 +325,16 @@ __device__ __forceinline__ size_t out_index(const PtJob& j, int lc, int lr)
         return (size_t)ty * j.tile_h * j.width * 3u + (size_t)tx * j.tile_w * j.tile_h * 3u +
                ((size_t)ly * j.tile_w + (size_t)(lx & ~7)) * 3u + (size_t)(lx & 7);
     }
+}
+
+// The elements of the job's buffer (the checked build's pixel guard, pt_guard.h): the job's rows for
+// the row layouts; the whole image in whole tile rows for the tiled layout, whose index is global.
+template <int LAYOUT>
+__device__ __forceinline__ size_t pixel_extent(const PtJob& j)
+{
+    if (LAYOUT != PT_LAYOUT_TILED_PLANAR8) return (size_t)j.nrows * (size_t)j.width * 3u;
+    const int rows = j.height > j.nrows ? j.height : j.nrows;
+    return (size_t)((rows + j.tile_h - 1) / j.tile_h) * (size_t)j.tile_h * (size_t)j.width * 3u;
 }
 
 // Frame-constant camera terms (mainImage, scalar.cpp:338-351).
@@ -705,7 +716,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
     constexpr uint32_t kNone = PtTileQueue<kWavesPerBlock>::kNone;
     PtTileQueue<kWavesPerBlock> tq(job.queue, job.order, job.units, job.nunits, total_tiles, wv);
     uint32_t tile = kNone, next_tile = kNone;
-    tile = tq.first();   // (the whole wave: uniform, scalar registers)
+    tile = tq.first(job.err);   // (the whole wave: uniform, scalar registers)
     tile = __builtin_amdgcn_readfirstlane(tile);
     while (tile != kNone) {
         // a queue entry is a tile or one half of it (pt_tile_queue.h): the pixels of the other half
@@ -927,7 +938,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 }
                 folded += __popcll(pt_ballot(fnow));
             }
-            next_tile = tq.next();   // the pool is done
+            next_tile = tq.next(job.err);   // the pool is done
         } else {
         // one chunk covers the launch's frames unless MULTI (then the loop carries acc and c_keep)
         for (int f0 = 0; f0 < (MULTI ? S : 1); f0 += CH) {
@@ -1078,7 +1089,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
                 }
             }
             if (DEFER && qn > 0) drain(0, qn);
-            if (f0 + CH >= S) next_tile = tq.next();   // the last chunk's pool is done
+            if (f0 + CH >= S) next_tile = tq.next(job.err);   // the last chunk's pool is done
             // ---------------- phase C: progressive lerp in frame order ----------------
             DIAG_MARK(t_c);
             const int clc = txi * 8 + (lane & 7), clr = tyi * 8 + (lane >> 3);
@@ -1119,7 +1130,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
             px[2 * cs] = acc.z;
         }
         if (job.cost && lane == 0) pt_record_cost(job.cost, this_tile, total_tiles, tile_work);
-        if (S <= 0) next_tile = tq.next();   // no chunk ran (nframes 0)
+        if (S <= 0) next_tile = tq.next(job.err);   // no chunk ran (nframes 0)
         tile = __builtin_amdgcn_readfirstlane(next_tile);
 #if PT_DIAG && !PT_DIAG_WAVES_ONLY
         if (job.counters && lane == 0 && n_tiles_diag <= 32) {
@@ -1131,6 +1142,7 @@ __device__ __forceinline__ void render_body(const PtJob& job)
 #endif
         DIAG_ADD(6, t_tile);
     }
+    tq.report(job.err);   // (a schedule entry outside the launch, pt_tile_queue.h)
     if (COUNT) {
         for (int off = 32; off > 0; off >>= 1) {
             n_seg += __shfl_xor(n_seg, off, 64);
@@ -1283,6 +1295,11 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
 #else
     float* const slots = job.ct_slots + (size_t)(blockIdx.x * kWavesPerBlock + wv) * kCtWaveFloats;
 #endif
+    // (the host launches at most ct_waves waves: launch_ct)
+    if (!PT_GUARD(job.err, blockIdx.x * (uint32_t)kWavesPerBlock + (uint32_t)wv < job.ct_waves, PT_G_SLOT_BASE,
+                  blockIdx.x * (uint32_t)kWavesPerBlock + (uint32_t)wv))
+        return;
+    const size_t px_extent = pixel_extent<LAYOUT>(job);   // (guards only)
     // lerp weight of frame f of the launch: the table, or its correctly rounded reciprocal (:812)
     auto weight = [&](int f) {
         return f < kMaxWeights ? s_w[f] : pt::rcp_rn((float)(job.frame_first + (uint32_t)f) + 1.0f);
@@ -1290,9 +1307,11 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     // the fused output stage: a pixel's final accumulator value -> its 8-bit pixel (OutputToScreen /
     // OutputToFile, v4 :1260-1331; pt_tonemap.h), at the point the launch writes that value
     auto present = [&](int lc, int lr, const V3& acc) {
-        if constexpr (PRESENT)
-            job.pix_out[(size_t)lr * (uint32_t)job.ncols + (uint32_t)lc] =
-                pt_tone::pack<true, true>(acc.x, acc.y, acc.z, job.pix_xrgb != 0);
+        if constexpr (PRESENT) {
+            const size_t o = (size_t)lr * (uint32_t)job.ncols + (uint32_t)lc;
+            if (PT_GUARD(job.err, o < (size_t)job.nrows * (uint32_t)job.ncols, PT_G_PIXOUT, o))
+                job.pix_out[o] = pt_tone::pack<true, true>(acc.x, acc.y, acc.z, job.pix_xrgb != 0);
+        }
     };
 
     Camera cam;
@@ -1384,7 +1403,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             const uint32_t flags = ws_ld(kWsFlags);
             if (flags & 2u) break;   // the queue is done
             PtTileQueue<kWavesPerBlock> tq = PtTileQueue<kWavesPerBlock>::restore(s_tq[wv]);
-            uint32_t tile = (flags & 1u) ? tq.next() : tq.first();
+            uint32_t tile = (flags & 1u) ? tq.next(job.err) : tq.first(job.err);
             tile = __builtin_amdgcn_readfirstlane(tile);
             tq.save(s_tq[wv], lane);
             ws_st(kWsFlags, tile == kNone ? 3u : 1u);   // claimed (and done)
@@ -1430,8 +1449,10 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                     items = B != 0;
                     c_keep = add(zero, mulv(v3(pr.er, pr.eg, pr.eb), one));    // :319 (ret after bounce 0)
                 }
-                if (!items) {   // the same radiance in every frame: fold all of the launch's frames now
-                    float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
+                const size_t pi = out_index<LAYOUT>(job, lc, lr);
+                if (!items && PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) {
+                    // the same radiance in every frame: fold all of the launch's frames now
+                    float* px = job.buf + pi;
                     V3 acc = v3(px[0], px[cs], px[2 * cs]);
                     for (int f = 0; f < S; ++f) acc = add(acc, mul(sub(c_keep, acc), weight(f)));
                     px[0] = acc.x;
@@ -1475,10 +1496,13 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
         if (ENV && lane < m) {
             const float4 e = s_envq[ENV ? wv : 0][q0 + lane][0], r = s_envq[ENV ? wv : 0][q0 + lane][1];
             const V3 c = env_sample(job.env, job.env_w, job.env_h, v3(e.x, e.y, e.z));
-            float* const o = slots + __builtin_bit_cast(int, e.w);
-            o[0] = r.x + c.x;
-            o[1] = r.y + c.y;
-            o[2] = r.z + c.z;
+            const uint32_t a = __builtin_bit_cast(uint32_t, e.w);
+            if (PT_GUARD(job.err, a + 3u <= kCtWaveFloats, PT_G_ITEM_SLOT, a)) {
+                float* const o = slots + a;
+                o[0] = r.x + c.x;
+                o[1] = r.y + c.y;
+                o[2] = r.z + c.z;
+            }
         }
     };
     // Fold D: every item of it has ended, its radiance is in the slots of context 1 - cA
@@ -1505,7 +1529,9 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             const float* fr = (const float*)v;
             const uint32_t tdi = pt_entry_tile(tD);
             const int lc = (int)(tdi % (uint32_t)tiles_x) * 8 + (lane & 7), lr = (int)(tdi / (uint32_t)tiles_x) * 8 + (lane >> 3);
-            float* px = job.buf + out_index<LAYOUT>(job, lc, lr);
+            size_t pi = out_index<LAYOUT>(job, lc, lr);
+            if (!PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) pi = 0;   // (checked build: reported)
+            float* px = job.buf + pi;
             V3 acc = first ? v3(px[0], px[cs], px[2 * cs]) : v3(s_acc[wv][0][lane], s_acc[wv][1][lane], s_acc[wv][2][lane]);
 #pragma unroll
             for (int f = 0; f < kChunk; ++f) {
@@ -1649,7 +1675,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                     done = bounce > B;
                 }
                 if (done) {
-                    if (!queued) {
+                    if (!queued && PT_GUARD(job.err, (uint32_t)it_addr + 3u <= kCtWaveFloats, PT_G_ITEM_SLOT, it_addr)) {
                         float* c = slots + it_addr;
                         c[0] = ret.x;
                         c[1] = ret.y;
@@ -1668,7 +1694,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                     drain(0, qn);
                     qn = 0;
                 }
-                if (queued) {
+                if (queued && PT_GUARD(job.err, qn + nq <= kQ, PT_G_ENVQ, qn + nq)) {
                     const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(qm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)qm, 0u));
                     s_envq[ENV ? wv : 0][qn + r][0] = make_float4(D.x, D.y, D.z, __builtin_bit_cast(float, it_addr));
                     s_envq[ENV ? wv : 0][qn + r][1] = make_float4(ret.x, ret.y, ret.z, 0.0f);
@@ -1702,6 +1728,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
         atomicAdd(&job.err[0], 1u);
         atomicMin(&job.err[1], pt_entry_tile(nitA > 0 ? ws_ld(kWsTcur) : (hasD ? ws_ld(kWsTD) : 0u)));
     }
+    PtTileQueue<kWavesPerBlock>::restore(s_tq[wv]).report(job.err);   // (a schedule entry outside the launch)
 #if PT_DIAG
     if (job.counters && lane == 0) {
         unsigned long long* rec = job.counters + 32 + 4 * (size_t)(blockIdx.x * kWavesPerBlock + wv);
@@ -1907,7 +1934,8 @@ __device__ uint32_t block_exclusive_scan_1024(uint32_t* a, uint32_t* wave_tot)
 
 __global__ __launch_bounds__(1024) void pt_schedule_kernel(const uint32_t* __restrict__ cost, uint32_t* __restrict__ order,
                                                            uint32_t* __restrict__ units, uint32_t* __restrict__ nunits,
-                                                           uint32_t n, uint32_t kUnitCost, uint32_t split_div)
+                                                           uint32_t n, uint32_t kUnitCost, uint32_t split_div,
+                                                           uint32_t* err)
 {
     __shared__ uint32_t hist[kCostBins];    // entries per bin, then the bin's first schedule position
     __shared__ uint32_t ucnt[kCostBins];    // units per bin, then the bin's first unit index
@@ -1968,10 +1996,10 @@ __global__ __launch_bounds__(1024) void pt_schedule_kernel(const uint32_t* __res
         }
         const uint32_t cb = (uint32_t)(kCostBins - 1) - lo;
         const uint32_t pb = cb >= kUnitCost || cb == 0 ? 1u : kUnitCost / cb;
-        units[u] = hist[lo] + (u - ucnt[lo]) * pb;
+        if (PT_GUARD(err, u < 2u * n, PT_G_SCHED_UNIT, u)) units[u] = hist[lo] + (u - ucnt[lo]) * pb;
     }
     __syncthreads();   // hist is advanced by the scatter below
-    if (t == 0) {
+    if (t == 0 && PT_GUARD(err, total_units <= 2u * n && npos <= 2u * n, PT_G_SCHED_UNIT, total_units)) {
         *nunits = total_units;
         units[total_units] = npos;
     }
@@ -1985,12 +2013,16 @@ __global__ __launch_bounds__(1024) void pt_schedule_kernel(const uint32_t* __res
         for (uint32_t k = 0; k < kBatch; ++k) {
             if (cc[k] == kNoTile) continue;
             const uint32_t tile = base + k * nt + t;
+            // (the checked build: every position inside order's 2 n entries)
+            auto put = [&](uint32_t pos, uint32_t e) {
+                if (PT_GUARD(err, pos < 2u * n, PT_G_SCHED_ORDER, pos)) order[pos] = e;
+            };
             if (split(cc[k])) {
                 const uint32_t b = bin_of((cc[k] + 1u) >> 1);
-                order[atomicAdd(&hist[b], 1u)] = tile | (1u << PT_TILE_PART_SHIFT);
-                order[atomicAdd(&hist[b], 1u)] = tile | (2u << PT_TILE_PART_SHIFT);
+                put(atomicAdd(&hist[b], 1u), tile | (1u << PT_TILE_PART_SHIFT));
+                put(atomicAdd(&hist[b], 1u), tile | (2u << PT_TILE_PART_SHIFT));
             } else {
-                order[atomicAdd(&hist[bin_of(cc[k])], 1u)] = tile;
+                put(atomicAdd(&hist[bin_of(cc[k])], 1u), tile);
             }
         }
     }
@@ -1999,7 +2031,7 @@ __global__ __launch_bounds__(1024) void pt_schedule_kernel(const uint32_t* __res
 }  // namespace
 
 hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* units, uint32_t* nunits,
-                              uint32_t ntiles, uint32_t split, uint32_t unit_mult, hipStream_t st)
+                              uint32_t ntiles, uint32_t split, uint32_t unit_mult, hipStream_t st, uint32_t* err)
 {
     if (ntiles == 0) return hipSuccess;
     if (!cost || !order || !units || !nunits) return hipErrorInvalidValue;
@@ -2022,7 +2054,7 @@ hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* u
         split_div = split ? (uint32_t)cus * 20u * split : 0u;
     }
     hipLaunchKernelGGL(pt_schedule_kernel, dim3(1), dim3(1024), 0, st, cost, order, units, nunits, ntiles, unit_cost,
-                       split_div);
+                       split_div, err);
     return hipGetLastError();
 }
 

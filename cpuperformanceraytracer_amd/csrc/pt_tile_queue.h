@@ -39,6 +39,7 @@
 #include <algorithm>
 
 #include "pt_kernel.h"   // PT_NQUEUES
+#include "pt_guard.h"
 
 __device__ __forceinline__ uint32_t pt_entry_tile(uint32_t e) { return e & PT_TILE_MASK; }
 __device__ __forceinline__ uint32_t pt_entry_part(uint32_t e) { return e >> PT_TILE_PART_SHIFT; }
@@ -67,15 +68,18 @@ __device__ __forceinline__ void pt_queue_zero_next(unsigned int* queue_next)
 // kernels' last-dispatched blocks, which the SQ's oldest-first issue leaves the slowest) takes its
 // group's cheapest units, so the launch's last expensive units go to fast waves; a claim is valid
 // while front + back stays below the group's dynamic unit count.
+static_assert(PT_NQUEUES <= 31, "the queue's dead-group mask keeps bit 31 for tile_at's flag");
 template <int WAVES_PER_BLOCK>
 struct PtTileQueue {
     static constexpr uint32_t kNone = 0xffffffffu;
+    static constexpr uint32_t kBadSeen = 0x80000000u;   // dead's flag: tile_at met a bad entry (groups: bits 0-7)
     unsigned int* base;       // PT_NQUEUES 64-bit counters, 128 B apart (zeroed before the launch)
     const uint32_t* order;    // schedule position -> tile, or nullptr (raster order)
     const uint32_t* units;    // unit -> first schedule position (units[u + 1] its end), or nullptr
                               // (order: entries -- tile | part << PT_TILE_PART_SHIFT)
     uint32_t nunits, ntiles, ngroups, qg, wave;
     uint32_t dead = 0;        // groups known to be exhausted
+    uint32_t bad = 0;         // a schedule entry outside the launch's tiles (tile_at: valid when dead's bit 31 is set)
     uint32_t c_pos = kNone, c_end = kNone;   // the current unit's remaining schedule positions
     uint32_t back = 0;        // 1: claim from the back of the own group
 
@@ -92,7 +96,7 @@ struct PtTileQueue {
     // The queue's state as kWords words (a wave's LDS copy: a kernel whose pool loop must not hold
     // the queue in scalar registers keeps it there between dequeues -- render_body_ct).  save: lane 0
     // stores; restore: uniform loads.
-    static constexpr int kWords = 15;
+    static constexpr int kWords = 16;
     __device__ PtTileQueue() = default;
     __device__ void save(uint32_t* w, int lane) const
     {
@@ -111,6 +115,7 @@ struct PtTileQueue {
         w[12] = c_pos;
         w[13] = c_end;
         w[14] = back;
+        w[15] = bad;
     }
     __device__ static PtTileQueue restore(const uint32_t* w)
     {
@@ -129,6 +134,7 @@ struct PtTileQueue {
         q.c_pos = u(12);
         q.c_end = u(13);
         q.back = u(14);
+        q.bad = u(15);
         return q;
     }
     __device__ uint32_t group_waves(uint32_t g) const
@@ -154,11 +160,31 @@ struct PtTileQueue {
     }
     __device__ uint32_t unit_lo(uint32_t u) const { return units ? __builtin_amdgcn_readfirstlane(units[u]) : u; }
     __device__ uint32_t unit_hi(uint32_t u) const { return units ? __builtin_amdgcn_readfirstlane(units[u + 1]) : u + 1; }
-    // (defensive: a schedule entry outside the launch's tiles ends the wave instead of faulting)
-    __device__ uint32_t tile_at(uint32_t i) const
+    // A schedule entry outside the launch's tiles ends the wave instead of faulting, and is kept in
+    // `bad`, which the kernel records in the job's error words when the wave ends, in every build
+    // (report(): guard PT_G_QUEUE_ENTRY, the host returns PT_EKERNEL -- a corrupt entry must not drop
+    // tiles silently; recorded at the end, off the claim path, whose registers the pool loop shares).
+    __device__ uint32_t tile_at(uint32_t i)
     {
         const uint32_t e = order ? __builtin_amdgcn_readfirstlane(order[i]) : i;
-        return pt_entry_tile(e) < ntiles && pt_entry_part(e) < 3u ? e : kNone;
+        if (pt_entry_tile(e) < ntiles && pt_entry_part(e) < 3u) return e;
+        bad = e;
+        dead |= kBadSeen;
+        return kNone;
+    }
+    // the wave's end: a bad entry seen by tile_at into the job's error words (the first active lane)
+    __device__ void report(uint32_t* err) const
+    {
+        if ((dead & kBadSeen) && err &&
+            __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) ==
+                (uint32_t)__builtin_amdgcn_readfirstlane(__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))))
+            pt_guard_report(err, PT_G_QUEUE_ENTRY, bad);
+    }
+    // the checked build: a unit's schedule positions [c_pos, c_end) inside order[] (2 x ntiles
+    // entries with a schedule, ntiles without); err: the job's error words
+    __device__ bool unit_ok(uint32_t* err) const
+    {
+        return PT_GUARD(err, c_pos <= c_end && c_end <= (units ? 2u * ntiles : ntiles), PT_G_UNIT_RANGE, c_end);
     }
 
     __device__ unsigned long long* counter(uint32_t g) const
@@ -197,17 +223,20 @@ struct PtTileQueue {
         return kNone;
     }
     // the first tile of this wave's static unit, kNone if the launch has fewer units than waves
-    __device__ uint32_t first()
+    __device__ uint32_t first(uint32_t* err = nullptr)
     {
+        // (the checked build: a unit count beyond the schedule's 2 x ntiles entries ends every wave)
+        if (!PT_GUARD(err, !units || nunits <= 2u * ntiles, PT_G_NUNITS, nunits)) nunits = 0;
         const uint32_t u0 = qg + ngroups * wave;
         if (u0 >= nunits) return kNone;
         c_pos = unit_lo(u0);
         c_end = unit_hi(u0);
-        return next();
+        if (!unit_ok(err)) return kNone;
+        return next(err);
     }
     // the next tile: the current unit's, or the first of a newly claimed unit; kNone when every
     // unit of every group has been taken
-    __device__ uint32_t next()
+    __device__ uint32_t next(uint32_t* err = nullptr)
     {
         if (c_pos >= c_end) {
             uint32_t u = ((dead >> qg) & 1u) ? kNone
@@ -219,6 +248,7 @@ struct PtTileQueue {
             if (u == kNone) return kNone;
             c_pos = unit_lo(u);
             c_end = unit_hi(u);
+            if (!unit_ok(err)) return kNone;
         }
         return tile_at(c_pos++);
     }

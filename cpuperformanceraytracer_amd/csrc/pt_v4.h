@@ -62,6 +62,7 @@ struct PtV4Job {
     const uint32_t* units;
     const uint32_t* nunits;
     uint32_t* cost;                 // per-tile cost written by this launch, or nullptr
+    uint32_t* err;                  // PT_ERR_WORDS error words (pt_kernel.h), nullptr = not recorded
     // continuous-tiles pool (pt_v4.hip pt_v4_ct_kernel): pt_ct_wave_floats() f32 per wave for ct_waves
     // waves (the diffuse kernels' slot area, pt_kernel.h); nullptr: the per-tile pool kernel
     float* ct_slots;

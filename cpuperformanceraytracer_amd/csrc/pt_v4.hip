@@ -35,6 +35,7 @@
 #include "pt_envcert.h"
 #include "pt_v4_default_scene.h"
 #include "pt_tile_queue.h"
+#include "pt_guard.h"
 #include "pt_wave.h"
 #include "pt_tonemap.h"
 #include <algorithm>
@@ -574,6 +575,16 @@ __device__ __forceinline__ size_t out_index(const PtV4Job& j, int x, int r)   //
            ((size_t)ly * j.tile_w + (size_t)(lx & ~7)) * 3u + (size_t)(lx & 7);
 }
 
+// The elements of the job's buffer (the checked build's pixel guard, pt_guard.h): the job's rows for
+// the row layouts; the whole image in whole tile rows for the tiled layout, whose row index is global.
+template <int LAYOUT>
+__device__ __forceinline__ size_t pixel_extent(const PtV4Job& j)
+{
+    if (LAYOUT != PT_LAYOUT_TILED_PLANAR8) return (size_t)j.nrows * (size_t)j.width * 3u;
+    const int rows = j.height > j.nrows ? j.height : j.nrows;
+    return (size_t)((rows + j.tile_h - 1) / j.tile_h) * (size_t)j.tile_h * (size_t)j.width * 3u;
+}
+
 // One iteration of an item's path: GetColorForRay's bounce loop, :733-909 (the pool kernels' shared
 // body).  done: the path ended (queued: DEFER, the miss's env term is deferred to the queue's drain).
 template <int ENV, bool COUNT, bool DEF, int FEXP, bool DFL>
@@ -816,7 +827,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     constexpr uint32_t kNone = PtTileQueue<kWaves>::kNone;
     PtTileQueue<kWaves> tq(job.queue, job.order, job.units, job.nunits, (uint32_t)ntiles, wv);
     uint32_t tile = kNone, next_tile = kNone;
-    tile = tq.first();   // (the whole wave: uniform, scalar registers)
+    tile = tq.first(job.err);   // (the whole wave: uniform, scalar registers)
     tile = __builtin_amdgcn_readfirstlane(tile);
     while (tile != kNone) {
     // (this kernel's schedules hold whole tiles: pt_capi.cpp v4_launch)
@@ -971,7 +982,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
             }
         }
         if (DEFER && qn > 0) drain(qn);
-        if (c0 + kChunk >= job.nframes) next_tile = tq.next();   // the last pool is done
+        if (c0 + kChunk >= job.nframes) next_tile = tq.next(job.err);   // the last pool is done
         // all radiance of this chunk is in LDS (written by lanes of this wave)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -991,7 +1002,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (job.nframes <= 0) next_tile = tq.next();   // no chunk ran
+    if (job.nframes <= 0) next_tile = tq.next(job.err);   // no chunk ran
     if (pvalid) {
         acc_p[0] = acc.x;
         acc_p[cs] = acc.y;
@@ -1001,6 +1012,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_OCC void pt_v4_kernel(PtV4Job jo
     if (job.cost && lane == 0) pt_record_cost(job.cost, tile, (uint32_t)ntiles, tile_work);
     tile = __builtin_amdgcn_readfirstlane(next_tile);
     }
+    tq.report(job.err);   // (a schedule entry outside the launch, pt_tile_queue.h)
     if (COUNT) {
         // per-lane counts summed over the wave by lane 0's atomics
         for (int off = 32; off > 0; off >>= 1) {
@@ -1070,6 +1082,11 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
     const uint32_t ntiles = (uint32_t)tiles_x * (uint32_t)((job.nrows + 7) >> 3);
     const int S = job.nframes;
     float* const slots = job.ct_slots + (size_t)(blockIdx.x * kWaves + wv) * kV4CtWaveFloats;
+    // (the host launches at most ct_waves waves: pt_launch_v4)
+    if (!PT_GUARD(job.err, blockIdx.x * (uint32_t)kWaves + (uint32_t)wv < job.ct_waves, PT_G_SLOT_BASE,
+                  blockIdx.x * (uint32_t)kWaves + (uint32_t)wv))
+        return;
+    const size_t px_extent = pixel_extent<LAYOUT>(job);   // (guards only)
     const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;
     const Tex tex{job.env, job.env_w, job.env_h};
     const bool random = DFL || job.random_jitter != 0, rejection = DFL || job.rejection != 0;
@@ -1120,6 +1137,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
         if (ENV == PT_V4_ENV_EQUIRECT_) amb = equirect(tex, d, random, r);
         if (ENV == PT_V4_ENV_CUBEMAP_) amb = cubemap(tex, d, random, r);
         const V3 rt = v3(fma_(amb.x, t.x, rs.x), fma_(amb.y, t.y, rs.y), fma_(amb.z, t.z, rs.z));   // :787
+        if (!PT_GUARD(job.err, k >= 0 && (uint32_t)k + 3u <= kV4CtWaveFloats, PT_G_ITEM_SLOT, k)) return;
         float* const o = slots + k;
         o[0] = fma_(rt.x, 1.0f, 0.0f);   // :1127
         o[1] = fma_(rt.y, 1.0f, 0.0f);
@@ -1168,7 +1186,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
             const uint32_t flags = ws_ld(kVwFlags);
             if (flags & 2u) break;   // the queue is done
             PtTileQueue<kWaves> tq = PtTileQueue<kWaves>::restore(s_tq[wv]);
-            uint32_t tile = (flags & 1u) ? tq.next() : tq.first();
+            uint32_t tile = (flags & 1u) ? tq.next(job.err) : tq.first(job.err);
             tile = __builtin_amdgcn_readfirstlane(tile);
             tq.save(s_tq[wv], lane);
             ws_st(kVwFlags, tile == kNone ? 3u : 1u);
@@ -1193,7 +1211,9 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
             int fsky = 0;
             if (DEF) {
                 const int orow = LAYOUT == PT_LAYOUT_TILED_PLANAR8 ? job.row_start + pr * job.row_stride : pr;
-                float* const acc_p = valid ? job.buf + out_index<LAYOUT>(job, X, orow) : nullptr;
+                size_t pi = valid ? out_index<LAYOUT>(job, X, orow) : 0;
+                if (valid && !PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) pi = 0;   // (checked build: reported)
+                float* const acc_p = valid ? job.buf + pi : nullptr;
                 V3 acc = v3(0.0f, 0.0f, 0.0f);
                 if (valid && job.accumulate) acc = v3(acc_p[0], acc_p[cs], acc_p[2 * cs]);
                 for (; fsky < S; ++fsky) {
@@ -1253,7 +1273,9 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
             const int tcol = ((int)pt_entry_tile(tD) % tiles_x) * 8, trow = ((int)pt_entry_tile(tD) / tiles_x) * 8;
             const int px = job.col0 + tcol + (lane & 7), pr = trow + (lane >> 3);
             const int orow = LAYOUT == PT_LAYOUT_TILED_PLANAR8 ? job.row_start + pr * job.row_stride : pr;
-            float* const acc_p = job.buf + out_index<LAYOUT>(job, px, orow);
+            size_t pi = out_index<LAYOUT>(job, px, orow);
+            if (!PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) pi = 0;   // (checked build: reported)
+            float* const acc_p = job.buf + pi;
             V3 acc = v3(0.0f, 0.0f, 0.0f);
             if (first) {
                 if (job.accumulate) acc = v3(acc_p[0], acc_p[cs], acc_p[2 * cs]);   // (:1233: only to blend)
@@ -1369,7 +1391,9 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
                                                        dir, T, ret, rng, bounce, done, queued, n_seg, n_esc, n_fb, n_sky);
                 if (done) {
                     qslot = slot;
-                    if (!(DEFER && queued)) {   // mainImage :1127: fmadd(color, 1/c_numRendersPerFrame, 0)
+                    if (!(DEFER && queued) &&
+                        PT_GUARD(job.err, slot >= 0 && (uint32_t)slot + 3u <= kV4CtWaveFloats, PT_G_ITEM_SLOT, slot)) {
+                        // mainImage :1127: fmadd(color, 1/c_numRendersPerFrame, 0)
                         float* const o = slots + slot;
                         o[0] = fma_(ret.x, 1.0f, 0.0f);
                         o[1] = fma_(ret.y, 1.0f, 0.0f);
@@ -1426,6 +1450,13 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
         }
     }
     if (__builtin_expect(fault, 0) && DEFER && qn > 0) drain(qn);
+    // a fault ends the wave with its chunks unfinished: recorded in the job's error words (the host
+    // returns PT_EKERNEL), as the diffuse pool's
+    if (__builtin_expect(fault, 0) && lane == 0 && job.err) {
+        atomicAdd(&job.err[0], 1u);
+        atomicMin(&job.err[1], pt_entry_tile(ws_ld(kVwTcur)));
+    }
+    PtTileQueue<kWaves>::restore(s_tq[wv]).report(job.err);   // (a schedule entry outside the launch)
     if (COUNT) {
         for (int off = 32; off > 0; off >>= 1) {
             n_seg += __shfl_down(n_seg, off);

@@ -177,6 +177,9 @@ int32_t pt_initialized_device(void);
  * they ran on, this reports PT_EKERNEL if any launch since the last check abandoned a tile (every
  * host-buffer entry point makes the same check before it returns). */
 int pt_check_device_errors(void);
+/* 1 if this library is the bounds-checked diagnostic build (-DPT_CHECKED=1: every global index of the
+ * continuous-tiles pools and the schedule builder is tested and reported as PT_EKERNEL), else 0 */
+int32_t pt_build_checked(void);
 int32_t pt_device_count(void);               /* logical devices (0 before pt_init)             */
 int32_t pt_device_ordinal(int32_t index);    /* HIP ordinal of logical device `index`, or -1    */
 

@@ -56,3 +56,24 @@ def mismatch_report(a: np.ndarray, b: np.ndarray) -> str:
         return "identical"
     d = np.abs(a[bad].astype(np.float64) - b[bad]).max(1)
     return f"{len(bad)} of {len(a)} pixels differ; first {bad[:5].tolist()}, max |d| {d.max():.3g}"
+
+
+@pytest.fixture(autouse=True)
+def _device_errors_after_gpu_test(request):
+    """After every -m gpu test: synchronise the device and read the kernels' error words
+    (pt_check_device_errors).  An asynchronous fault is then reported by the test whose work caused it,
+    not by whichever later test synchronises first (the round-5 r05z3 illegal address surfaced in the
+    test after the pinned work-queue tests), and a launch whose pool or bounds guards fired fails its
+    own test even when its image was not compared."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    from cpuperformanceraytracer_amd import _native as N
+    if getattr(N, "_lib", None) is None:
+        return
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    rc = N.load().pt_check_device_errors()
+    if rc != N.PT_OK:
+        pytest.fail(f"device error words after the test: {N.load().pt_last_error().decode(errors='replace')}")

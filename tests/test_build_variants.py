@@ -11,6 +11,7 @@
   PT_AMBIENT_WAVES=4, PT_V4_WAVES=5  occupancy A/B builds
   PT_RING_MIN=9                     every MULTI launch on the ring pool (its parity run: all 130 GPU
                                     tests bit-exact, profiles/r03x_gpu_tests.txt)
+  PT_CHECKED=1                      the bounds-guarded build (pt_guard.h; build.build_checked)
 Every other alternate measured slower was removed from the sources (DESIGN.md records the numbers).
 """
 from __future__ import annotations
@@ -37,6 +38,8 @@ VARIANTS = [
     ("pt_kernel.hip", ["PT_RING_MIN=9"]),
     ("pt_v4.hip", ["PT_EC_FORCE_EXACT=1"]),
     ("pt_capi.cpp", ["PT_DIAG=1"]),
+    ("pt_kernel.hip", ["PT_CHECKED=1"]),
+    ("pt_v4.hip", ["PT_CHECKED=1"]),
 ]
 
 
