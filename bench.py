@@ -344,6 +344,22 @@ class HostOps:
         return torch.zeros(n, dtype=torch.float32)
 
 
+def reduce_values(vals, op, *, world: int, dev, rehearse: bool = False, force_collective: bool = False) -> list:
+    """vals (numbers) reduced over the ranks with the ReduceOp `op`: an all-reduce of one f64 tensor, on
+    the rank's device under RCCL (nccl), in host memory under gloo (CPU tests, PT_BENCH_REHEARSE).  One
+    rank returns the values themselves, unless force_collective (the RCCL call an N-GPU run makes,
+    executed on one GPU by tests/test_gpu_rccl.py).  Counts stay exact below 2^53."""
+    import torch
+    import torch.distributed as dist
+    if world == 1 and not force_collective:
+        return [float(v) for v in vals]
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64)
+    if not rehearse and str(dev) != "cpu" and dist.get_backend() == "nccl":
+        t = t.to(dev)
+    dist.all_reduce(t, op=op)
+    return [float(v) for v in t.tolist()]
+
+
 def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: bool = False,
         roofline: bool = True) -> dict | None:
     """The timed job of one rank (both scaling modes); returns rank 0's result dict (None elsewhere).
@@ -373,15 +389,7 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
         return gather_rows(buf.cpu() if rehearse else buf, Wg, Hg, rank, world)
 
     def all_ranks(vals, op):
-        """vals reduced over the ranks (op: a torch.distributed ReduceOp); the values themselves when
-        world == 1.  Device tensors under RCCL, host tensors under gloo."""
-        if world == 1:
-            return list(vals)
-        t = torch.tensor(list(vals), dtype=torch.float64)
-        if not rehearse and ops.dev != "cpu" and dist.get_backend() == "nccl":
-            t = t.to(ops.dev)
-        dist.all_reduce(t, op=op)
-        return [float(v) for v in t.tolist()]
+        return reduce_values(vals, op, world=world, dev=ops.dev, rehearse=rehearse)
 
     # Device warm-up, untimed, before the W warmup steps: the MI355X reaches its steady clocks only
     # after ~25 ms of sustained load (per-launch time at 1080p, 8 spp: 0.46 ms over the first 20
@@ -460,11 +468,7 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
         if world > 1:
             gather_ms = ops.elapsed_ms(g0, g1)
     if world > 1:
-        t = torch.tensor([elapsed, gather_ms, launch_ms_avg], dtype=torch.float64)
-        if not rehearse and ops.dev != "cpu" and dist.get_backend() == "nccl":
-            t = t.to(ops.dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, gather_ms, launch_ms_avg = float(t[0]), float(t[1]), float(t[2])
+        elapsed, gather_ms, launch_ms_avg = all_ranks([elapsed, gather_ms, launch_ms_avg], dist.ReduceOp.MAX)
         if rank == 0:
             assert full is not None and tuple(full.shape) == (Hg, Wg, 3)
 
@@ -510,11 +514,8 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
         sky += c.get("sky_skipped", 0)
     del scratch
     if world > 1:   # whole-job work: summed over ranks
-        t = torch.tensor([segs, samples, slots, prim, escaped, sky], dtype=torch.float64)
-        if not rehearse and ops.dev != "cpu" and dist.get_backend() == "nccl":
-            t = t.to(ops.dev)
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        segs, samples, slots, prim, escaped, sky = (int(v) for v in t.tolist())
+        segs, samples, slots, prim, escaped, sky = (
+            int(v) for v in all_ranks([segs, samples, slots, prim, escaped, sky], dist.ReduceOp.SUM))
     if rank != 0:
         return None
 

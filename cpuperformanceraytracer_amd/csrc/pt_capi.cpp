@@ -66,6 +66,7 @@ struct Sched {
     hipEvent_t tune_ev[2 * 18] = {};
     uint32_t tuned = 0;           // timed launches enqueued
     uint32_t narms = 0;           // arms timed (2 or 3; 0: not started)
+    int32_t tune_nframes = 0;     // the frames of the first timed launch: only launches of that length are timed
     int8_t wide = -1;             // the pick: arm index (-1: not yet)
 };
 constexpr uint32_t kTuneRounds = 3;   // rounds of the palindromic arm order timed; the first is discarded
@@ -718,7 +719,7 @@ int use_ct_slots(Dev& dv, const LaunchSched& ls, hipStream_t st, float** slots, 
 // *tev: the event pair to record around this launch while it is timed.
 constexpr uint32_t kBackWide = 45;
 constexpr uint32_t kEnvBack[3] = {0, 33, 45};   // env arms 1, 2 (arm 0: the default share)
-int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
+int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev, bool count)
 {
     *tev = nullptr;
     j.ct_wide = g.ct_waves == 6 ? 1u : 0u;
@@ -737,19 +738,25 @@ int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev)
         j.ct_wide = arm != 0 ? 1u : 0u;
         if (arm == 2 && j.ct_back_pct != 0) j.ct_back_pct = kBackWide;   // (launches that take back claims)
     };
-    if (!s->narms) s->narms = (j.env || (j.ct_back_pct != 0 && !g.back_set)) ? 3u : 2u;
-    const uint32_t per_round = s->narms == 3 ? 6u : 4u, nt = kTuneRounds * per_round;
+    // only uncounted launches of the first timed launch's length are timed: a counted launch (the
+    // bench's work-count pass) or one of another length sharing the geometry's schedule would bias the
+    // arms' sums; they run the interim choice below.  The first timed launch fixes the
+    // arms (and the length).
+    const bool timeable = !count && (s->tune_nframes == 0 || s->tune_nframes == j.nframes);
+    if (!s->narms && timeable) s->narms = (j.env || (j.ct_back_pct != 0 && !g.back_set)) ? 3u : 2u;
+    const uint32_t per_round = s->narms == 3 ? 6u : 4u, nt = s->narms ? kTuneRounds * per_round : 0u;
     static constexpr int kOrder3[6] = {0, 1, 2, 2, 1, 0};
     const auto arm_of = [&](uint32_t t) { return s->narms == 3 ? kOrder3[t % 6] : (int)((t ^ (t >> 1)) & 1u); };
     if (s->wide >= 0) {
         apply(s->wide);
-    } else if (s->tuned < nt) {
+    } else if (s->tuned < nt && timeable) {
+        s->tune_nframes = j.nframes;
         hipEvent_t* ev = &s->tune_ev[2 * s->tuned];
         for (int i = 0; i < 2; ++i)
             if (!ev[i]) HIP_TRY(hipEventCreate(&ev[i]));
         apply(arm_of(s->tuned++));
         *tev = ev;
-    } else if (hipEventQuery(s->tune_ev[2 * nt - 1]) == hipSuccess) {
+    } else if (nt && s->tuned >= nt && hipEventQuery(s->tune_ev[2 * nt - 1]) == hipSuccess) {
         float t[3] = {0.f, 0.f, 0.f};
         for (uint32_t i = per_round; i < nt; ++i) {
             float ms = 0.f;
@@ -792,7 +799,7 @@ int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
     // env 16 spp 0.4967 vs 0.5030, 4K 8 spp 0.8217 vs 0.8309; 4K 64 spp 5.913 vs 5.763: not there)
     j.ct_back_pct = j.nframes <= 16 ? g.ct_back_pct : 0u;
     hipEvent_t* tev = nullptr;
-    if ((rc = ct_occupancy(ls, j, &tev))) return rc;
+    if ((rc = ct_occupancy(ls, j, &tev, count))) return rc;
     if (tev) HIP_TRY(hipEventRecord(tev[0], st));
     hipError_t e = pt_launch_render(j, st, count);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
@@ -1818,6 +1825,11 @@ int pt_launch_variant(const pt_device_job* dj, int32_t* waves, int32_t* back_pct
     }
     SchedKey key = sched_key(j);
     key.split = j.nframes <= 8 ? g.split : 0u;
+    if (key.ntiles < kSchedMinTiles) {   // never scheduled, never timed: the fixed fallback (ct_occupancy)
+        *waves = j.env ? pt_ct_env_waves() : 5;
+        *back_pct = (int32_t)dflt;
+        return PT_OK;
+    }
     for (const Sched& s : dv->sched) {
         if (!s.used || !(s.key == key) || s.wide < 0) continue;
         if (j.env) {

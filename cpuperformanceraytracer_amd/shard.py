@@ -25,12 +25,14 @@ def max_rows(world: int, height: int) -> int:
     return (height + world - 1) // world
 
 
-def gather_rows(sub, width: int, height: int, rank: int, world: int, dst: int = 0, group=None):
+def gather_rows(sub, width: int, height: int, rank: int, world: int, dst: int = 0, group=None,
+                force_collective: bool = False):
     """Gather every rank's compact sub-image (nrows x width x 3, rows rank::world) to `dst` and
     un-interleave into the full height x width x 3 image there (None on other ranks).
 
     `sub` must hold max_rows(world, height) rows (the tail row of shorter shards is padding) so
-    that every rank sends the same byte count."""
+    that every rank sends the same byte count.  One rank returns its sub-image without a collective,
+    unless force_collective (tests: the RCCL call an N-GPU run makes, executed on one GPU)."""
     import torch
     import torch.distributed as dist
 
@@ -38,7 +40,7 @@ def gather_rows(sub, width: int, height: int, rank: int, world: int, dst: int = 
     sub = sub.reshape(-1)
     if sub.numel() != mr * width * 3:
         raise ValueError(f"sub-image must hold {mr} rows of {width}x3 floats, got {sub.numel()}")
-    if world == 1:
+    if world == 1 and not force_collective:
         return sub.view(height, width, 3)
     # the root receives every rank's sub-image into one (world, mr, W*3) tensor; rank r's row k is the
     # global row k * world + r, so the un-interleave is ONE transposing copy (world, mr) -> (mr, world)

@@ -129,10 +129,12 @@ def test_split_schedules_match_oracle(monkeypatch, pool, env, frames):
 @pytest.mark.parametrize("waves", ["5", "6", "0"])
 def test_ct_occupancy_variants_match_oracle(monkeypatch, waves):
     """The diffuse continuous-tiles kernel at 5 and 6 waves per SIMD (PT_MI355_CT_WAVES, read by
-    pt_init) runs the same per-pixel code, and "0" -- the per-geometry timing, which alternates the
-    two grids on a geometry's first 8 scheduled launches and then keeps the faster -- changes the
-    grid between the launches of one accumulation: 12 launches of 2 frames of one scheduled geometry
-    equal the oracle bit for bit in every mode (tests/test_gpu_regime.py: the same at bench sizes)."""
+    pt_init) runs the same per-pixel code, and "0" -- the per-geometry timing, which times the arms
+    (5 / 6 waves, and 6 waves at 45 % back claims for launches that take them) on a geometry's first
+    12-18 scheduled launches in palindromic order, then keeps the fastest -- changes the grid between
+    the launches of one accumulation: 12 launches of 2 frames of one scheduled geometry equal the
+    oracle bit for bit in every mode (tests/test_gpu_regime.py: the same at bench sizes, including
+    launches after the pick)."""
     import torch
     import cpuperformanceraytracer_amd as pt
     from cpuperformanceraytracer_amd.device import render_device

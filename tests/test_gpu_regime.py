@@ -31,10 +31,12 @@ K_SCHED_REBUILD = 64   # pt_capi.cpp kSchedRebuild
 
 
 def _launch_series(W, H, B, S, launches, *, row_start=0, row_stride=1, nrows=None, env=False, count_at=(),
-                   v4=False):
+                   v4=False, sync_at=()):
     """`launches` JobLauncher launches of S frames (frames 1 .. launches*S) into a zeroed buffer, on
     the current stream, as bench.py's render_fn; at the launch indices in count_at also a counted
-    launch on a scratch buffer of the same geometry (bench.py's count pass).  Returns the image."""
+    launch on a scratch buffer of the same geometry (bench.py's count pass); after the launch indices
+    in sync_at a device synchronisation (the timed arms' events are then complete, so the next
+    launch takes the pick).  Returns the image."""
     import torch
     from cpuperformanceraytracer_amd.device import JobLauncher, check_device_errors, count_device, count_v4_device
     nrows = H if nrows is None else nrows
@@ -50,6 +52,8 @@ def _launch_series(W, H, B, S, launches, *, row_start=0, row_stride=1, nrows=Non
         if k in count_at:
             cfn(scratch, W, H, frame_first=frame, nframes=S, num_bounces=B, row_start=row_start,
                 row_stride=row_stride, nrows=nrows, use_env=env, stream=stream)
+        if k in sync_at:
+            torch.cuda.synchronize()
         frame += S
     torch.cuda.synchronize()
     check_device_errors()
@@ -80,8 +84,9 @@ def fresh(monkeypatch):
 
 def test_c2_bench_regime_matches_oracle(fresh):
     """configs[1] as bench.py times it: 1920x1080, 8 spp per launch, 8 bounces, 70 prepared-job
-    launches (unscheduled, scheduled, rebuilt at launch 65) with counted launches interleaved; the
-    whole image after 560 frames equals the oracle bit for bit."""
+    launches (unscheduled, scheduled -- the first 18 timing the launch variant's arms --, rebuilt at
+    launch 65) with counted launches interleaved; the whole image after 560 frames equals the oracle
+    bit for bit."""
     W, H, B, S = 1920, 1080, 8, 8
     fresh(B)
     img, frames = _launch_series(W, H, B, S, K_SCHED_REBUILD + 6, count_at=(5, 40))
@@ -91,14 +96,22 @@ def test_c2_bench_regime_matches_oracle(fresh):
 
 
 def test_c2_occupancy_timing_matches_oracle(fresh):
-    """PT_MI355_CT_WAVES=0: the first 8 scheduled launches of the geometry alternate the 5- and
-    6-waves-per-SIMD grids (1280 / 1536 blocks) between event pairs, then the faster is kept --
-    the grid changes between the launches of one accumulation; 24 launches of configs[1] equal the
-    oracle on sampled rows."""
+    """PT_MI355_CT_WAVES=0 (the default): the geometry's first 18 scheduled uncounted launches time the
+    three arms (5 waves / 6 waves per SIMD at the default 20 % back claims / 6 waves at 45 %) in the
+    palindromic order ABCCBA, three rounds, between event pairs (pt_capi.cpp ct_occupancy); a counted
+    launch in between is not timed; after a synchronisation the next launch takes the pick, and the
+    launches after it run the picked arm -- the grid and the back-claim share change between the
+    launches of one accumulation.  30 launches of configs[1]: rows equal the oracle, and the pick is
+    one of the arms (pt_launch_variant)."""
+    import torch
+    from cpuperformanceraytracer_amd.device import launch_variant
     W, H, B, S = 1920, 1080, 8, 8
     fresh(B, PT_MI355_CT_WAVES="0")
-    img, frames = _launch_series(W, H, B, S, 24)
+    img, frames = _launch_series(W, H, B, S, 30, count_at=(7,), sync_at=(21,))
     _check_rows(img, W, H, frames, B, range(27, H, 108))
+    buf = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda:0")
+    v = launch_variant(buf, W, H, nframes=S, num_bounces=B)
+    assert (v["waves_per_simd"], v["back_claim_pct"]) in ((5, 20), (6, 20), (6, 45)), v
 
 
 @pytest.mark.parametrize("seq", ["5665", "56"])
