@@ -1289,12 +1289,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     const uint32_t total_tiles = (uint32_t)tiles_x * (uint32_t)((job.nrows + 7) >> 3);
     const int S = job.nframes, B = job.num_bounces;
     const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;   // channel stride
-#if PT_CT_SLOT_ALIAS   // timing-only A/B build (wrong images): every XCD's waves share 32 waves' slots,
-                      // which stay in its L2 -- what the slot area's fabric traffic costs
-    float* const slots = job.ct_slots + (size_t)((blockIdx.x % 8u) * kWavesPerBlock + wv) * kCtWaveFloats;
-#else
     float* const slots = job.ct_slots + (size_t)(blockIdx.x * kWavesPerBlock + wv) * kCtWaveFloats;
-#endif
     // (the host launches at most ct_waves waves: launch_ct)
     if (!PT_GUARD(job.err, blockIdx.x * (uint32_t)kWavesPerBlock + (uint32_t)wv < job.ct_waves, PT_G_SLOT_BASE,
                   blockIdx.x * (uint32_t)kWavesPerBlock + (uint32_t)wv))
@@ -1860,7 +1855,16 @@ hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
     // job.pix_out themselves)
     bool presented = false;
     hipError_t e;
-    if (count ? launch_ct<LAYOUT, ENV, true>(job, st, tiles, &presented) : launch_ct<LAYOUT, ENV, false>(job, st, tiles, &presented))
+    // counted launches are device jobs (pt_capi.cpp pt_count_device: the row layouts only), so the
+    // tiled layout has no counting instances
+    constexpr bool kCountable = LAYOUT != PT_LAYOUT_TILED_PLANAR8;
+    if (!kCountable && count) return hipErrorInvalidValue;
+    bool ct;
+    if constexpr (kCountable)
+        ct = count ? launch_ct<LAYOUT, ENV, true>(job, st, tiles, &presented) : launch_ct<LAYOUT, ENV, false>(job, st, tiles, &presented);
+    else
+        ct = launch_ct<LAYOUT, ENV, false>(job, st, tiles, &presented);
+    if (ct)
         e = hipGetLastError();
     else
         e = launch_pools<LAYOUT, ENV>(job, st, count, tiles);
@@ -1875,7 +1879,11 @@ hipError_t launch_pools(const PtJob& job, hipStream_t st, bool count, unsigned t
 {
     const bool multi = job.nframes > kChunk;
     const bool ring = !ENV && job.nframes >= kRingMinFrames && job.nframes > kChunk;
-    if (count) {
+    if constexpr (LAYOUT == PT_LAYOUT_TILED_PLANAR8) {   // (no counting instances: launch_t)
+        if (ring) launch_k<LAYOUT, ENV, false, true, !ENV>(job, st, tiles);
+        else if (multi) launch_k<LAYOUT, ENV, false, true>(job, st, tiles);
+        else launch_k<LAYOUT, ENV, false, false>(job, st, tiles);
+    } else if (count) {
         if (ring) launch_k<LAYOUT, ENV, true, true, !ENV>(job, st, tiles);
         else if (multi) launch_k<LAYOUT, ENV, true, true>(job, st, tiles);
         else launch_k<LAYOUT, ENV, true, false>(job, st, tiles);
@@ -2066,25 +2074,24 @@ uint32_t pt_ct_resident_waves()
 {
     static_assert(waves_per_block<false>() == waves_per_block<true>(), "one block shape for the CT kernels");
     constexpr int wpb = waves_per_block<false>();
-    const int r[18] = {pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, false, 5>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, true, 5>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, false, 5>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, true, 5>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, false, 5>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, true, 5>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, false, 6>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, true, 6>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, false, 6>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, true, 6>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, false, 6>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, true, 6>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_INTERLEAVED, false>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_INTERLEAVED, true>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_PLANAR8, false>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_PLANAR8, true>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_TILED_PLANAR8, false>, 64 * wpb),
-                       pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_TILED_PLANAR8, true>, 64 * wpb)};
-    return (uint32_t)*std::max_element(r, r + 18) * (uint32_t)wpb;
+    // (every continuous-tiles instance launch_ct can pick; the presenting ones have the plain ones'
+    // occupancy attributes and LDS, and launch_ct checks the grid against ct_waves anyway)
+    const int r[] = {pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, false, 5>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, true, 5>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, false, 5>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, true, 5>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, false, 5>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, false, 6>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_INTERLEAVED, true, 6>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, false, 6>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_PLANAR8, true, 6>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_kernel<PT_LAYOUT_TILED_PLANAR8, false, 6>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_INTERLEAVED, false>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_INTERLEAVED, true>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_PLANAR8, false>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_PLANAR8, true>, 64 * wpb),
+                     pt_resident_blocks(pt_render_ct_env_kernel<PT_LAYOUT_TILED_PLANAR8, false>, 64 * wpb)};
+    return (uint32_t)*std::max_element(std::begin(r), std::end(r)) * (uint32_t)wpb;
 }
 
 hipError_t pt_launch_render(const PtJob& job_in, hipStream_t st, bool count)

@@ -763,10 +763,7 @@ __device__ __forceinline__ void v4_segment(const PtV4Job& job, const PtV4Scene& 
 // 32 spp 1.247 vs 1.261, 4K 8 spp 1.272 vs 1.296 -- and ahead of the per-tile kernel (0.3602,
 // 1.260, 1.298) at all three.  The instance with the reference's default flags (DFL) only: the
 // others spill in their pool loops at 80 VGPRs and keep 5 waves.
-#ifndef PT_V4_CT_DFL_WAVES
-#define PT_V4_CT_DFL_WAVES 6   // (A/B builds: -DPT_V4_CT_DFL_WAVES=k)
-#endif
-#define PT_V4_CT_OCC __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : (DFL ? PT_V4_CT_DFL_WAVES : 5))))
+#define PT_V4_CT_OCC __attribute__((amdgpu_waves_per_eu(COUNT ? 1 : (DFL ? 6 : 5))))
 #endif
 // FEXP: USE_FAST_APPROXIMATE_EXP as a compile-time switch (1 fast, 0 exact) for the render
 // instances -- the exact expf's registers in the Beer branch would otherwise raise the kernel from
@@ -1505,7 +1502,24 @@ hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool 
             return hipGetLastError();
         }
     }
-    if (j.default_scene) {
+    // The tiled layout is the drop-in's (pt_capi.cpp pt_render_opt_v4 and its work-queue entries): one
+    // frame per call (NUM_SAMPLES_PER_FRAME = 1), never counted (counted launches are device jobs, the
+    // row layouts only) -- so only the per-tile pool's uncounted instances exist for it.
+    if constexpr (LAYOUT == PT_LAYOUT_TILED_PLANAR8) {
+        if (count || j.nframes >= kChunk) return hipErrorInvalidValue;
+        const auto tile_go = [&](auto kern) {
+            const long blocks = std::min<long>(pt_resident_blocks(kern, 64 * kWaves), (tiles + kWaves - 1) / kWaves);
+            hipLaunchKernelGGL(kern, dim3((unsigned)blocks), block, 0, st, j, sc);
+        };
+        if (j.default_scene) {
+            if (j.fast_exp && j.random_jitter && j.rejection) tile_go(pt_v4_kernel<ENV, LAYOUT, false, true, 1, true>);
+            else if (j.fast_exp) tile_go(pt_v4_kernel<ENV, LAYOUT, false, true, 1>);
+            else tile_go(pt_v4_kernel<ENV, LAYOUT, false, true, 0>);
+        } else {
+            if (j.fast_exp) tile_go(pt_v4_kernel<ENV, LAYOUT, false, false, 1>);
+            else tile_go(pt_v4_kernel<ENV, LAYOUT, false, false, 0>);
+        }
+    } else if (j.default_scene) {
         if (count) go(pt_v4_kernel<ENV, LAYOUT, true, true, 2>, pt_v4_ct_kernel<ENV, LAYOUT, true, true, 2>);
         else if (j.fast_exp && j.random_jitter && j.rejection)
             go(pt_v4_kernel<ENV, LAYOUT, false, true, 1, true>, pt_v4_ct_kernel<ENV, LAYOUT, false, true, 1, true>);

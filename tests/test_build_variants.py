@@ -72,7 +72,7 @@ def test_no_removed_alternates_left():
                "PT_V4_IEEE_DIV", "PT_V4_SPHERE_CLOSEST", "PT_V4_SPHERE_ORDER", "PT_V4_UNIFIED_DIR",
                "PT_V4_SKY_SKIP", "PT_V4_FORCE_GENERIC", "PT_SQRT_MARKSTEIN", "PT_SCHED_REBUILD", "PT_RING_PM",
                "PT_RING_ANY", "PT_RING_FOLDK", "PT_X_ENV_AMB", "PT_X_ENV_SPHC", "PT_V4_T_NOENV", "PT_V4_T_NOTRIG",
-               "PT_V4_T_FLAGS"]
+               "PT_V4_T_FLAGS", "PT_V4_CT_DFL_WAVES", "PT_CT_SLOT_ALIAS"]
     import re
     for f in list(CSRC.glob("*.hip")) + list(CSRC.glob("*.h")) + list(CSRC.glob("*.cpp")):
         text = f.read_text()
