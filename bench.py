@@ -62,6 +62,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c2_1080p")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-chain", action="store_true",
+                    help="diffuse workloads: plain pt_render_device steps, one after the other, instead of chained "
+                         "launches (pt_render_device_chain) that overlap consecutive steps")
     ap.add_argument("--no-configs4", action="store_true",
                     help="default workload: skip the configs[4] strong-scaling leg (c5_8k, a few steps)")
     ap.add_argument("--device-warmup-ms", type=float, default=60.0,
@@ -361,12 +364,17 @@ def reduce_values(vals, op, *, world: int, dev, rehearse: bool = False, force_co
 
 
 def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: bool = False,
-        roofline: bool = True) -> dict | None:
+        roofline: bool = True, chain_counts=None) -> dict | None:
     """The timed job of one rank (both scaling modes); returns rank 0's result dict (None elsewhere).
 
     render_fn(buf, Wg, Hg, frame_first, nframes, row_start, row_stride, nrows) renders asynchronously
     into buf; count_fn(...) the same, synchronously, returning the work counters.  Multi-rank runs
-    need torch.distributed initialised (RCCL, or gloo when rehearsing / on CPU)."""
+    need torch.distributed initialised (RCCL, or gloo when rehearsing / on CPU).
+    chain_counts: () -> {"restarts", "continued"} (pt_chain_counts) when render_fn takes chain=True
+    (pt_render_device_chain): the weak-scaling steps are then chained launches -- consecutive steps
+    overlap on the GPU, each pixel's frames still folded in order -- and the line reports
+    how many of the timed launches continued the overlap.  Strong-scaling steps (a gather of the image
+    between them) are never chained."""
     import torch
     import torch.distributed as dist
     from cpuperformanceraytracer_amd import roofline as RL
@@ -382,8 +390,11 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
     verify_rows = args.verify_rows if args.verify_rows is not None else (2 if rehearse else 0)
     frame = 1
 
+    chained = chain_counts is not None and not strong
+    chain_kw = {"chain": True} if chained else {}
+
     def step(f):
-        render_fn(buf, Wg, Hg, f, S, row_start, row_stride, nrows)
+        render_fn(buf, Wg, Hg, f, S, row_start, row_stride, nrows, **chain_kw)
 
     def gather():
         return gather_rows(buf.cpu() if rehearse else buf, Wg, Hg, rank, world)
@@ -427,6 +438,7 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
     timed_first = frame
     full = None
     render_ms = gather_ms = 0.0
+    cc0 = chain_counts() if chained else None
     t0 = time.perf_counter()
     if strong:
         for k in range(K):
@@ -460,6 +472,7 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
     ops.sync()
     elapsed = time.perf_counter() - t0
     timed_end = frame
+    cc1 = chain_counts() if chained else None
     lo, hi = all_ranks([-timed_end, timed_end], dist.ReduceOp.MAX)
     if -lo != hi:   # (the invariant the gathered image and its check rely on)
         raise AssertionError(f"the ranks accumulated different frame ranges: ends {-lo:.0f} .. {hi:.0f}")
@@ -564,6 +577,15 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
                 "note": "SQ_INSTS_VALU of the committed PMC pass over this run's kernel time and the 1024 SIMDs; "
                         "2-cycle f32 ops issue at ~1.0 per SIMD per ns, the 4-cycle class (compares, selects, "
                         "min/max, f64, conversions) at ~0.58 (DESIGN.md §3)"}
+    launch_chain = {"enabled": False}
+    if chained:
+        launch_chain = {"enabled": True, "timed_restarts": cc1["restarts"] - cc0["restarts"],
+                        "timed_continued": cc1["continued"] - cc0["continued"],
+                        "note": "pt_render_device_chain: consecutive steps overlap on two streams (the next "
+                                "launch's waves fill the CUs the finishing ones free); a launch touches a tile "
+                                "only after the previous one stored it, so every pixel's frames fold in order "
+                                "(DESIGN.md 3e).  kernel_ms_avg is then the per-step time of the overlapped "
+                                "launches, not one launch's duration"}
     res = {
         "metric": metric_label(wl.width, wl.height),
         "value": value,
@@ -592,6 +614,7 @@ def run(args, wl, rank: int, world: int, ops, render_fn, count_fn, *, rehearse: 
         "ref_segments_per_sample": (segs if v4 else RL.ref_segments(segs, prim, samples)) / samples,
         "simd_lane_efficiency": segs / slots if slots else None,
         "sky_skipped_traces_per_launch": sky / K * per_rank,
+        "launch_chain": launch_chain,
         "kernel_ms_avg": avg_kernel_s * 1e3,
         "kernel_ms_source": ("per step: HIP events around the render launch on its stream (max over ranks)" if strong
                              else "HIP events bracketing the K timed launches on their stream, interval / K"),
@@ -662,8 +685,10 @@ class Hooks:
     -> dict, rank 0's output-stage measurement on its accumulator (None: skipped); cpu_baseline()
     -> dict (None: skipped)."""
 
-    def __init__(self, check_errors=None, launch_variant=None, output_stage=None, cpu_baseline=None):
+    def __init__(self, check_errors=None, launch_variant=None, output_stage=None, cpu_baseline=None,
+                 chain_counts=None):
         self.check_errors = check_errors or (lambda: None)
+        self.chain_counts = chain_counts   # (bench.run: render_fn takes chain=True)
         self.launch_variant = launch_variant
         self.output_stage = output_stage
         self.cpu_baseline = cpu_baseline
@@ -679,7 +704,7 @@ def drive(args, wl, rank: int, world: int, ops, render_fn, count_fn, hooks: Hook
     left rank 0 waiting in its all-reduce: ADVICE round 5).  leg_workload: the strong leg's workload
     (default configs[4], c5_8k; tests pass a tiny one)."""
     from cpuperformanceraytracer_amd.shard import rows_of
-    res = run(args, wl, rank, world, ops, render_fn, count_fn, rehearse=rehearse)
+    res = run(args, wl, rank, world, ops, render_fn, count_fn, rehearse=rehearse, chain_counts=hooks.chain_counts)
     hooks.check_errors()   # no launch of the run abandoned a tile (PT_EKERNEL otherwise)
     acc = None
     if res is not None:
@@ -762,8 +787,8 @@ def main() -> None:
 
     from cpuperformanceraytracer_amd.config import CONFIGS, synthetic_env
     from cpuperformanceraytracer_amd.shard import rows_of
-    from cpuperformanceraytracer_amd.device import (JobLauncher, check_device_errors, count_device, count_v4_device,
-                                                    ensure_backend, launch_variant, set_env_map)
+    from cpuperformanceraytracer_amd.device import (JobLauncher, chain_counts, check_device_errors, count_device,
+                                                    count_v4_device, ensure_backend, launch_variant, set_env_map)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -799,12 +824,12 @@ def main() -> None:
     # step to step), so the host enqueues a step in a few microseconds
     launchers = {}
 
-    def render_fn(buf, Wg, Hg, f, n, rs, st, nr):
-        key = (buf.data_ptr(), Wg, Hg, n, rs, st, nr)
+    def render_fn(buf, Wg, Hg, f, n, rs, st, nr, chain=False):
+        key = (buf.data_ptr(), Wg, Hg, n, rs, st, nr, chain)
         launch = launchers.get(key)
         if launch is None:
             launch = launchers[key] = JobLauncher(buf, Wg, Hg, nframes=n, num_bounces=B, row_start=rs, row_stride=st,
-                                                  nrows=nr, use_env=wl.env, stream=stream, v4=v4)
+                                                  nrows=nr, use_env=wl.env, stream=stream, v4=v4, chain=chain)
         launch(f)
 
     def count_fn(buf, Wg, Hg, f, n, rs, st, nr):
@@ -835,7 +860,9 @@ def main() -> None:
                                                                      row_start=rs, row_stride=st, nrows=nr,
                                                                      use_env=wl.env)),
                   output_stage=output_stage,
-                  cpu_baseline=lambda: cpu_baseline(wl, args.cpu_seconds, env))
+                  cpu_baseline=lambda: cpu_baseline(wl, args.cpu_seconds, env),
+                  # the diffuse renderer's steps are chained launches (pt_render_device_chain) unless --no-chain
+                  chain_counts=None if v4 or args.no_chain else chain_counts)
     res = drive(args, wl, rank, world, ops, render_fn, count_fn, hooks, rehearse=rehearse)
     if rank == 0:
         print(json.dumps(res))

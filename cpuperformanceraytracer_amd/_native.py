@@ -37,7 +37,7 @@ EXPORTED_SYMBOLS = (
     "pt_init", "pt_shutdown", "pt_last_error", "pt_default_config", "pt_set_frame", "pt_get_frame",
     "pt_render_scalar", "pt_render_simd", "pt_render_simd_tiled", "pt_render_tile", "pt_begin_frame",
     "pt_readback", "pt_gather_root", "pt_unpin_host", "pt_release_buffer", "pt_initialized_device", "pt_check_device_errors", "pt_build_checked", "pt_device_count",
-    "pt_device_ordinal", "pt_render_device", "pt_count_device", "pt_render_device_present", "pt_launch_variant",
+    "pt_device_ordinal", "pt_render_device", "pt_render_device_chain", "pt_chain_counts", "pt_count_device", "pt_render_device_present", "pt_launch_variant",
     "pt_load_texture", "pt_decode_hdr", "pt_free_texture", "pt_set_env_map", "pt_render_simt_textured",
     "pt_tonemap", "pt_tonemap_device", "pt_write_bmp", "pt_load_cubemap_texture",
     "pt_v4_default_config", "pt_v4_set_config", "pt_v4_get_config", "pt_v4_initialize_global_render_resources",
@@ -165,6 +165,8 @@ def load() -> ctypes.CDLL:
         "pt_render_device": (i32, [ctypes.POINTER(PtDeviceJob), vp]),
         "pt_count_device": (i32, [ctypes.POINTER(PtDeviceJob), vp, ctypes.POINTER(PtWorkCounts)]),
         "pt_render_device_present": (i32, [ctypes.POINTER(PtDeviceJob), vp, i32, vp]),
+        "pt_render_device_chain": (i32, [ctypes.POINTER(PtDeviceJob), vp]),
+        "pt_chain_counts": (i32, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
         "pt_launch_variant": (i32, [ctypes.POINTER(PtDeviceJob), ctypes.POINTER(i32), ctypes.POINTER(i32)]),
         "pt_load_texture": (i32, [ctypes.c_char_p, ctypes.POINTER(PtTexture)]),
         "pt_decode_hdr": (i32, [vp, ctypes.c_size_t, ctypes.POINTER(PtTexture)]),

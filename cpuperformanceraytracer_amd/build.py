@@ -55,20 +55,49 @@ def _stale(target: Path, deps) -> bool:
     return any(Path(d).stat().st_mtime > t for d in deps)
 
 
+def _compile_link(out: Path, flags, tag: str, verbose: bool = False) -> None:
+    """Compile SOURCES to objects in parallel (one hipcc per file: the same translation units as one
+    hipcc call over all of them) under build/obj/<tag>/, then link the shared library `out`."""
+    from concurrent.futures import ThreadPoolExecutor
+    objdir = ROOT / "build" / "obj" / tag
+    objdir.mkdir(parents=True, exist_ok=True)
+    base = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *flags, f"-I{ROOT / 'include'}",
+            f"-I{CSRC}", "-Wno-unused-function"]
+
+    deps = [CSRC / h for h in HEADERS] + [ROOT / "include" / "pt_mi355.h", ROOT / "include" / "demofox_path_tracing_mi355.h"]
+
+    def one(src):
+        obj = objdir / (src + ".o")
+        cmd = [*base, "-c", str(CSRC / src), "-o", str(obj)]
+        stamp = obj.with_suffix(".cmd")
+        # (an object is reused when it is newer than its source and every header, and was built by the same command)
+        if obj.exists() and stamp.exists() and stamp.read_text() == " ".join(cmd) and not _stale(obj, [CSRC / src, *deps]):
+            return obj
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        stamp.write_text(" ".join(cmd))
+        return obj
+
+    # the largest translation units first
+    order = sorted(SOURCES, key=lambda f: -(CSRC / f).stat().st_size)
+    with ThreadPoolExecutor(max_workers=min(len(order), os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(one, order))
+    tmp = str(out) + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", tmp]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, out)
+
+
 def build_lib(force: bool = False, verbose: bool = False) -> Path:
     deps = [CSRC / s for s in SOURCES + HEADERS] + [ROOT / "include" / "pt_mi355.h",
                                                      ROOT / "include" / "demofox_path_tracing_mi355.h",
                                                      Path(__file__)]
     if not force and not _stale(LIB, deps):
         return LIB
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           *PARITY_FLAGS, *PERF_FLAGS, f"-I{ROOT / 'include'}", f"-I{CSRC}",
-           "-Wall", "-Wno-unused-function",
-           *[str(CSRC / s) for s in SOURCES], "-o", str(LIB) + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(str(LIB) + ".tmp", LIB)
+    _compile_link(LIB, [*PARITY_FLAGS, *PERF_FLAGS, "-Wall"], "lib", verbose)
     return LIB
 
 
@@ -77,10 +106,7 @@ def build_variant(name: str, defines=(), extra=()) -> Path:
     PT_MI355_LIB=...); used for kernel A/B experiments."""
     out = ROOT / "build" / f"libpt_{name}.so"
     out.parent.mkdir(exist_ok=True)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           *PARITY_FLAGS, *PERF_FLAGS, *[f"-D{d}" for d in defines], *extra, f"-I{ROOT / 'include'}", f"-I{CSRC}",
-           "-Wno-unused-function", *[str(CSRC / s) for s in SOURCES], "-o", str(out)]
-    subprocess.run(cmd, check=True)
+    _compile_link(out, [*PARITY_FLAGS, *PERF_FLAGS, *[f"-D{d}" for d in defines], *extra], f"v_{name}")
     return out
 
 
@@ -92,13 +118,7 @@ def build_checked(force: bool = False, verbose: bool = False) -> Path:
     if not force and not _stale(CHECKED_LIB, deps):
         return CHECKED_LIB
     CHECKED_LIB.parent.mkdir(exist_ok=True)
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", *PARITY_FLAGS, *PERF_FLAGS,
-           "-DPT_CHECKED=1", f"-I{ROOT / 'include'}", f"-I{CSRC}", "-Wall", "-Wno-unused-function",
-           *[str(CSRC / s) for s in SOURCES], "-o", str(CHECKED_LIB) + ".tmp"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(str(CHECKED_LIB) + ".tmp", CHECKED_LIB)
+    _compile_link(CHECKED_LIB, [*PARITY_FLAGS, *PERF_FLAGS, "-DPT_CHECKED=1", "-Wall"], "checked", verbose)
     return CHECKED_LIB
 
 

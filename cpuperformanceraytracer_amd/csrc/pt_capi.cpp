@@ -68,6 +68,10 @@ struct Sched {
     uint32_t narms = 0;           // arms timed (2 or 3; 0: not started)
     int32_t tune_nframes = 0;     // the frames of the first timed launch: only launches of that length are timed
     int8_t wide = -1;             // the pick: arm index (-1: not yet)
+    // chained launches (launch_chain): per half-tile, the chain sequence number of the last launch
+    // that stored its pixels (2 ntiles words), and that number of the geometry's last chained launch
+    uint32_t* epoch = nullptr;
+    uint32_t chain_seq = 0;
 };
 constexpr uint32_t kTuneRounds = 3;   // rounds of the palindromic arm order timed; the first is discarded
 constexpr int kSchedSlots = 16;
@@ -116,6 +120,25 @@ struct Dev {
     size_t dgather_cap = 0;
     hipEvent_t ev_gather = nullptr;     // recorded after this device's rows were stored
     bool peer_root = false;             // this device may store into the root's memory
+    // chained launches (pt_render_device_chain, launch_chain): consecutive launches of one geometry
+    // alternate on two streams of the library's and overlap on the GPU
+    struct Chain {
+        hipStream_t st[2] = {};            // the two streams (non-blocking)
+        hipEvent_t done[2] = {};           // recorded after each stream's last launch
+        bool pending[2] = {};              // done[i] has been recorded
+        hipEvent_t ev_caller = nullptr;    // the caller's stream at a chain (re)start
+        float* area1 = nullptr;            // a second continuous-tiles slot area (the first: dct)
+        unsigned int* qblk = nullptr;      // 4 tile-queue blocks of the continuing launches
+        // blocks started by every chained launch so far (monotonic: a stream gate that is evaluated
+        // before a restart's launch has started -- its stream waits only for the gate -- must not pass
+        // on a count from before the restart), and the blocks those launches have
+        unsigned long long* started = nullptr;
+        unsigned long long cum = 0;
+        Sched* sched = nullptr;            // the live chain's geometry (nullptr: the next chained launch restarts)
+        int area = 0;                      // slot area of the live chain's last launch (0: dct, 1: area1)
+        int par = 0;                       // stream of the live chain's last launch
+        unsigned long long restarts = 0, continued = 0;   // chained launches of each kind (pt_chain_counts)
+    } chain;
 };
 
 // The host buffer the device mirrors currently represent, and the geometry they were split by.
@@ -169,6 +192,7 @@ struct State {
     uint32_t split = 1;   // PT_MI355_SPLIT (read by pt_init): tile split factor of the schedule (0: none)
     int64_t test_bad_entry = -1;   // PT_MI355_TEST_BAD_ENTRY (test hook, pt_init)
     bool no_ct = false;   // PT_MI355_NO_CT=1 (read by pt_init): one-chunk launches on render_body (A/B)
+    uint32_t test_chain_delay = 0;   // PT_MI355_TEST_CHAIN_DELAY=<us> (pt_init): chained launches publish late
 };
 
 State g;
@@ -320,6 +344,7 @@ const char* guard_name(uint32_t id)
         case PT_G_SCHED_UNIT: return "schedule builder: unit index out of range";
         case PT_G_RECORD: return "item record slot >= 64";
         case PT_G_QUEUE_GROUP: return "queue group out of range";
+        case PT_G_CHAIN_WAIT: return "chained launch: the previous launch's tile never became ready";
         default: return "unknown";
     }
 }
@@ -495,6 +520,10 @@ PtJob base_job(float* buf, int32_t w, int32_t h)
     j.ct_back_pct = 0;   // (launch(): launches of <= 16 frames)
     j.ct_wide = 0;
     j.scene = nullptr;
+    j.tile_epoch = nullptr;
+    j.chain_seq = 0;
+    j.chain_wait = 0;
+    j.started = nullptr;
     return j;
 }
 
@@ -503,6 +532,7 @@ void free_sched(Sched& s)
     if (s.cost) (void)hipFree(s.cost);
     if (s.order) (void)hipFree(s.order);
     if (s.units) (void)hipFree(s.units);
+    if (s.epoch) (void)hipFree(s.epoch);
     for (hipEvent_t e : s.tune_ev)
         if (e) (void)hipEventDestroy(e);
     s = Sched{};
@@ -556,6 +586,7 @@ Sched* find_sched(Dev& dv, const SchedKey& key, hipStream_t st)
     }
     if (lru->used) {   // evict: its buffers may still be read by a launch (its stream may be gone)
         (void)hipDeviceSynchronize();
+        if (dv.chain.sched == lru) dv.chain.sched = nullptr;   // (its chain ends: the next chained launch restarts)
         free_sched(*lru);
     }
     Sched s;
@@ -597,11 +628,34 @@ struct LaunchSched {
     uint32_t* cost = nullptr;
     Sched* sched = nullptr;
 };
-// split: the schedule builder's tile split factor (pt_launch_schedule; 0: whole tiles)
-int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls, uint32_t split)
+// Order `st` after every chained launch of the device and end the live chain (launch_chain): a
+// launch that is not a continuing chained one may use what the chained launches use -- the slot
+// areas, the geometry's schedule, the accumulator.
+int chain_join(Dev& dv, hipStream_t st)
+{
+    for (int i = 0; i < 2; ++i) {
+        if (!dv.chain.pending[i]) continue;
+        if (hipEventQuery(dv.chain.done[i]) == hipSuccess) {
+            dv.chain.pending[i] = false;
+        } else {
+            (void)hipGetLastError();   // (hipErrorNotReady)
+            HIP_TRY(hipStreamWaitEvent(st, dv.chain.done[i], 0));
+        }
+    }
+    dv.chain.sched = nullptr;
+    return PT_OK;
+}
+
+// split: the schedule builder's tile split factor (pt_launch_schedule; 0: whole tiles).  *sched_st: the
+// stream that identifies the geometry's schedule (launch_chain: the caller's stream, which may be the
+// null stream; nullptr: st).
+int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls, uint32_t split,
+              const hipStream_t* sched_st = nullptr)
 {
     *ls = LaunchSched{};
-    if (Sched* s = find_sched(dv, key, st)) {
+    int rc;
+    if ((rc = chain_join(dv, st))) return rc;
+    if (Sched* s = find_sched(dv, key, sched_st ? *sched_st : st)) {
         // (re)build the schedule from the last launch's costs on the 2nd launch of a geometry and
         // then every kSchedRebuild launches (the costs of a fixed view barely change; the builder
         // is a one-workgroup kernel of ~57 us at 1080p)
@@ -677,16 +731,22 @@ int queue_done(Dev& dv, unsigned slot, hipStream_t st, bool zeroed_next)
 
 // The continuous-tiles pools' slot area (pt_kernel.hip render_body_ct, pt_v4.hip pt_v4_ct_kernel) for
 // a launch in ring slot ls.slot on `st`: nullptr (the per-tile pool kernels) with PT_MI355_NO_CT=1.
+// The device's slot area (Dev::dct), allocated on first use: 12 KiB per wave of the resident grid
+// (~75 MB).  Left null when the allocation fails (the per-tile pools then: correct, slower).
+void ct_area_alloc(Dev& dv)
+{
+    if (dv.dct) return;
+    const uint32_t w = pt_ct_resident_waves();
+    if (hipMalloc(&dv.dct, (size_t)w * pt_ct_wave_floats() * sizeof(float)) == hipSuccess) dv.dct_waves = w;
+    else dv.dct = nullptr, (void)hipGetLastError();
+}
+
 int use_ct_slots(Dev& dv, const LaunchSched& ls, hipStream_t st, float** slots, uint32_t* waves)
 {
     *slots = nullptr;
     *waves = 0;
     if (g.no_ct) return PT_OK;
-    if (!dv.dct) {   // once per device: 12 KiB per wave of the resident grid (~60 MB)
-        const uint32_t w = pt_ct_resident_waves();
-        if (hipMalloc(&dv.dct, (size_t)w * pt_ct_wave_floats() * sizeof(float)) == hipSuccess) dv.dct_waves = w;
-        else dv.dct = nullptr, (void)hipGetLastError();   // (the per-tile pools then: correct, slower)
-    }
+    ct_area_alloc(dv);
     *slots = dv.dct;
     *waves = dv.dct_waves;
     if (dv.dct) {   // launches on several streams share the slots: one after the other
@@ -775,7 +835,8 @@ int ct_occupancy(const LaunchSched& ls, PtJob& j, hipEvent_t** tev, bool count)
     return PT_OK;
 }
 
-int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
+// *ct_blocks (optional): the continuous-tiles grid launched (0: none); sched_st: see use_sched.
+int launch(Dev& dv, PtJob j, hipStream_t st, bool count, uint32_t* ct_blocks = nullptr, const hipStream_t* sched_st = nullptr)
 {
     LaunchSched ls;
     int rc;
@@ -783,7 +844,7 @@ int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
     // each, and the pool's two chunk contexts then wait on each other: 1080p 16 spp 0.452 vs 0.437 ms)
     SchedKey key = sched_key(j);
     key.split = j.nframes <= 8 ? g.split : 0u;
-    if ((rc = use_dev(dv)) || (rc = use_sched(dv, key, st, &ls, key.split))) return rc;
+    if ((rc = use_dev(dv)) || (rc = use_sched(dv, key, st, &ls, key.split, sched_st))) return rc;
     j.scene = dv.dscene;
     j.queue = ls.queue;
     j.queue_next = ls.queue_next;
@@ -801,10 +862,135 @@ int launch(Dev& dv, PtJob j, hipStream_t st, bool count)
     hipEvent_t* tev = nullptr;
     if ((rc = ct_occupancy(ls, j, &tev, count))) return rc;
     if (tev) HIP_TRY(hipEventRecord(tev[0], st));
-    hipError_t e = pt_launch_render(j, st, count);
+    hipError_t e = pt_launch_render(j, st, count, ct_blocks);
     if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
     if (tev) HIP_TRY(hipEventRecord(tev[1], st));
     return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_render's early return)
+}
+
+// Chained launches (pt_render_device_chain).  A progressive renderer launches the same geometry again
+// and again; back to back on one stream, each launch's end leaves the chip partly idle (c2: the queue
+// runs dry ~170 us into a ~234 us launch and the last waves finish their chunks while the others have
+// exited).  Consecutive chained launches alternate between two streams, so the next
+// launch's blocks take the CUs the finishing waves free.  Each pixel's frames still fold in order:
+// the kernel touches a tile's pixels only after the previous launch has stored them (the tile epochs,
+// render_body_ct), and nothing else passes between the two launches -- each has its own tile-queue
+// block, slot area and started counter, and the schedule they share is read-only while they overlap.
+// Deadlock freedom: a launch waits only for its predecessor's tiles, and its stream starts it only
+// after every block of the predecessor has started (hipStreamWaitValue64 on the chain's started
+// counter), so the oldest running launch never waits and all of its waves are resident: it completes,
+// then the next oldest, and so on (the kernel's bounded wait is a report, not a mechanism).
+// A chained launch RESTARTS the chain -- its stream waits for the caller's stream and every chained
+// launch before it, as a plain launch would -- when another launch came between (any launch on the
+// device ends the live chain: chain_join), on the geometry's first launches (schedule not built, launch
+// variant being timed), when it builds the schedule or records the costs it is built from, or when it
+// is not a continuous-tiles launch.  Otherwise it CONTINUES: it does not wait for the caller's stream
+// (the caller promises that nothing enqueued there since its previous chained call is needed by this
+// one, include/pt_mi355.h) -- only for its predecessor's blocks to have started.  Every chained launch
+// is joined back into the caller's stream (it waits for the launch's event), so work the caller
+// enqueues afterwards sees it complete.
+int chain_setup(Dev& dv, Sched& sc)
+{
+    Dev::Chain& c = dv.chain;
+    for (int i = 0; i < 2; ++i) {
+        if (!c.st[i]) HIP_TRY(hipStreamCreateWithFlags(&c.st[i], hipStreamNonBlocking));
+        if (!c.done[i]) HIP_TRY(hipEventCreateWithFlags(&c.done[i], hipEventDisableTiming));
+    }
+    if (!c.ev_caller) HIP_TRY(hipEventCreateWithFlags(&c.ev_caller, hipEventDisableTiming));
+    if (!c.qblk && hipMalloc(&c.qblk, 4 * PT_QUEUE_WORDS * sizeof(unsigned)) != hipSuccess)
+        return fail(PT_ENOMEM, "hipMalloc(chain queue blocks) failed");
+    if (!c.started) {   // (never reset: a gate evaluated early must not see a count from before a restart)
+        if (hipMalloc(&c.started, sizeof(unsigned long long)) != hipSuccess)
+            return fail(PT_ENOMEM, "hipMalloc(chain counter) failed");
+        HIP_TRY(hipMemset(c.started, 0, sizeof(unsigned long long)));
+        c.cum = 0;
+    }
+    if (!c.area1 && dv.dct &&
+        hipMalloc(&c.area1, (size_t)dv.dct_waves * pt_ct_wave_floats() * sizeof(float)) != hipSuccess)
+        return fail(PT_ENOMEM, "hipMalloc(second slot area) failed");
+    if (!sc.epoch) {
+        if (hipMalloc(&sc.epoch, 2 * (size_t)sc.key.ntiles * sizeof(uint32_t)) != hipSuccess)
+            return fail(PT_ENOMEM, "hipMalloc(tile epochs) failed");
+        HIP_TRY(hipMemset(sc.epoch, 0, 2 * (size_t)sc.key.ntiles * sizeof(uint32_t)));
+        sc.chain_seq = 0;
+    }
+    return PT_OK;
+}
+
+int launch_chain(Dev& dv, PtJob j, hipStream_t s)
+{
+    int rc;
+    if ((rc = use_dev(dv))) return rc;
+    SchedKey key = sched_key(j);
+    key.split = j.nframes <= 8 ? g.split : 0u;
+    // (the continuous-tiles pool and a scheduled geometry: the tile epochs live in its schedule)
+    Sched* sc = g.no_ct || j.ncols <= 0 || j.nrows <= 0 || j.nframes <= 0 ? nullptr : find_sched(dv, key, s);
+    if (!sc) return launch(dv, j, s, false);
+    ct_area_alloc(dv);
+    if ((rc = chain_setup(dv, *sc))) return rc;
+    Dev::Chain& c = dv.chain;
+    if (!dv.dct || !c.area1) return launch(dv, j, s, false);
+    // what launch()'s use_sched / ct_occupancy would do for this launch
+    const bool builds = sc->have_cost && (!sc->built || sc->launches % kSchedRebuild == 0);
+    const bool records = !sc->built || (sc->launches + 1) % kSchedRebuild == 0;
+    const bool env_arms = j.env && j.nframes <= 16 && g.ct_back_pct != 0 && !g.back_set;
+    const bool variant_fixed = g.ct_waves || g.ct_seq_len || sc->wide >= 0 || (j.env && !env_arms);
+    // (a launch that records the tile costs may continue: the overlapped launches before it do not write
+    // them, and the next launch, which builds the schedule from them, restarts)
+    const bool cont = c.sched == sc && sc->built && !builds && variant_fixed;
+    const uint32_t seq = sc->chain_seq + 1;
+    const int par = cont ? c.par ^ 1 : 0;
+    hipStream_t X = c.st[par];
+    j.tile_epoch = sc->epoch;
+    j.chain_seq = seq;
+    j.started = c.started;
+    j.chain_delay = g.test_chain_delay;
+    uint32_t blocks = 0;
+    if (!cont) {
+        // restart: after the caller's stream and every chained launch (launch()'s use_sched joins them)
+        HIP_TRY(hipEventRecord(c.ev_caller, s));
+        HIP_TRY(hipStreamWaitEvent(X, c.ev_caller, 0));
+        if ((rc = chain_join(dv, X))) return rc;
+        HIP_TRY(hipMemsetAsync(c.qblk, 0, 4 * PT_QUEUE_WORDS * sizeof(unsigned), X));
+        j.chain_wait = 0;
+        if ((rc = launch(dv, j, X, false, &blocks, &s))) return rc;   // (slot area dct)
+        c.area = 0;
+    } else {
+        // continue: once every block of the previous launch has started
+        HIP_TRY(hipStreamWaitValue64(X, c.started, c.cum, hipStreamWaitValueGte, ~0ull));
+        j.chain_wait = seq - 1;
+        j.scene = dv.dscene;
+        j.queue = c.qblk + (size_t)(seq % 4u) * PT_QUEUE_WORDS;
+        j.queue_next = c.qblk + (size_t)((seq + 2u) % 4u) * PT_QUEUE_WORDS;   // (the launch after next: this stream's)
+        j.order = sc->order;
+        j.units = sc->units;
+        j.nunits = sc->units + 2 * sc->key.ntiles + 1;
+        j.cost = records ? sc->cost : nullptr;
+        if (records) sc->have_cost = true;
+        j.err = dv.derr;
+        c.area ^= 1;
+        j.ct_slots = c.area ? c.area1 : dv.dct;
+        j.ct_waves = dv.dct_waves;
+        j.ct_back_pct = j.nframes <= 16 ? g.ct_back_pct : 0u;
+        LaunchSched ls;
+        ls.sched = sc;
+        hipEvent_t* tev = nullptr;
+        if ((rc = ct_occupancy(ls, j, &tev, false))) return rc;
+        ++sc->launches;
+        hipError_t e = pt_launch_render(j, X, false, &blocks);
+        if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
+    }
+    c.cum += blocks;
+    sc->chain_seq = seq;
+    ++(cont ? c.continued : c.restarts);
+    HIP_TRY(hipEventRecord(c.done[par], X));
+    c.pending[par] = true;
+    HIP_TRY(hipStreamWaitEvent(s, c.done[par], 0));
+    // a launch that did not run the continuous-tiles pool published no epochs and counted no blocks:
+    // the next chained launch restarts
+    c.sched = blocks ? sc : nullptr;
+    c.par = par;
+    return PT_OK;
 }
 
 void unpin()
@@ -1335,6 +1521,14 @@ void free_dev(Dev& dv)
         if (sc.used) free_sched(sc);
     for (hipEvent_t& e : dv.queue_event)
         if (e) (void)hipEventDestroy(e);
+    for (int i = 0; i < 2; ++i) {
+        if (dv.chain.st[i]) (void)hipStreamSynchronize(dv.chain.st[i]), (void)hipStreamDestroy(dv.chain.st[i]);
+        if (dv.chain.done[i]) (void)hipEventDestroy(dv.chain.done[i]);
+    }
+    if (dv.chain.ev_caller) (void)hipEventDestroy(dv.chain.ev_caller);
+    if (dv.chain.area1) (void)hipFree(dv.chain.area1);
+    if (dv.chain.qblk) (void)hipFree(dv.chain.qblk);
+    if (dv.chain.started) (void)hipFree(dv.chain.started);
     if (dv.stream) (void)hipStreamDestroy(dv.stream);
     dv = Dev{};
 }
@@ -1453,6 +1647,7 @@ int pt_init(const pt_config* cfg)
     g.frame = 0;
     g.ring_guard_cap = ~0u;
     g.no_ct = getenv("PT_MI355_NO_CT") && !strcmp(getenv("PT_MI355_NO_CT"), "1");
+    g.test_chain_delay = getenv("PT_MI355_TEST_CHAIN_DELAY") ? (uint32_t)strtoul(getenv("PT_MI355_TEST_CHAIN_DELAY"), nullptr, 10) : 0u;
     g.v4_ct_force = getenv("PT_MI355_V4_CT") && !strcmp(getenv("PT_MI355_V4_CT"), "1");
     g.ct_back_pct = 20;
     g.back_set = false;
@@ -1788,6 +1983,31 @@ int pt_render_device(const pt_device_job* dj, void* stream)
 #else
     return launch(*dv, j, (hipStream_t)stream, false);
 #endif
+}
+
+int pt_render_device_chain(const pt_device_job* dj, void* stream)
+{
+    int rc;
+    PtJob j;
+    Dev* dv = nullptr;
+    DeviceGuard guard;
+    if ((rc = ensure_init()) || (rc = device_job(dj, &j)) || (rc = dev_of(dj->buf, &dv))) return rc;
+    if (dj->use_env) j.env = dv->denv;
+#if PT_DIAG
+    if (getenv("PT_DIAG_OUT")) return pt_render_device(dj, stream);   // (the diagnostic timeline: one launch)
+#endif
+    return launch_chain(*dv, j, (hipStream_t)stream);
+}
+
+int pt_chain_counts(uint64_t* restarts, uint64_t* continued)
+{
+    if (!restarts || !continued) return fail(PT_EINVAL, "null output");
+    *restarts = *continued = 0;
+    for (int d = 0; d < (g.inited ? g.ndev : 0); ++d) {
+        *restarts += g.dev[d].chain.restarts;
+        *continued += g.dev[d].chain.continued;
+    }
+    return PT_OK;
 }
 
 int pt_render_device_present(const pt_device_job* dj, uint32_t* pixels, int32_t format, void* stream)

@@ -61,6 +61,18 @@ struct PtJob {
     // same correctly rounded f32 operations: W, H, 1/W, 1/H, W/H, 1/(W/H).  Kernel arguments are
     // scalar registers; computed in the kernel they were VGPRs that the tile loop spilled.
     float cam_W, cam_H, cam_yW, cam_yH, cam_aspect, cam_yAspect;
+    // chained launches (pt_render_device_chain; pt_capi.cpp launch_chain): consecutive launches of one
+    // geometry run overlapped on two streams, so the next launch's waves fill the CUs the finishing
+    // ones free.  The only data one launch needs from the one before is a tile's accumulator values
+    // (the lerp chain of :812): a launch touches a tile's pixels only after the previous launch has
+    // stored them -- per half-tile epochs, stored after the tile's last pixel stores (`sc1` stores,
+    // vmcnt(0), an `sc1` epoch store; MI355X_MICROARCH.md hand-off row 1) and polled with `sc1`
+    // loads.  The continuous-tiles kernels only (render_body_ct).
+    uint32_t* tile_epoch;          // 2 x tiles words (halves: rows 0-3, 4-7); nullptr: not chained
+    uint32_t chain_seq;            // stored into a tile's epochs once its pixels are final
+    uint32_t chain_wait;           // touch a tile's pixels only once its epochs are >= chain_wait (0: none)
+    unsigned long long* started;   // + 1 per block at its start: the next launch's stream gate (nullptr: none)
+    uint32_t chain_delay;          // test hook (PT_MI355_TEST_CHAIN_DELAY): ~us a wave sleeps before publishing
 };
 
 // Kernel error words (PtJob::err, PtV4Job::err; reset by the host after it reports them, pt_capi.cpp
@@ -84,6 +96,7 @@ enum PtGuardId : uint32_t {
     PT_G_SCHED_UNIT = 10,   // the schedule builder: a unit index > 2 x tiles
     PT_G_RECORD = 11,       // a tile's item record slot >= 64
     PT_G_QUEUE_GROUP = 12,  // a queue group counter beyond PT_NQUEUES
+    PT_G_CHAIN_WAIT = 13,   // a chained launch waited > ~1.3 s for the previous launch's tile (every build)
 };
 
 // Tile queues: one counter per XCD group, 128 B apart (PT_QUEUE_WORDS u32 per launch).
@@ -99,7 +112,9 @@ enum PtGuardId : uint32_t {
 // Enqueue one render launch on `stream`.  Returns hipSuccess or the launch error.  With job.pix_out
 // the pixels are written by the render kernel itself when it is a continuous-tiles one, else by the
 // standalone output pass enqueued after it (pt_output.hip).
-hipError_t pt_launch_render(const PtJob& job, hipStream_t stream, bool count);
+// *ct_blocks (optional): the grid of the continuous-tiles kernel it launched (0: another pool, or
+// nothing launched) -- a chained launch's gate waits for that many started blocks.
+hipError_t pt_launch_render(const PtJob& job, hipStream_t stream, bool count, uint32_t* ct_blocks = nullptr);
 
 // The continuous-tiles pool's scratch: f32 per wave, and the waves of its resident grid on the
 // current device (the most a launch uses).

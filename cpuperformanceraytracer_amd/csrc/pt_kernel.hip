@@ -1231,9 +1231,45 @@ static_assert(PT_ENV_Q >= 64 && PT_ENV_Q <= 128, "the env miss queue holds 64 ..
 // (render_body's `cp + c`) to their slots.  D's fold drains the whole queue first.
 // PRESENT: the fused output stage (job.pix_out; pt_render_device_present) -- its own instances, so
 // the plain kernels' register allocation is untouched.
+// The accumulator's loads and stores in the continuous-tiles pools are `sc1` (agent-scope relaxed
+// atomics: global_load / global_store ... sc1, past the L1), so that in a chained launch
+// (PtJob::tile_epoch) a tile's pixels stored by one launch's wave are seen by the next launch's wave
+// on any CU once the tile's epoch says so -- the hand-off of MI355X_MICROARCH.md ("Workgroup
+// dispatch ... inter-workgroup visibility", row 1: sc1 stores, the storing wave's vmcnt(0), an sc1
+// flag store; sc1 polls and sc1 loads).  One code path for every launch: a pixel is loaded and stored
+// once per launch.
+__device__ __forceinline__ float px_ld(const float* p)
+{
+    return __builtin_bit_cast(float, __hip_atomic_load(reinterpret_cast<uint32_t*>(const_cast<float*>(p)), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void px_st(float* p, float v)
+{
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// A chained launch's queue entry e (a tile or one half) may be touched once the previous launch has
+// stored its pixels: the entry's half-tile epochs are >= w.  (Every lane loads the same word; the
+// value is made wave-uniform.)
+__device__ __forceinline__ uint32_t epoch_ld(const uint32_t* p)
+{
+    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool chain_ready(const uint32_t* ep, uint32_t e, uint32_t w)
+{
+    const uint32_t t = pt_entry_tile(e), part = pt_entry_part(e);
+    uint32_t m = ~0u;
+    if (part != 2u) m = std::min(m, epoch_ld(ep + 2u * t));
+    if (part != 1u) m = std::min(m, epoch_ld(ep + 2u * t + 1u));
+    return __builtin_amdgcn_readfirstlane(m) >= w;
+}
+
 template <int LAYOUT, bool ENV, bool COUNT, bool PRESENT>
 __device__ __forceinline__ void render_body_ct(const PtJob& job)
 {
+    // chained launches: this block has started (the next launch's stream waits for every block of
+    // this one: hipStreamWaitValue64 in pt_capi.cpp launch_chain)
+    if (job.started && threadIdx.x == 0)
+        __hip_atomic_fetch_add(job.started, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const PtScene* __restrict__ sc = job.scene;
     constexpr int kWavesPerBlock = waves_per_block<ENV>();
     constexpr bool QV = true;
@@ -1346,6 +1382,34 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     auto ws_st = [&](int k, uint32_t v) {
         if (lane == 0) ws[k] = v;
     };
+    // Chained launches: before touching entry e's pixels, wait for the previous launch's epoch (rare:
+    // both launches take the tiles longest first, so the next launch reaches a tile long after the
+    // previous one has folded it).  Bounded: a wait of ~1.3 s is reported (PT_G_CHAIN_WAIT, every
+    // build) instead of hanging the GPU -- the host's stream gate makes it unreachable (launch_chain).
+    auto chain_wait_tile = [&](uint32_t e) {
+        if (job.chain_wait == 0u || chain_ready(job.tile_epoch, e, job.chain_wait)) return;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        bool ok = false;
+        do {
+            __builtin_amdgcn_s_sleep(8);
+            ok = chain_ready(job.tile_epoch, e, job.chain_wait);
+        } while (!ok && __builtin_amdgcn_s_memrealtime() - t0 < (1ull << 27));   // (100 MHz)
+        if (!ok && lane == 0) pt_guard_report(job.err, PT_G_CHAIN_WAIT, pt_entry_tile(e));
+    };
+    // ... and after entry e's last pixel store, publish this launch's epoch for it
+    auto chain_publish = [&](uint32_t e) {
+        if (!job.tile_epoch) return;
+        if (__builtin_expect(job.chain_delay != 0u, 0)) {   // (test hook: the next launch meets unready tiles)
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * job.chain_delay) __builtin_amdgcn_s_sleep(8);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every lane's sc1 pixel stores have completed
+        if (lane == 0) {
+            const uint32_t t = pt_entry_tile(e), part = pt_entry_part(e);
+            if (part != 2u) __hip_atomic_store(job.tile_epoch + 2u * t, job.chain_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (part != 1u) __hip_atomic_store(job.tile_epoch + 2u * t + 1u, job.chain_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
     if (lane == 0) {
         ws[kWsTcur] = kNone;   // the tile being chunked (A's tile whenever A is set)
         ws[kWsFlags] = 0u;
@@ -1403,6 +1467,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             tq.save(s_tq[wv], lane);
             ws_st(kWsFlags, tile == kNone ? 3u : 1u);   // claimed (and done)
             if (tile == kNone) break;
+            chain_wait_tile(tile);
 #if PT_DIAG && !PT_DIAG_WAVES_ONLY
             didx_cur = (uint32_t)n_tiles_diag;
             if (dtl && lane == 0 && n_tiles_diag < 32) {
@@ -1448,11 +1513,11 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 if (!items && PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) {
                     // the same radiance in every frame: fold all of the launch's frames now
                     float* px = job.buf + pi;
-                    V3 acc = v3(px[0], px[cs], px[2 * cs]);
+                    V3 acc = v3(px_ld(px), px_ld(px + cs), px_ld(px + 2 * cs));
                     for (int f = 0; f < S; ++f) acc = add(acc, mul(sub(c_keep, acc), weight(f)));
-                    px[0] = acc.x;
-                    px[cs] = acc.y;
-                    px[2 * cs] = acc.z;
+                    px_st(px, acc.x);
+                    px_st(px + cs, acc.y);
+                    px_st(px + 2 * cs, acc.z);
                     present(lc, lr, acc);
                 }
             }
@@ -1460,6 +1525,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             const int nh = __popcll(hm);
             if (nh == 0) {
                 if (job.cost && lane == 0) pt_record_cost(job.cost, tile, total_tiles, 1u);
+                chain_publish(tile);   // (every pixel of the tile was stored above)
 #if PT_DIAG && !PT_DIAG_WAVES_ONLY
                 if (dtl && lane == 0 && didx_cur < 32) {
                     dtl[3 * didx_cur + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1527,7 +1593,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             size_t pi = out_index<LAYOUT>(job, lc, lr);
             if (!PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) pi = 0;   // (checked build: reported)
             float* px = job.buf + pi;
-            V3 acc = first ? v3(px[0], px[cs], px[2 * cs]) : v3(s_acc[wv][0][lane], s_acc[wv][1][lane], s_acc[wv][2][lane]);
+            V3 acc = first ? v3(px_ld(px), px_ld(px + cs), px_ld(px + 2 * cs)) : v3(s_acc[wv][0][lane], s_acc[wv][1][lane], s_acc[wv][2][lane]);
 #pragma unroll
             for (int f = 0; f < kChunk; ++f) {
                 if (f < nfD) {
@@ -1537,9 +1603,9 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 }
             }
             if (last) {
-                px[0] = acc.x;
-                px[cs] = acc.y;
-                px[2 * cs] = acc.z;
+                px_st(px, acc.x);
+                px_st(px + cs, acc.y);
+                px_st(px + 2 * cs, acc.z);
                 present(lc, lr, acc);
             } else {
                 s_acc[wv][0][lane] = acc.x;
@@ -1555,6 +1621,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
         const uint32_t tile_cost = 1u + (tile_seg + 63u) / 64u;
         if (last) {
             if (job.cost && lane == 0) pt_record_cost(job.cost, tD, total_tiles, tile_cost);
+            chain_publish(tD);   // (the item-less pixels were stored when the tile started)
 #if PT_DIAG && !PT_DIAG_WAVES_ONLY
             if (dtl && lane == 0 && didxD < 32) {
                 const unsigned long long it0 = dtl[3 * didxD + 1];
@@ -1825,7 +1892,7 @@ constexpr auto ct_kernel_of()
 
 // *presented: the kernel wrote job.pix_out (the presenting instances: row layouts, uncounted launches)
 template <int LAYOUT, bool ENV, bool COUNT>
-bool launch_ct(const PtJob& job, hipStream_t st, unsigned tiles, bool* presented)
+bool launch_ct(const PtJob& job, hipStream_t st, unsigned tiles, bool* presented, uint32_t* ct_blocks)
 {
     constexpr int wpb = waves_per_block<ENV>();
     *presented = false;
@@ -1841,6 +1908,7 @@ bool launch_ct(const PtJob& job, hipStream_t st, unsigned tiles, bool* presented
     if (!job.ct_slots || (uint64_t)blocks * wpb > job.ct_waves) return false;
     hipLaunchKernelGGL(k, dim3(blocks), dim3(64 * wpb), 0, st, job);
     *presented = pres;
+    if (ct_blocks) *ct_blocks = blocks;
     return true;
 }
 
@@ -1848,7 +1916,7 @@ template <int LAYOUT, bool ENV>
 hipError_t launch_pools(const PtJob& job, hipStream_t st, bool count, unsigned tiles);
 
 template <int LAYOUT, bool ENV>
-hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
+hipError_t launch_t(const PtJob& job, hipStream_t st, bool count, uint32_t* ct_blocks)
 {
     const unsigned tiles = (unsigned)((job.ncols + 7) / 8) * (unsigned)((job.nrows + 7) / 8);
     // the continuous-tiles pool when its slots are provided (its presenting instances write
@@ -1861,9 +1929,10 @@ hipError_t launch_t(const PtJob& job, hipStream_t st, bool count)
     if (!kCountable && count) return hipErrorInvalidValue;
     bool ct;
     if constexpr (kCountable)
-        ct = count ? launch_ct<LAYOUT, ENV, true>(job, st, tiles, &presented) : launch_ct<LAYOUT, ENV, false>(job, st, tiles, &presented);
+        ct = count ? launch_ct<LAYOUT, ENV, true>(job, st, tiles, &presented, ct_blocks)
+                   : launch_ct<LAYOUT, ENV, false>(job, st, tiles, &presented, ct_blocks);
     else
-        ct = launch_ct<LAYOUT, ENV, false>(job, st, tiles, &presented);
+        ct = launch_ct<LAYOUT, ENV, false>(job, st, tiles, &presented, ct_blocks);
     if (ct)
         e = hipGetLastError();
     else
@@ -2094,8 +2163,9 @@ uint32_t pt_ct_resident_waves()
     return (uint32_t)*std::max_element(std::begin(r), std::end(r)) * (uint32_t)wpb;
 }
 
-hipError_t pt_launch_render(const PtJob& job_in, hipStream_t st, bool count)
+hipError_t pt_launch_render(const PtJob& job_in, hipStream_t st, bool count, uint32_t* ct_blocks)
 {
+    if (ct_blocks) *ct_blocks = 0;
     if (job_in.ncols <= 0 || job_in.nrows <= 0) return hipSuccess;
     if (job_in.nframes <= 0) {   // nothing to render; a presenting job still converts the accumulator
         if (!job_in.pix_out) return hipSuccess;
@@ -2116,16 +2186,16 @@ hipError_t pt_launch_render(const PtJob& job_in, hipStream_t st, bool count)
     if (job.env) {
         if (job.env_w <= 0 || job.env_h <= 0) return hipErrorInvalidValue;
         switch (job.layout) {
-            case PT_LAYOUT_INTERLEAVED: return launch_t<PT_LAYOUT_INTERLEAVED, true>(job, st, count);
-            case PT_LAYOUT_PLANAR8: return launch_t<PT_LAYOUT_PLANAR8, true>(job, st, count);
-            case PT_LAYOUT_TILED_PLANAR8: return launch_t<PT_LAYOUT_TILED_PLANAR8, true>(job, st, count);
+            case PT_LAYOUT_INTERLEAVED: return launch_t<PT_LAYOUT_INTERLEAVED, true>(job, st, count, ct_blocks);
+            case PT_LAYOUT_PLANAR8: return launch_t<PT_LAYOUT_PLANAR8, true>(job, st, count, ct_blocks);
+            case PT_LAYOUT_TILED_PLANAR8: return launch_t<PT_LAYOUT_TILED_PLANAR8, true>(job, st, count, ct_blocks);
             default: return hipErrorInvalidValue;
         }
     }
     switch (job.layout) {
-        case PT_LAYOUT_INTERLEAVED: return launch_t<PT_LAYOUT_INTERLEAVED, false>(job, st, count);
-        case PT_LAYOUT_PLANAR8: return launch_t<PT_LAYOUT_PLANAR8, false>(job, st, count);
-        case PT_LAYOUT_TILED_PLANAR8: return launch_t<PT_LAYOUT_TILED_PLANAR8, false>(job, st, count);
+        case PT_LAYOUT_INTERLEAVED: return launch_t<PT_LAYOUT_INTERLEAVED, false>(job, st, count, ct_blocks);
+        case PT_LAYOUT_PLANAR8: return launch_t<PT_LAYOUT_PLANAR8, false>(job, st, count, ct_blocks);
+        case PT_LAYOUT_TILED_PLANAR8: return launch_t<PT_LAYOUT_TILED_PLANAR8, false>(job, st, count, ct_blocks);
         default: return hipErrorInvalidValue;
     }
 }

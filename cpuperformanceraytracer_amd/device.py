@@ -63,13 +63,24 @@ def _stream(stream):
 
 def render_device(buf, width: int, height: int, *, frame_first: int, nframes: int, num_bounces: int,
                   row_start: int = 0, row_stride: int = 1, nrows: int | None = None,
-                  layout: int = N.PT_LAYOUT_INTERLEAVED, use_env: bool = False, stream=None) -> None:
+                  layout: int = N.PT_LAYOUT_INTERLEAVED, use_env: bool = False, stream=None,
+                  chain: bool = False) -> None:
     """Accumulate frames [frame_first, frame_first+nframes) of global rows row_start + k*row_stride
     (k < nrows) into `buf` (nrows x width x 3 f32, in HBM).  Asynchronous on `stream`.
-    use_env: miss radiance from the env map of set_env_map (config 4) instead of the ambient."""
+    use_env: miss radiance from the env map of set_env_map (config 4) instead of the ambient.
+    chain: pt_render_device_chain -- this launch may overlap the previous chained launch of the same
+    geometry on `stream` (same result; nothing enqueued on `stream` since that call may be needed)."""
     nrows = height if nrows is None else nrows
     job = _job(buf, width, height, row_start, row_stride, nrows, frame_first, nframes, num_bounces, layout, use_env)
-    N.check(N.load().pt_render_device(ctypes.byref(job), _stream(stream)), "pt_render_device")
+    fn = "pt_render_device_chain" if chain else "pt_render_device"
+    N.check(getattr(N.load(), fn)(ctypes.byref(job), _stream(stream)), fn)
+
+
+def chain_counts() -> dict:
+    """pt_chain_counts: chained launches since init that restarted / continued the overlap."""
+    r, c = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    N.check(N.load().pt_chain_counts(ctypes.byref(r), ctypes.byref(c)), "pt_chain_counts")
+    return {"restarts": int(r.value), "continued": int(c.value)}
 
 
 def render_device_present(buf, pixels, width: int, height: int, *, frame_first: int, nframes: int,
@@ -138,7 +149,7 @@ class JobLauncher:
     def __init__(self, buf, width: int, height: int, *, nframes: int, num_bounces: int, row_start: int = 0,
                  row_stride: int = 1, nrows: int | None = None, layout: int = N.PT_LAYOUT_INTERLEAVED,
                  use_env: bool = False, stream=None, v4: bool = False, pixels=None,
-                 pixel_format: int = N.PT_PIXEL_RGBA8):
+                 pixel_format: int = N.PT_PIXEL_RGBA8, chain: bool = False):
         nrows = height if nrows is None else nrows
         self._buf = buf   # (kept alive with the job that points at it)
         self.job = _job(buf, width, height, row_start, row_stride, nrows, 1, nframes, num_bounces, layout, use_env)
@@ -153,9 +164,10 @@ class JobLauncher:
             fn, args = L.pt_render_device_present, (self._ref, pixels.data_ptr(), pixel_format, self._stream)
             self._what = "pt_render_device_present"
         else:
-            fn = L.pt_v4_render_device if v4 else L.pt_render_device
+            # chain (the diffuse renderer): pt_render_device_chain, consecutive launches overlap
+            self._what = "pt_v4_render_device" if v4 else ("pt_render_device_chain" if chain else "pt_render_device")
+            fn = getattr(L, self._what)
             args = (self._ref, self._stream)
-            self._what = "pt_v4_render_device" if v4 else "pt_render_device"
         self._fn, self._args = fn, args
 
     def __call__(self, frame_first: int) -> None:

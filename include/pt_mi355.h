@@ -319,6 +319,20 @@ void pt_free_work_queue(pt_work_queue* q);
 
 /* --- device-resident entry points -------------------------------------------------------------- */
 int pt_render_device(const pt_device_job* job, void* hip_stream);      /* async on hip_stream     */
+/* pt_render_device for a progressive renderer's consecutive launches of one geometry: the launch may
+ * run overlapped with the previous pt_render_device_chain launch of that geometry on this stream (on
+ * two streams of the library's; the next launch's waves fill the CUs where the previous launch's last
+ * waves end), with every pixel's frames still accumulated in order -- bit for bit the result of
+ * pt_render_device.  The caller promises that nothing enqueued on hip_stream since its previous chained
+ * call of this geometry is needed by this launch (so the launch does not wait for it); anything the
+ * caller enqueues on hip_stream after this call is ordered after the launch, as with pt_render_device.
+ * Any other launch on the device (another geometry, pt_render_device, counting, v4, host-buffer
+ * calls) ends the overlap: the next chained call then waits for hip_stream as pt_render_device does.
+ * Async on hip_stream. */
+int pt_render_device_chain(const pt_device_job* job, void* hip_stream);
+/* pt_render_device_chain launches since pt_init that restarted the overlap (waited for hip_stream as
+ * pt_render_device does) and that continued it (overlapped with their predecessor).  Host state. */
+int pt_chain_counts(uint64_t* restarts, uint64_t* continued);
 int pt_count_device(const pt_device_job* job, void* hip_stream, pt_work_counts* out); /* sync;    */
                                   /* renders like pt_render_device AND counts the work it did     */
 /* pt_render_device with the output stage fused into the render (the
