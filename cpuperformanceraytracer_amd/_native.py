@@ -203,8 +203,13 @@ def load() -> ctypes.CDLL:
         "pt_work_queue_size": (i32, [vp]),
         "pt_free_work_queue": (None, [vp]),
     }
+    dev_lib = bool(os.environ.get("PT_MI355_LIB"))
     for name, (res, args) in sig.items():
-        fn = getattr(L, name)
+        fn = getattr(L, name, None)
+        if fn is None and dev_lib:   # (an A/B library of an earlier revision: entry points added since are absent)
+            continue
+        if fn is None:
+            raise AttributeError(f"{path}: missing symbol {name}")
         fn.restype = res
         fn.argtypes = args
     _lib = L

@@ -1238,13 +1238,21 @@ static_assert(PT_ENV_Q >= 64 && PT_ENV_Q <= 128, "the env miss queue holds 64 ..
 // dispatch ... inter-workgroup visibility", row 1: sc1 stores, the storing wave's vmcnt(0), an sc1
 // flag store; sc1 polls and sc1 loads).  One code path for every launch: a pixel is loaded and stored
 // once per launch.
+#ifndef PT_PX_SC1
+#define PT_PX_SC1 3   // (A/B only: bit 0 the loads, bit 1 the stores sc1)
+#endif
 __device__ __forceinline__ float px_ld(const float* p)
 {
+    if (!(PT_PX_SC1 & 1)) return *p;
     return __builtin_bit_cast(float, __hip_atomic_load(reinterpret_cast<uint32_t*>(const_cast<float*>(p)), __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT));
 }
 __device__ __forceinline__ void px_st(float* p, float v)
 {
+    if (!(PT_PX_SC1 & 2)) {
+        *p = v;
+        return;
+    }
     __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // A chained launch's queue entry e (a tile or one half) may be touched once the previous launch has
@@ -1386,8 +1394,11 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     // both launches take the tiles longest first, so the next launch reaches a tile long after the
     // previous one has folded it).  Bounded: a wait of ~1.3 s is reported (PT_G_CHAIN_WAIT, every
     // build) instead of hanging the GPU -- the host's stream gate makes it unreachable (launch_chain).
+#ifndef PT_CHAIN_CODE
+#define PT_CHAIN_CODE 1   // (A/B only: 0 compiles the chained-launch code out)
+#endif
     auto chain_wait_tile = [&](uint32_t e) {
-        if (job.chain_wait == 0u || chain_ready(job.tile_epoch, e, job.chain_wait)) return;
+        if (!PT_CHAIN_CODE || job.chain_wait == 0u || chain_ready(job.tile_epoch, e, job.chain_wait)) return;
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         bool ok = false;
         do {
@@ -1398,7 +1409,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     };
     // ... and after entry e's last pixel store, publish this launch's epoch for it
     auto chain_publish = [&](uint32_t e) {
-        if (!job.tile_epoch) return;
+        if (!PT_CHAIN_CODE || !job.tile_epoch) return;
         if (__builtin_expect(job.chain_delay != 0u, 0)) {   // (test hook: the next launch meets unready tiles)
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * job.chain_delay) __builtin_amdgcn_s_sleep(8);

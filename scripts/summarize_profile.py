@@ -81,9 +81,38 @@ if traces:
         steady_ns = sum(d[k0:]) / len(d[k0:])
         lines.append(f"kernel_trace_steady_average_ns {steady_ns:.1f} (dispatches {k0 + 1}..{len(d)} of {len(d)}: "
                      "after the clock ramp)")
+# Chained launches (bench.py's diffuse steps) overlap: each launch's own duration is longer
+# than the step.  The comparable figure is the span of the longest run of overlapping or back-to-back
+# dispatches of the instance (start of the next <= end of the previous + 20 us, i.e. no host
+# synchronisation between them) divided by its number of dispatches.
+span_ns = None
+if traces:
+    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(traces[0]))
+                if KERNEL in r["Kernel_Name"])
+    runs, cur = [], [ev[0]] if ev else []
+    for a, b in ev[1:]:
+        if a <= max(e for _, e in cur[-2:]) + 20000:
+            cur.append((a, b))
+        else:
+            runs.append(cur)
+            cur = [(a, b)]
+    if cur:
+        runs.append(cur)
+    # the longest run whose every dispatch started before its predecessor ended (the timed steps:
+    # bench.py's K chained launches); none such (plain launches): the longest run
+    ovl = [r for r in runs if all(r[i][0] < r[i - 1][1] for i in range(1, len(r)))]
+    if runs:
+        best = max(ovl or runs, key=len)
+        n_ovl = sum(1 for i in range(1, len(best)) if best[i][0] < best[i - 1][1])
+        span_ns = (max(b for _, b in best) - best[0][0]) / len(best)
+        lines.append(f"kernel_trace_run_span_per_launch_ns {span_ns:.1f} (longest run of {len(best)} back-to-back "
+                     f"dispatches, {n_ovl} of them starting before their predecessor ended)")
+        if ovl:
+            own = sum(b - a for a, b in best) / len(best)
+            lines.append(f"kernel_trace_overlapped_own_duration_ns {own:.1f} (each launch's own start..end in that run)")
 (dst / f"{tag}_pmc.txt").write_text("\n".join(lines) + "\n")
 out = {"source": f"profiles/{tag}_pmc.txt", "workload": workload, "kernel": KERNEL, "kernel_average_ns": avg_ns,
-       "kernel_steady_average_ns": steady_ns}
+       "kernel_steady_average_ns": steady_ns, "kernel_run_span_per_launch_ns": span_ns}
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     out["fetch_kib"] = mean["FETCH_SIZE"]
     out["write_kib"] = mean["WRITE_SIZE"]
