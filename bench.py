@@ -63,7 +63,7 @@ def parse(argv=None):
     ap.add_argument("--workload", default="c2_1080p")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-chain", action="store_true",
-                    help="diffuse workloads: plain pt_render_device steps, one after the other, instead of chained "
+                    help="plain pt_render_device / pt_v4_render_device steps, one after the other, instead of chained "
                          "launches (pt_render_device_chain) that overlap consecutive steps")
     ap.add_argument("--no-configs4", action="store_true",
                     help="default workload: skip the configs[4] strong-scaling leg (c5_8k, a few steps)")
@@ -861,8 +861,9 @@ def main() -> None:
                                                                      use_env=wl.env)),
                   output_stage=output_stage,
                   cpu_baseline=lambda: cpu_baseline(wl, args.cpu_seconds, env),
-                  # the diffuse renderer's steps are chained launches (pt_render_device_chain) unless --no-chain
-                  chain_counts=None if v4 or args.no_chain else chain_counts)
+                  # the steps are chained launches (pt_render_device_chain / pt_v4_render_device_chain) unless
+                  # --no-chain
+                  chain_counts=None if args.no_chain else chain_counts)
     res = drive(args, wl, rank, world, ops, render_fn, count_fn, hooks, rehearse=rehearse)
     if rank == 0:
         print(json.dumps(res))

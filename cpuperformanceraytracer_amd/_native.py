@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = (
     "pt_v4_default_config", "pt_v4_set_config", "pt_v4_get_config", "pt_v4_initialize_global_render_resources",
     "pt_v4_reinitialize_render_tile_data", "pt_v4_initialize_scene", "pt_v4_clear_scene", "pt_v4_add_material",
     "pt_v4_add_quad", "pt_v4_add_sphere", "pt_v4_set_frame", "pt_v4_get_frame", "pt_v4_get_scene_tables", "pt_render_opt_v4",
-    "pt_copy_output_to_file", "pt_v4_render_device", "pt_v4_count_device", "pt_v4_begin_frame",
+    "pt_copy_output_to_file", "pt_v4_render_device", "pt_v4_render_device_chain", "pt_v4_count_device", "pt_v4_begin_frame",
     "pt_make_work_queue", "pt_add_work_queue_entry", "pt_complete_all_work", "pt_complete_all_work_async",
     "pt_wait_work", "pt_work_queue_size", "pt_free_work_queue",
 )
@@ -193,6 +193,7 @@ def load() -> ctypes.CDLL:
         "pt_render_opt_v4": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, ctypes.POINTER(PtTexture), vp]),
         "pt_copy_output_to_file": (i32, [vp, i32, i32, i32, i32, i32, i32, i32, vp]),
         "pt_v4_render_device": (i32, [ctypes.POINTER(PtDeviceJob), vp]),
+        "pt_v4_render_device_chain": (i32, [ctypes.POINTER(PtDeviceJob), vp]),
         "pt_v4_count_device": (i32, [ctypes.POINTER(PtDeviceJob), vp, ctypes.POINTER(PtWorkCounts)]),
         "pt_v4_begin_frame": (i32, []),
         "pt_make_work_queue": (vp, [i32]),

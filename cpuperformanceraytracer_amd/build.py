@@ -26,7 +26,8 @@ ARCH = os.environ.get("PT_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["pt_kernel.hip", "pt_output.hip", "pt_v4.hip", "pt_scene.cpp", "pt_v4_scene.cpp", "pt_capi.cpp",
            "pt_dropin.cpp", "pt_texture.cpp"]
 HEADERS = ["pt_kernel.h", "pt_output.h", "pt_v4.h", "pt_v4_default_scene.h", "pt_scene.h", "pt_sincosf.h", "pt_exactmath.h",
-           "pt_invtrig.h", "pt_envcert.h", "pt_tile_queue.h", "pt_quadcull.h", "pt_libmf.h", "pt_wave.h", "pt_guard.h"]
+           "pt_invtrig.h", "pt_envcert.h", "pt_tile_queue.h", "pt_quadcull.h", "pt_libmf.h", "pt_wave.h", "pt_guard.h",
+           "pt_chain.h"]
 CHECKED_LIB = ROOT / "build" / "libpt_checked.so"
 PARITY_FLAGS = [
     "-ffp-contract=off",

@@ -917,27 +917,75 @@ int chain_setup(Dev& dv, Sched& sc)
     return PT_OK;
 }
 
-int launch_chain(Dev& dv, PtJob j, hipStream_t s)
+int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count, bool* presented = nullptr, uint32_t* ct_blocks = nullptr,
+              const hipStream_t* sched_st = nullptr);
+
+// What differs between the diffuse and the v4 renderer in launch_chain: the schedule's key, whether
+// the launch variant is settled (the diffuse kernels time their arms on a geometry's first launches;
+// v4 has one variant), the restarting launch (launch / v4_launch) and the continuing one.
+SchedKey chain_key(const PtJob& j)
+{
+    SchedKey k = sched_key(j);
+    k.split = j.nframes <= 8 ? g.split : 0u;   // (as launch())
+    return k;
+}
+SchedKey chain_key(const PtV4Job& j) { return sched_key(j); }   // (v4 takes whole tiles: v4_launch)
+bool chain_variant_fixed(const PtJob& j, const Sched& sc)
+{
+    const bool env_arms = j.env && j.nframes <= 16 && g.ct_back_pct != 0 && !g.back_set;   // (ct_occupancy)
+    return g.ct_waves || g.ct_seq_len || sc.wide >= 0 || (j.env && !env_arms);
+}
+bool chain_variant_fixed(const PtV4Job&, const Sched&) { return true; }
+int chain_restart(Dev& dv, const PtJob& j, hipStream_t X, uint32_t* blocks, const hipStream_t* s)
+{
+    return launch(dv, j, X, false, blocks, s);
+}
+int chain_restart(Dev& dv, const PtV4Job& j, hipStream_t X, uint32_t* blocks, const hipStream_t* s)
+{
+    return v4_launch(dv, j, X, false, nullptr, blocks, s);
+}
+int chain_continue(Dev& dv, PtJob& j, Sched* sc, hipStream_t X, uint32_t* blocks)
+{
+    int rc;
+    j.scene = dv.dscene;
+    j.ct_back_pct = j.nframes <= 16 ? g.ct_back_pct : 0u;   // (as launch())
+    LaunchSched ls;
+    ls.sched = sc;
+    hipEvent_t* tev = nullptr;   // (none: the variant is settled)
+    if ((rc = ct_occupancy(ls, j, &tev, false))) return rc;
+    hipError_t e = pt_launch_render(j, X, false, blocks);
+    if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
+    return PT_OK;
+}
+int chain_continue(Dev& dv, PtV4Job& j, Sched*, hipStream_t X, uint32_t* blocks)
+{
+    if (j.env_mode != PT_V4_ENV_NONE) j.env = dv.denv;   // (as v4_launch())
+    j.ct_force = g.v4_ct_force;
+    j.ct_back_pct = j.nframes <= 16 ? g.ct_back_pct : 0u;
+    hipError_t e = pt_launch_v4(j, g.v4scene, X, false, nullptr, blocks);
+    if (e != hipSuccess) return fail(PT_EHIP, "v4 render launch failed: %s", hipGetErrorString(e));
+    return PT_OK;
+}
+
+template <typename Job>
+int launch_chain(Dev& dv, Job j, hipStream_t s)
 {
     int rc;
     if ((rc = use_dev(dv))) return rc;
-    SchedKey key = sched_key(j);
-    key.split = j.nframes <= 8 ? g.split : 0u;
+    const SchedKey key = chain_key(j);
     // (the continuous-tiles pool and a scheduled geometry: the tile epochs live in its schedule)
     Sched* sc = g.no_ct || j.ncols <= 0 || j.nrows <= 0 || j.nframes <= 0 ? nullptr : find_sched(dv, key, s);
-    if (!sc) return launch(dv, j, s, false);
+    if (!sc) return chain_restart(dv, j, s, nullptr, nullptr);   // (a plain launch: use_sched joins the chain)
     ct_area_alloc(dv);
     if ((rc = chain_setup(dv, *sc))) return rc;
     Dev::Chain& c = dv.chain;
-    if (!dv.dct || !c.area1) return launch(dv, j, s, false);
-    // what launch()'s use_sched / ct_occupancy would do for this launch
+    if (!dv.dct || !c.area1) return chain_restart(dv, j, s, nullptr, nullptr);
+    // what the plain launch's use_sched would do for this launch: build the schedule (restart), record
+    // the costs it is built from (a launch that records them may continue: the overlapped launches
+    // before it do not write them, and the next launch, which builds from them, restarts)
     const bool builds = sc->have_cost && (!sc->built || sc->launches % kSchedRebuild == 0);
     const bool records = !sc->built || (sc->launches + 1) % kSchedRebuild == 0;
-    const bool env_arms = j.env && j.nframes <= 16 && g.ct_back_pct != 0 && !g.back_set;
-    const bool variant_fixed = g.ct_waves || g.ct_seq_len || sc->wide >= 0 || (j.env && !env_arms);
-    // (a launch that records the tile costs may continue: the overlapped launches before it do not write
-    // them, and the next launch, which builds the schedule from them, restarts)
-    const bool cont = c.sched == sc && sc->built && !builds && variant_fixed;
+    const bool cont = c.sched == sc && sc->built && !builds && chain_variant_fixed(j, *sc);
     const uint32_t seq = sc->chain_seq + 1;
     const int par = cont ? c.par ^ 1 : 0;
     hipStream_t X = c.st[par];
@@ -947,19 +995,18 @@ int launch_chain(Dev& dv, PtJob j, hipStream_t s)
     j.chain_delay = g.test_chain_delay;
     uint32_t blocks = 0;
     if (!cont) {
-        // restart: after the caller's stream and every chained launch (launch()'s use_sched joins them)
+        // restart: after the caller's stream and every chained launch (the plain launch's use_sched joins them)
         HIP_TRY(hipEventRecord(c.ev_caller, s));
         HIP_TRY(hipStreamWaitEvent(X, c.ev_caller, 0));
         if ((rc = chain_join(dv, X))) return rc;
         HIP_TRY(hipMemsetAsync(c.qblk, 0, 4 * PT_QUEUE_WORDS * sizeof(unsigned), X));
         j.chain_wait = 0;
-        if ((rc = launch(dv, j, X, false, &blocks, &s))) return rc;   // (slot area dct)
+        if ((rc = chain_restart(dv, j, X, &blocks, &s))) return rc;   // (slot area dct)
         c.area = 0;
     } else {
         // continue: once every block of the previous launch has started
         HIP_TRY(hipStreamWaitValue64(X, c.started, c.cum, hipStreamWaitValueGte, ~0ull));
         j.chain_wait = seq - 1;
-        j.scene = dv.dscene;
         j.queue = c.qblk + (size_t)(seq % 4u) * PT_QUEUE_WORDS;
         j.queue_next = c.qblk + (size_t)((seq + 2u) % 4u) * PT_QUEUE_WORDS;   // (the launch after next: this stream's)
         j.order = sc->order;
@@ -971,14 +1018,8 @@ int launch_chain(Dev& dv, PtJob j, hipStream_t s)
         c.area ^= 1;
         j.ct_slots = c.area ? c.area1 : dv.dct;
         j.ct_waves = dv.dct_waves;
-        j.ct_back_pct = j.nframes <= 16 ? g.ct_back_pct : 0u;
-        LaunchSched ls;
-        ls.sched = sc;
-        hipEvent_t* tev = nullptr;
-        if ((rc = ct_occupancy(ls, j, &tev, false))) return rc;
         ++sc->launches;
-        hipError_t e = pt_launch_render(j, X, false, &blocks);
-        if (e != hipSuccess) return fail(PT_EHIP, "render launch failed: %s", hipGetErrorString(e));
+        if ((rc = chain_continue(dv, j, sc, X, &blocks))) return rc;
     }
     c.cum += blocks;
     sc->chain_seq = seq;
@@ -986,7 +1027,7 @@ int launch_chain(Dev& dv, PtJob j, hipStream_t s)
     HIP_TRY(hipEventRecord(c.done[par], X));
     c.pending[par] = true;
     HIP_TRY(hipStreamWaitEvent(s, c.done[par], 0));
-    // a launch that did not run the continuous-tiles pool published no epochs and counted no blocks:
+    // a launch that did not run a continuous-tiles pool published no epochs and counted no blocks:
     // the next chained launch restarts
     c.sched = blocks ? sc : nullptr;
     c.par = par;
@@ -1432,13 +1473,14 @@ int v4_use_env(PtV4Job& j)
     return PT_OK;
 }
 
-int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count, bool* presented = nullptr)
+// *ct_blocks, sched_st: as launch()
+int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count, bool* presented, uint32_t* ct_blocks, const hipStream_t* sched_st)
 {
     LaunchSched ls;
     int rc;
     // v4 takes whole tiles: its per-tile kernel runs launches of < 8 frames (and PT_MI355_NO_CT=1), and
     // split tiles measured slower on the continuous-tiles one (0.3666 vs 0.3633 ms at 1080p 8 spp)
-    if ((rc = use_dev(dv)) || (rc = use_sched(dv, sched_key(j), st, &ls, 0u))) return rc;
+    if ((rc = use_dev(dv)) || (rc = use_sched(dv, sched_key(j), st, &ls, 0u, sched_st))) return rc;
     if (j.env_mode != PT_V4_ENV_NONE) j.env = dv.denv;
     j.queue = ls.queue;
     j.queue_next = ls.queue_next;
@@ -1451,7 +1493,7 @@ int v4_launch(Dev& dv, PtV4Job j, hipStream_t st, bool count, bool* presented = 
     if ((rc = use_ct_slots(dv, ls, st, &j.ct_slots, &j.ct_waves))) return rc;
     j.ct_force = g.v4_ct_force;
     j.ct_back_pct = j.nframes <= 16 ? g.ct_back_pct : 0u;   // (as launch())
-    hipError_t e = pt_launch_v4(j, g.v4scene, st, count, presented);
+    hipError_t e = pt_launch_v4(j, g.v4scene, st, count, presented, ct_blocks);
     if (e != hipSuccess) return fail(PT_EHIP, "v4 render launch failed: %s", hipGetErrorString(e));
     return queue_done(dv, ls.slot, st, j.ncols > 0 && j.nrows > 0 && j.nframes > 0);   // (pt_launch_v4's early return)
 }
@@ -2364,6 +2406,16 @@ int pt_v4_render_device(const pt_device_job* dj, void* stream)
     DeviceGuard guard;
     if ((rc = ensure_init()) || (rc = v4_device_job(dj, &j)) || (rc = dev_of(dj->buf, &dv))) return rc;
     return v4_launch(*dv, j, (hipStream_t)stream, false);
+}
+
+int pt_v4_render_device_chain(const pt_device_job* dj, void* stream)
+{
+    int rc;
+    PtV4Job j;
+    Dev* dv = nullptr;
+    DeviceGuard guard;
+    if ((rc = ensure_init()) || (rc = v4_device_job(dj, &j)) || (rc = dev_of(dj->buf, &dv))) return rc;
+    return launch_chain(*dv, j, (hipStream_t)stream);
 }
 
 int pt_v4_count_device(const pt_device_job* dj, void* stream, pt_work_counts* out)

@@ -1,0 +1,90 @@
+// pt_chain.h -- the device side of chained launches (pt_capi.cpp launch_chain), shared by
+// the continuous-tiles pools of pt_kernel.hip (render_body_ct) and pt_v4.hip (pt_v4_ct_kernel).
+//
+// Consecutive launches of one geometry overlap on two streams.  The only data a launch needs from the
+// one before is a tile's accumulator values: the progressive lerp of demofox_path_tracing_scalar.cpp:812
+// (v4: the fused lerp of demofox_path_tracing_optimization_v4.cpp:1233-1241) folds each pixel's frames
+// in order.  So a launch touches a tile's pixels only after the previous launch has stored them:
+//   * the accumulator's loads and stores are `sc1` (agent-scope relaxed atomics: global_load /
+//     global_store ... sc1, past the L1) -- in every continuous-tiles launch, one code path (a pixel is
+//     loaded and stored once per launch; A/B: no measurable cost, profiles/r06/r06l_ab_chain_code.txt);
+//   * after a queue entry's (tile or half tile) last pixel store the wave waits for its stores
+//     (s_waitcnt vmcnt(0)) and one lane stores the launch's sequence number into the entry's half-tile
+//     epoch words (`sc1`);
+//   * a chained launch polls the epochs of an entry it claims (`sc1` loads) until they reach its
+//     predecessor's number, before it touches the entry's pixels.
+// This is the hand-off of MI355X_MICROARCH.md's inter-workgroup table, row 1 (sc1 stores, the storing
+// wave's vmcnt(0), an sc1 flag store; sc1 polls and loads).  Every block adds 1 to the chain's started
+// counter at its start: the next launch's stream waits for all of them (hipStreamWaitValue64), which
+// makes the chain deadlock-free (tests/test_chain_protocol.py).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt_kernel.h"        // PT_G_CHAIN_WAIT
+#include "pt_guard.h"         // pt_guard_report
+#include "pt_tile_queue.h"    // pt_entry_tile / pt_entry_part
+
+__device__ __forceinline__ float pt_px_ld(const float* p)
+{
+    return __builtin_bit_cast(float, __hip_atomic_load(reinterpret_cast<uint32_t*>(const_cast<float*>(p)), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void pt_px_st(float* p, float v)
+{
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the block has started (the next chained launch's stream gate); started: nullptr when not chained
+__device__ __forceinline__ void pt_chain_started(unsigned long long* started)
+{
+    if (started && threadIdx.x == 0) __hip_atomic_fetch_add(started, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// entry e's half-tile epochs are >= w (every lane loads the same words; the value is made wave-uniform)
+__device__ __forceinline__ bool pt_chain_ready(const uint32_t* ep, uint32_t e, uint32_t w)
+{
+    const uint32_t t = pt_entry_tile(e), part = pt_entry_part(e);
+    uint32_t m = ~0u;
+    if (part != 2u) {
+        const uint32_t a = __hip_atomic_load(const_cast<uint32_t*>(ep + 2u * t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        m = a < m ? a : m;
+    }
+    if (part != 1u) {
+        const uint32_t b = __hip_atomic_load(const_cast<uint32_t*>(ep + 2u * t + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        m = b < m ? b : m;
+    }
+    return __builtin_amdgcn_readfirstlane(m) >= w;
+}
+
+// (the whole wave) before touching entry e's pixels: wait until the previous launch has published it.
+// Rare -- both launches take the tiles longest first, so a launch reaches a tile long after its
+// predecessor folded it.  Bounded: after ~1.3 s the wait is reported (guard PT_G_CHAIN_WAIT, every
+// build) instead of hanging the GPU; the host's stream gate makes that unreachable.
+__device__ __forceinline__ void pt_chain_wait(const uint32_t* ep, uint32_t e, uint32_t w, uint32_t* err, int lane)
+{
+    if (pt_chain_ready(ep, e, w)) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool ok = false;
+    do {
+        __builtin_amdgcn_s_sleep(8);
+        ok = pt_chain_ready(ep, e, w);
+    } while (!ok && __builtin_amdgcn_s_memrealtime() - t0 < (1ull << 27));   // (100 MHz)
+    if (!ok && lane == 0) pt_guard_report(err, PT_G_CHAIN_WAIT, pt_entry_tile(e));
+}
+
+// (the whole wave) after entry e's last pixel store: publish sequence number seq for it.  delay: the
+// test hook PT_MI355_TEST_CHAIN_DELAY (~us slept first, so that the next launch meets unready tiles)
+__device__ __forceinline__ void pt_chain_publish(uint32_t* ep, uint32_t e, uint32_t seq, uint32_t delay, int lane)
+{
+    if (__builtin_expect(delay != 0u, 0)) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * delay) __builtin_amdgcn_s_sleep(8);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every lane's sc1 pixel stores have completed
+    if (lane == 0) {
+        const uint32_t t = pt_entry_tile(e), part = pt_entry_part(e);
+        if (part != 2u) __hip_atomic_store(ep + 2u * t, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (part != 1u) __hip_atomic_store(ep + 2u * t + 1u, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}

@@ -51,6 +51,7 @@
 #include "pt_tonemap.h"
 #include "pt_output.h"
 #include "pt_wave.h"
+#include "pt_chain.h"
 #include <math.h>
 #include <algorithm>
 
@@ -1231,53 +1232,12 @@ static_assert(PT_ENV_Q >= 64 && PT_ENV_Q <= 128, "the env miss queue holds 64 ..
 // (render_body's `cp + c`) to their slots.  D's fold drains the whole queue first.
 // PRESENT: the fused output stage (job.pix_out; pt_render_device_present) -- its own instances, so
 // the plain kernels' register allocation is untouched.
-// The accumulator's loads and stores in the continuous-tiles pools are `sc1` (agent-scope relaxed
-// atomics: global_load / global_store ... sc1, past the L1), so that in a chained launch
-// (PtJob::tile_epoch) a tile's pixels stored by one launch's wave are seen by the next launch's wave
-// on any CU once the tile's epoch says so -- the hand-off of MI355X_MICROARCH.md ("Workgroup
-// dispatch ... inter-workgroup visibility", row 1: sc1 stores, the storing wave's vmcnt(0), an sc1
-// flag store; sc1 polls and sc1 loads).  One code path for every launch: a pixel is loaded and stored
-// once per launch.
-#ifndef PT_PX_SC1
-#define PT_PX_SC1 3   // (A/B only: bit 0 the loads, bit 1 the stores sc1)
-#endif
-__device__ __forceinline__ float px_ld(const float* p)
-{
-    if (!(PT_PX_SC1 & 1)) return *p;
-    return __builtin_bit_cast(float, __hip_atomic_load(reinterpret_cast<uint32_t*>(const_cast<float*>(p)), __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void px_st(float* p, float v)
-{
-    if (!(PT_PX_SC1 & 2)) {
-        *p = v;
-        return;
-    }
-    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// A chained launch's queue entry e (a tile or one half) may be touched once the previous launch has
-// stored its pixels: the entry's half-tile epochs are >= w.  (Every lane loads the same word; the
-// value is made wave-uniform.)
-__device__ __forceinline__ uint32_t epoch_ld(const uint32_t* p)
-{
-    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool chain_ready(const uint32_t* ep, uint32_t e, uint32_t w)
-{
-    const uint32_t t = pt_entry_tile(e), part = pt_entry_part(e);
-    uint32_t m = ~0u;
-    if (part != 2u) m = std::min(m, epoch_ld(ep + 2u * t));
-    if (part != 1u) m = std::min(m, epoch_ld(ep + 2u * t + 1u));
-    return __builtin_amdgcn_readfirstlane(m) >= w;
-}
-
 template <int LAYOUT, bool ENV, bool COUNT, bool PRESENT>
 __device__ __forceinline__ void render_body_ct(const PtJob& job)
 {
     // chained launches: this block has started (the next launch's stream waits for every block of
     // this one: hipStreamWaitValue64 in pt_capi.cpp launch_chain)
-    if (job.started && threadIdx.x == 0)
-        __hip_atomic_fetch_add(job.started, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    pt_chain_started(job.started);
     const PtScene* __restrict__ sc = job.scene;
     constexpr int kWavesPerBlock = waves_per_block<ENV>();
     constexpr bool QV = true;
@@ -1390,37 +1350,15 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     auto ws_st = [&](int k, uint32_t v) {
         if (lane == 0) ws[k] = v;
     };
-    // Chained launches: before touching entry e's pixels, wait for the previous launch's epoch (rare:
-    // both launches take the tiles longest first, so the next launch reaches a tile long after the
-    // previous one has folded it).  Bounded: a wait of ~1.3 s is reported (PT_G_CHAIN_WAIT, every
-    // build) instead of hanging the GPU -- the host's stream gate makes it unreachable (launch_chain).
-#ifndef PT_CHAIN_CODE
-#define PT_CHAIN_CODE 1   // (A/B only: 0 compiles the chained-launch code out)
-#endif
+    // chained launches (pt_chain.h): before touching entry e's pixels, wait for the previous launch's
+    // epoch; after e's last pixel store, publish this launch's
     auto chain_wait_tile = [&](uint32_t e) {
-        if (!PT_CHAIN_CODE || job.chain_wait == 0u || chain_ready(job.tile_epoch, e, job.chain_wait)) return;
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        bool ok = false;
-        do {
-            __builtin_amdgcn_s_sleep(8);
-            ok = chain_ready(job.tile_epoch, e, job.chain_wait);
-        } while (!ok && __builtin_amdgcn_s_memrealtime() - t0 < (1ull << 27));   // (100 MHz)
-        if (!ok && lane == 0) pt_guard_report(job.err, PT_G_CHAIN_WAIT, pt_entry_tile(e));
+        if (job.chain_wait != 0u) pt_chain_wait(job.tile_epoch, e, job.chain_wait, job.err, lane);
     };
-    // ... and after entry e's last pixel store, publish this launch's epoch for it
     auto chain_publish = [&](uint32_t e) {
-        if (!PT_CHAIN_CODE || !job.tile_epoch) return;
-        if (__builtin_expect(job.chain_delay != 0u, 0)) {   // (test hook: the next launch meets unready tiles)
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * job.chain_delay) __builtin_amdgcn_s_sleep(8);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every lane's sc1 pixel stores have completed
-        if (lane == 0) {
-            const uint32_t t = pt_entry_tile(e), part = pt_entry_part(e);
-            if (part != 2u) __hip_atomic_store(job.tile_epoch + 2u * t, job.chain_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (part != 1u) __hip_atomic_store(job.tile_epoch + 2u * t + 1u, job.chain_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (job.tile_epoch) pt_chain_publish(job.tile_epoch, e, job.chain_seq, job.chain_delay, lane);
     };
+
     if (lane == 0) {
         ws[kWsTcur] = kNone;   // the tile being chunked (A's tile whenever A is set)
         ws[kWsFlags] = 0u;
@@ -1524,11 +1462,11 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 if (!items && PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) {
                     // the same radiance in every frame: fold all of the launch's frames now
                     float* px = job.buf + pi;
-                    V3 acc = v3(px_ld(px), px_ld(px + cs), px_ld(px + 2 * cs));
+                    V3 acc = v3(pt_px_ld(px), pt_px_ld(px + cs), pt_px_ld(px + 2 * cs));
                     for (int f = 0; f < S; ++f) acc = add(acc, mul(sub(c_keep, acc), weight(f)));
-                    px_st(px, acc.x);
-                    px_st(px + cs, acc.y);
-                    px_st(px + 2 * cs, acc.z);
+                    pt_px_st(px, acc.x);
+                    pt_px_st(px + cs, acc.y);
+                    pt_px_st(px + 2 * cs, acc.z);
                     present(lc, lr, acc);
                 }
             }
@@ -1604,7 +1542,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             size_t pi = out_index<LAYOUT>(job, lc, lr);
             if (!PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) pi = 0;   // (checked build: reported)
             float* px = job.buf + pi;
-            V3 acc = first ? v3(px_ld(px), px_ld(px + cs), px_ld(px + 2 * cs)) : v3(s_acc[wv][0][lane], s_acc[wv][1][lane], s_acc[wv][2][lane]);
+            V3 acc = first ? v3(pt_px_ld(px), pt_px_ld(px + cs), pt_px_ld(px + 2 * cs)) : v3(s_acc[wv][0][lane], s_acc[wv][1][lane], s_acc[wv][2][lane]);
 #pragma unroll
             for (int f = 0; f < kChunk; ++f) {
                 if (f < nfD) {
@@ -1614,9 +1552,9 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 }
             }
             if (last) {
-                px_st(px, acc.x);
-                px_st(px + cs, acc.y);
-                px_st(px + 2 * cs, acc.z);
+                pt_px_st(px, acc.x);
+                pt_px_st(px + cs, acc.y);
+                pt_px_st(px + 2 * cs, acc.z);
                 present(lc, lr, acc);
             } else {
                 s_acc[wv][0][lane] = acc.x;

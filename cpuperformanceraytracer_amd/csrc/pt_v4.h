@@ -77,6 +77,13 @@ struct PtV4Job {
     uint32_t* pix_out;
     int32_t pix_xrgb;               // PT_PIXEL_XRGB8 (OutputToScreen) else RGBA8 (OutputToFile)
     int32_t pix_fast_tone;
+    // chained launches (pt_v4_render_device_chain): as PtJob's (pt_kernel.h) -- the continuous-tiles
+    // kernel only
+    uint32_t* tile_epoch;
+    uint32_t chain_seq;
+    uint32_t chain_wait;
+    unsigned long long* started;
+    uint32_t chain_delay;
 };
 
 // Scene description in AddQuad/Sphere/MaterialToScene order (v4 :1368-1401).
@@ -92,5 +99,7 @@ int pt_v4_build_scene(const PtV4SceneDesc* d, PtV4Scene* out);     // Precompute
 bool pt_v4_is_default_geometry(const PtV4Scene& s);                // geometry == pt_v4_default_scene.h
 // *presented (optional): the launch also wrote job.pix_out (the fused output stage; only for the
 // presenting configuration, pt_v4.hip pt_launch_v4 -- otherwise the caller converts separately)
+// *ct_blocks (optional): the grid of the continuous-tiles kernel it launched (0: the per-tile pool, or
+// nothing launched) -- a chained launch's gate waits for that many started blocks.
 hipError_t pt_launch_v4(const PtV4Job& job, const PtV4Scene& scene, hipStream_t stream, bool count,
-                        bool* presented = nullptr);
+                        bool* presented = nullptr, uint32_t* ct_blocks = nullptr);

@@ -36,6 +36,7 @@
 #include "pt_v4_default_scene.h"
 #include "pt_tile_queue.h"
 #include "pt_guard.h"
+#include "pt_chain.h"
 #include "pt_wave.h"
 #include "pt_tonemap.h"
 #include <algorithm>
@@ -1072,6 +1073,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
     }
     __syncthreads();
 
+    pt_chain_started(job.started);   // (chained launches, pt_chain.h)
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     pt_queue_zero_next(job.queue_next);   // (pt_tile_queue.h)
@@ -1188,6 +1190,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
             tq.save(s_tq[wv], lane);
             ws_st(kVwFlags, tile == kNone ? 3u : 1u);
             if (tile == kNone) break;
+            if (job.chain_wait != 0u) pt_chain_wait(job.tile_epoch, tile, job.chain_wait, job.err, lane);   // (pt_chain.h)
             // (a queue entry is a tile or one half of it, pt_tile_queue.h)
             const int tcol = ((int)pt_entry_tile(tile) % tiles_x) * 8, trow = ((int)pt_entry_tile(tile) / tiles_x) * 8;
             const bool valid = (tcol + (lane & 7)) < job.ncols && trow + (lane >> 3) < job.nrows &&
@@ -1212,7 +1215,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
                 if (valid && !PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) pi = 0;   // (checked build: reported)
                 float* const acc_p = valid ? job.buf + pi : nullptr;
                 V3 acc = v3(0.0f, 0.0f, 0.0f);
-                if (valid && job.accumulate) acc = v3(acc_p[0], acc_p[cs], acc_p[2 * cs]);
+                if (valid && job.accumulate) acc = v3(pt_px_ld(acc_p), pt_px_ld(acc_p + cs), pt_px_ld(acc_p + 2 * cs));
                 for (; fsky < S; ++fsky) {
                     uint32_t r;
                     V3 d;
@@ -1235,12 +1238,13 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
                     }
                 }
                 if (fsky > 0 && valid) {   // (the pool's first chunk of the tile reads it back)
-                    acc_p[0] = acc.x;
-                    acc_p[cs] = acc.y;
-                    acc_p[2 * cs] = acc.z;
+                    pt_px_st(acc_p, acc.x);
+                    pt_px_st(acc_p + cs, acc.y);
+                    pt_px_st(acc_p + 2 * cs, acc.z);
                 }
                 if (fsky == S) {   // the whole tile: ~one pool iteration per frame (the schedule's cost)
                     if (rec_cost && lane == 0) pt_record_cost(job.cost, tile, ntiles, 1u + (uint32_t)fsky);
+                    if (job.tile_epoch) pt_chain_publish(job.tile_epoch, tile, job.chain_seq, job.chain_delay, lane);
                     continue;
                 }
             }
@@ -1275,7 +1279,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
             float* const acc_p = job.buf + pi;
             V3 acc = v3(0.0f, 0.0f, 0.0f);
             if (first) {
-                if (job.accumulate) acc = v3(acc_p[0], acc_p[cs], acc_p[2 * cs]);   // (:1233: only to blend)
+                if (job.accumulate) acc = v3(pt_px_ld(acc_p), pt_px_ld(acc_p + cs), pt_px_ld(acc_p + 2 * cs));   // (:1233: only to blend)
             } else {
                 acc = v3(s_acc[wv][0][lane], s_acc[wv][1][lane], s_acc[wv][2][lane]);
             }
@@ -1298,15 +1302,16 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
                 }
             }
             if (last) {
-                acc_p[0] = acc.x;
-                acc_p[cs] = acc.y;
-                acc_p[2 * cs] = acc.z;
+                pt_px_st(acc_p, acc.x);
+                pt_px_st(acc_p + cs, acc.y);
+                pt_px_st(acc_p + 2 * cs, acc.z);
             } else {
                 s_acc[wv][0][lane] = acc.x;
                 s_acc[wv][1][lane] = acc.y;
                 s_acc[wv][2][lane] = acc.z;
             }
         }
+        if (last && job.tile_epoch) pt_chain_publish(job.tile_epoch, tD, job.chain_seq, job.chain_delay, lane);
         if (rec_cost) {   // the schedule's cost: about the tile's pool iterations (its sky frames: one each)
             const uint32_t tile_seg = ws_ld(kVwTileSeg) + ws_ld(kVwSegD) + (first ? 64u * ws_ld(kVwSkyD) : 0u);
             ws_st(kVwTileSeg, last ? 0u : tile_seg);
@@ -1472,7 +1477,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
 }
 
 template <int ENV, int LAYOUT>
-hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool count)
+hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool count, uint32_t* ct_blocks_out)
 {
     const int tiles = ((j.ncols + 7) / 8) * ((j.nrows + 7) / 8);
     const dim3 block(64 * kWaves);
@@ -1489,6 +1494,7 @@ hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool 
         if (j.ct_slots && ct_waves <= j.ct_waves && j.nframes >= kChunk &&
             (j.ct_force || (uint64_t)j.nframes * (uint64_t)tiles >= 4ull * kChunk * ct_waves)) {
             hipLaunchKernelGGL(ct_kern, dim3((unsigned)ct_blocks), block, 0, st, j, sc);
+            if (ct_blocks_out) *ct_blocks_out = (uint32_t)ct_blocks;
             return;
         }
         const long blocks = std::min<long>(pt_resident_blocks(kern, 64 * kWaves), (tiles + kWaves - 1) / kWaves);
@@ -1534,21 +1540,23 @@ hipError_t launch_t(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool 
 }
 
 template <int ENV>
-hipError_t launch_env(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool count)
+hipError_t launch_env(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, bool count, uint32_t* ct_blocks)
 {
     switch (j.layout) {
-        case PT_LAYOUT_INTERLEAVED: return launch_t<ENV, PT_LAYOUT_INTERLEAVED>(j, sc, st, count);
-        case PT_LAYOUT_PLANAR8: return launch_t<ENV, PT_LAYOUT_PLANAR8>(j, sc, st, count);
-        case PT_LAYOUT_TILED_PLANAR8: return launch_t<ENV, PT_LAYOUT_TILED_PLANAR8>(j, sc, st, count);
+        case PT_LAYOUT_INTERLEAVED: return launch_t<ENV, PT_LAYOUT_INTERLEAVED>(j, sc, st, count, ct_blocks);
+        case PT_LAYOUT_PLANAR8: return launch_t<ENV, PT_LAYOUT_PLANAR8>(j, sc, st, count, ct_blocks);
+        case PT_LAYOUT_TILED_PLANAR8: return launch_t<ENV, PT_LAYOUT_TILED_PLANAR8>(j, sc, st, count, ct_blocks);
         default: return hipErrorInvalidValue;
     }
 }
 
 }  // namespace
 
-hipError_t pt_launch_v4(const PtV4Job& j_in, const PtV4Scene& sc, hipStream_t st, bool count, bool* presented)
+hipError_t pt_launch_v4(const PtV4Job& j_in, const PtV4Scene& sc, hipStream_t st, bool count, bool* presented,
+                        uint32_t* ct_blocks)
 {
     if (presented) *presented = false;
+    if (ct_blocks) *ct_blocks = 0;
     if (j_in.ncols <= 0 || j_in.nrows <= 0 || j_in.nframes <= 0) return hipSuccess;
     // the fused output stage (j.pix_out) runs in the presenting instances only: the drop-in's calls
     // (DemofoxRenderOptV4: the tiled layout, one frame -- the per-tile pool kernel), the default scene
@@ -1563,9 +1571,9 @@ hipError_t pt_launch_v4(const PtV4Job& j_in, const PtV4Scene& sc, hipStream_t st
     if (count && !j.counters) return hipErrorInvalidValue;
     if (!j.queue || (j.order && (!j.units || !j.nunits))) return hipErrorInvalidValue;
     switch (j.env_mode) {
-        case PT_V4_ENV_NONE_: return launch_env<PT_V4_ENV_NONE_>(j, sc, st, count);
-        case PT_V4_ENV_EQUIRECT_: return launch_env<PT_V4_ENV_EQUIRECT_>(j, sc, st, count);
-        case PT_V4_ENV_CUBEMAP_: return launch_env<PT_V4_ENV_CUBEMAP_>(j, sc, st, count);
+        case PT_V4_ENV_NONE_: return launch_env<PT_V4_ENV_NONE_>(j, sc, st, count, ct_blocks);
+        case PT_V4_ENV_EQUIRECT_: return launch_env<PT_V4_ENV_EQUIRECT_>(j, sc, st, count, ct_blocks);
+        case PT_V4_ENV_CUBEMAP_: return launch_env<PT_V4_ENV_CUBEMAP_>(j, sc, st, count, ct_blocks);
         default: return hipErrorInvalidValue;
     }
 }

@@ -164,8 +164,8 @@ class JobLauncher:
             fn, args = L.pt_render_device_present, (self._ref, pixels.data_ptr(), pixel_format, self._stream)
             self._what = "pt_render_device_present"
         else:
-            # chain (the diffuse renderer): pt_render_device_chain, consecutive launches overlap
-            self._what = "pt_v4_render_device" if v4 else ("pt_render_device_chain" if chain else "pt_render_device")
+            # chain: pt_render_device_chain / pt_v4_render_device_chain, consecutive launches overlap
+            self._what = ("pt_v4_render_device" if v4 else "pt_render_device") + ("_chain" if chain else "")
             fn = getattr(L, self._what)
             args = (self._ref, self._stream)
         self._fn, self._args = fn, args

@@ -293,6 +293,9 @@ int pt_v4_begin_frame(void);
 /* HBM-resident v4 job (bench / shards): the interleaved or planar8 layout; use_env selects the
  * config's env mode with the map of pt_set_env_map (else the ambient); num_bounces from the job */
 int pt_v4_render_device(const pt_device_job* job, void* hip_stream);
+/* pt_v4_render_device for consecutive launches of one geometry: may overlap the previous chained launch
+ * of that geometry on this stream, same result (the contract of pt_render_device_chain) */
+int pt_v4_render_device_chain(const pt_device_job* job, void* hip_stream);
 int pt_v4_count_device(const pt_device_job* job, void* hip_stream, pt_work_counts* out);   /* sync */
 
 /* --- tile work queue: the host tile scheduler, on the GPU ------------------------
@@ -323,9 +326,10 @@ int pt_render_device(const pt_device_job* job, void* hip_stream);      /* async 
  * run overlapped with the previous pt_render_device_chain launch of that geometry on this stream (on
  * two streams of the library's; the next launch's waves fill the CUs where the previous launch's last
  * waves end), with every pixel's frames still accumulated in order -- bit for bit the result of
- * pt_render_device.  The caller promises that nothing enqueued on hip_stream since its previous chained
- * call of this geometry is needed by this launch (so the launch does not wait for it); anything the
- * caller enqueues on hip_stream after this call is ordered after the launch, as with pt_render_device.
+ * pt_render_device.  The launch does not wait for work enqueued on hip_stream since the previous
+ * chained call: such work must not read or write the buffer unless it has completed before this call
+ * (the caller synchronised), else make this call a plain pt_render_device.  Anything the caller
+ * enqueues on hip_stream after this call is ordered after the launch, as with pt_render_device.
  * Any other launch on the device (another geometry, pt_render_device, counting, v4, host-buffer
  * calls) ends the overlap: the next chained call then waits for hip_stream as pt_render_device does.
  * Async on hip_stream. */

@@ -12,8 +12,11 @@ K=${2:-}
 timeout -k 10 800 python -u -m pytest tests/test_gpu_chain.py -x -v --timeout 400 --timeout-method thread --durations=0 \
     ${K:+-k "$K"} > "$OUT/chain_tests.log" 2>&1 || { tail -40 "$OUT/chain_tests.log"; exit 1; }
 tail -15 "$OUT/chain_tests.log"
-timeout -k 10 200 python bench.py --no-cpu-baseline --no-configs4 > "$OUT/bench_chain.json" 2> "$OUT/bench_chain.err" || { tail -20 "$OUT/bench_chain.err"; exit 1; }
-timeout -k 10 200 python bench.py --no-cpu-baseline --no-configs4 --no-chain > "$OUT/bench_nochain.json" 2> "$OUT/bench_nochain.err" || { tail -20 "$OUT/bench_nochain.err"; exit 1; }
-for f in bench_chain bench_nochain; do
+WL=${WORKLOADS:-c2_1080p}
+for wl in $WL; do
+    timeout -k 10 200 python bench.py --workload "$wl" --no-cpu-baseline --no-configs4 > "$OUT/bench_chain_$wl.json" 2> "$OUT/bench_chain_$wl.err" || { tail -20 "$OUT/bench_chain_$wl.err"; exit 1; }
+    timeout -k 10 200 python bench.py --workload "$wl" --no-cpu-baseline --no-configs4 --no-chain > "$OUT/bench_nochain_$wl.json" 2> "$OUT/bench_nochain_$wl.err" || { tail -20 "$OUT/bench_nochain_$wl.err"; exit 1; }
+done
+for f in $(for wl in $WL; do echo bench_chain_$wl bench_nochain_$wl; done); do
     python3 -c "import json;d=json.loads(open('$OUT/$f.json').read().strip().splitlines()[-1]);print('$f', d['ms_per_step'], '%.3e' % d['value'], round(d['roofline']['frac'], 4), d.get('launch_chain'))"
 done

@@ -32,31 +32,33 @@ def fresh(monkeypatch):
         pt.init(num_bounces=B)
     yield init
     pt.shutdown()
-    for k in ("PT_MI355_CT_WAVES", "PT_MI355_BACK", "PT_MI355_TEST_CHAIN_DELAY"):
+    for k in ("PT_MI355_CT_WAVES", "PT_MI355_BACK", "PT_MI355_TEST_CHAIN_DELAY", "PT_MI355_V4_CT"):
         monkeypatch.delenv(k, raising=False)
 
 
 def _series(W, H, B, S, launches, *, row_start=0, row_stride=1, nrows=None, env=False, plain_at=(), count_at=(),
-            sync_at=()):
+            sync_at=(), v4=False):
     """`launches` launches of S frames (frames 1 .. launches*S) into a zeroed buffer on the current
     stream: chained (JobLauncher(chain=True), as bench.py), except a plain pt_render_device launch at
     the indices in plain_at; a counted launch on a scratch buffer after the indices in count_at and a
     device synchronisation after those in sync_at.  Returns (image, frames, chain counts)."""
     import torch
-    from cpuperformanceraytracer_amd.device import JobLauncher, chain_counts, check_device_errors, count_device
+    from cpuperformanceraytracer_amd.device import (JobLauncher, chain_counts, check_device_errors, count_device,
+                                                    count_v4_device)
     nrows = H if nrows is None else nrows
     stream = torch.cuda.current_stream()
     buf = torch.zeros(nrows * W * 3, dtype=torch.float32, device="cuda:0")
     scratch = torch.zeros_like(buf)
     kw = dict(nframes=S, num_bounces=B, row_start=row_start, row_stride=row_stride, nrows=nrows, use_env=env,
               stream=stream)
-    chained, plain = JobLauncher(buf, W, H, chain=True, **kw), JobLauncher(buf, W, H, **kw)
+    chained, plain = JobLauncher(buf, W, H, chain=True, v4=v4, **kw), JobLauncher(buf, W, H, v4=v4, **kw)
+    cfn = count_v4_device if v4 else count_device
     c0 = chain_counts()
     frame = 1
     for k in range(launches):
         (plain if k in plain_at else chained)(frame)
         if k in count_at:
-            count_device(scratch, W, H, frame_first=frame, **{a: kw[a] for a in kw if a != "nframes"}, nframes=S)
+            cfn(scratch, W, H, frame_first=frame, **{a: kw[a] for a in kw if a != "nframes"}, nframes=S)
         if k in sync_at:
             torch.cuda.synchronize()
         frame += S
@@ -168,4 +170,39 @@ def test_c4_env_chained_matches_oracle(fresh):
     img, frames, counts = _series(W, H, B, S, 7, env=True)
     assert counts["continued"] >= 4, counts
     ref = pyoracle.render(W, H, nframes=frames, num_bounces=B, env=env)
+    assert bits_equal(img, ref), mismatch_report(img, ref)
+
+
+def test_v4_chained_matches_oracle(fresh):
+    """The v4 workload chained (pt_v4_render_device_chain): 1920x1080, 8 spp, 8 bounces, the default
+    glass scene and the synthetic 2k equirect map, 12 launches with a counted launch at 4 (the
+    continuous-tiles v4 kernel, its sky frames published at the claim): rows 5::90 after 96 frames
+    equal the v4 oracle."""
+    import cpuperformanceraytracer_amd as pt
+    from cpuperformanceraytracer_amd.config import synthetic_env
+    W, H, B, S = 1920, 1080, 8, 8
+    fresh(B)
+    env = synthetic_env()
+    pt.v4_config(num_bounces=B)
+    pt.set_env_map(env)
+    img, frames, counts = _series(W, H, B, S, 12, env=True, v4=True, count_at=(4,))
+    assert counts["continued"] >= 6, counts
+    for k in range(5, H, 90):
+        ref = pyoracle.render4(W, H, nframes=frames, num_bounces=B, row_start=k, row_stride=1, nrows=1, env=env)
+        assert bits_equal(img[k:k + 1], ref), (k, mismatch_report(img[k:k + 1], ref))
+
+
+def test_v4_chained_waits_match_oracle(fresh):
+    """v4 chained with forced waits (PT_MI355_TEST_CHAIN_DELAY) and the continuous-tiles kernel forced
+    (PT_MI355_V4_CT) at 640x360: the whole image equals the v4 oracle."""
+    import cpuperformanceraytracer_amd as pt
+    from cpuperformanceraytracer_amd.config import synthetic_env
+    W, H, B, S = 640, 360, 8, 8
+    fresh(B, PT_MI355_TEST_CHAIN_DELAY="300", PT_MI355_V4_CT="1")
+    env = synthetic_env()
+    pt.v4_config(num_bounces=B)
+    pt.set_env_map(env)
+    img, frames, counts = _series(W, H, B, S, 8, env=True, v4=True)
+    assert counts["continued"] >= 5, counts
+    ref = pyoracle.render4(W, H, nframes=frames, num_bounces=B, env=env)
     assert bits_equal(img, ref), mismatch_report(img, ref)
