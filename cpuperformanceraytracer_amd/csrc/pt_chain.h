@@ -35,6 +35,43 @@ __device__ __forceinline__ void pt_px_st(float* p, float v)
     __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// A pixel's three channels at element pi of the accumulator `buf` (channel stride cs).  The interleaved
+// layout (cs = 1) keeps one 12-byte access per pixel: a raw buffer load / store of 96 bits with the
+// sc1 cache policy (buffer_load/store_dwordx3 ... sc1) over the job's buffer (nbytes: its size, < 2^31;
+// 0: the per-channel accesses above), so a tile row's eight pixels stay one 96-byte write -- three
+// dword sc1 stores per pixel wrote each dword through on its own (c2: 217 vs 177 MB of WRITE_SIZE).
+typedef unsigned pt_v3u __attribute__((ext_vector_type(3)));
+typedef float pt_v3f __attribute__((ext_vector_type(3)));
+constexpr int kPtCpolSc1 = 16;               // CPol::SC1 (gfx940+ cache-policy bits of the buffer intrinsics)
+constexpr int kPtBufRsrcWord3 = 0x00020000;  // raw (untyped) buffer resource, the gfx9 data-format word
+__device__ __forceinline__ void pt_px_ld3(const float* buf, uint32_t nbytes, size_t cs, size_t pi, float& x, float& y, float& z)
+{
+    if (cs == 1 && nbytes) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(buf), 0, (int)nbytes, kPtBufRsrcWord3);
+        // (the whole vector is bit-cast: element-wise bit casts of the u32 vector made this compiler
+        // shrink the load to its first dword -- tests/test_isa_lgkm.py checks the built loads)
+        const pt_v3f v = __builtin_bit_cast(pt_v3f, __builtin_amdgcn_raw_buffer_load_b96(r, (int)(pi * 4u), 0, kPtCpolSc1));
+        x = v.x, y = v.y, z = v.z;
+        return;
+    }
+    x = pt_px_ld(buf + pi), y = pt_px_ld(buf + pi + cs), z = pt_px_ld(buf + pi + 2 * cs);
+}
+__device__ __forceinline__ void pt_px_st3(float* buf, uint32_t nbytes, size_t cs, size_t pi, float x, float y, float z)
+{
+    if (cs == 1 && nbytes) {
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(buf, 0, (int)nbytes, kPtBufRsrcWord3);
+        const pt_v3f v = {x, y, z};
+        __builtin_amdgcn_raw_buffer_store_b96(__builtin_bit_cast(pt_v3u, v), r, (int)(pi * 4u), 0, kPtCpolSc1);
+        return;
+    }
+    pt_px_st(buf + pi, x), pt_px_st(buf + pi + cs, y), pt_px_st(buf + pi + 2 * cs, z);
+}
+// the accumulator's size in bytes for pt_px_ld3 / pt_px_st3 (0: too large for a buffer resource)
+__device__ __forceinline__ uint32_t pt_px_nbytes(size_t floats)
+{
+    return floats * 4u < (1ull << 31) ? (uint32_t)(floats * 4u) : 0u;
+}
+
 // the block has started (the next chained launch's stream gate); started: nullptr when not chained
 __device__ __forceinline__ void pt_chain_started(unsigned long long* started)
 {

@@ -1298,7 +1298,8 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     if (!PT_GUARD(job.err, blockIdx.x * (uint32_t)kWavesPerBlock + (uint32_t)wv < job.ct_waves, PT_G_SLOT_BASE,
                   blockIdx.x * (uint32_t)kWavesPerBlock + (uint32_t)wv))
         return;
-    const size_t px_extent = pixel_extent<LAYOUT>(job);   // (guards only)
+    const size_t px_extent = pixel_extent<LAYOUT>(job);   // (guards; the accumulator's buffer resource)
+    const uint32_t pxb = pt_px_nbytes(px_extent);          // (pt_chain.h pt_px_ld3 / pt_px_st3)
     // lerp weight of frame f of the launch: the table, or its correctly rounded reciprocal (:812)
     auto weight = [&](int f) {
         return f < kMaxWeights ? s_w[f] : pt::rcp_rn((float)(job.frame_first + (uint32_t)f) + 1.0f);
@@ -1461,12 +1462,10 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 const size_t pi = out_index<LAYOUT>(job, lc, lr);
                 if (!items && PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) {
                     // the same radiance in every frame: fold all of the launch's frames now
-                    float* px = job.buf + pi;
-                    V3 acc = v3(pt_px_ld(px), pt_px_ld(px + cs), pt_px_ld(px + 2 * cs));
+                    V3 acc;
+                    pt_px_ld3(job.buf, pxb, cs, pi, acc.x, acc.y, acc.z);
                     for (int f = 0; f < S; ++f) acc = add(acc, mul(sub(c_keep, acc), weight(f)));
-                    pt_px_st(px, acc.x);
-                    pt_px_st(px + cs, acc.y);
-                    pt_px_st(px + 2 * cs, acc.z);
+                    pt_px_st3(job.buf, pxb, cs, pi, acc.x, acc.y, acc.z);
                     present(lc, lr, acc);
                 }
             }
@@ -1541,8 +1540,9 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
             const int lc = (int)(tdi % (uint32_t)tiles_x) * 8 + (lane & 7), lr = (int)(tdi / (uint32_t)tiles_x) * 8 + (lane >> 3);
             size_t pi = out_index<LAYOUT>(job, lc, lr);
             if (!PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) pi = 0;   // (checked build: reported)
-            float* px = job.buf + pi;
-            V3 acc = first ? v3(pt_px_ld(px), pt_px_ld(px + cs), pt_px_ld(px + 2 * cs)) : v3(s_acc[wv][0][lane], s_acc[wv][1][lane], s_acc[wv][2][lane]);
+            V3 acc;
+            if (first) pt_px_ld3(job.buf, pxb, cs, pi, acc.x, acc.y, acc.z);
+            else acc = v3(s_acc[wv][0][lane], s_acc[wv][1][lane], s_acc[wv][2][lane]);
 #pragma unroll
             for (int f = 0; f < kChunk; ++f) {
                 if (f < nfD) {
@@ -1552,9 +1552,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
                 }
             }
             if (last) {
-                pt_px_st(px, acc.x);
-                pt_px_st(px + cs, acc.y);
-                pt_px_st(px + 2 * cs, acc.z);
+                pt_px_st3(job.buf, pxb, cs, pi, acc.x, acc.y, acc.z);
                 present(lc, lr, acc);
             } else {
                 s_acc[wv][0][lane] = acc.x;

@@ -1085,7 +1085,8 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
     if (!PT_GUARD(job.err, blockIdx.x * (uint32_t)kWaves + (uint32_t)wv < job.ct_waves, PT_G_SLOT_BASE,
                   blockIdx.x * (uint32_t)kWaves + (uint32_t)wv))
         return;
-    const size_t px_extent = pixel_extent<LAYOUT>(job);   // (guards only)
+    const size_t px_extent = pixel_extent<LAYOUT>(job);   // (guards; the accumulator's buffer resource)
+    const uint32_t pxb = pt_px_nbytes(px_extent);          // (pt_chain.h pt_px_ld3 / pt_px_st3)
     const size_t cs = (LAYOUT == PT_LAYOUT_INTERLEAVED) ? 1u : 8u;
     const Tex tex{job.env, job.env_w, job.env_h};
     const bool random = DFL || job.random_jitter != 0, rejection = DFL || job.rejection != 0;
@@ -1213,9 +1214,8 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
                 const int orow = LAYOUT == PT_LAYOUT_TILED_PLANAR8 ? job.row_start + pr * job.row_stride : pr;
                 size_t pi = valid ? out_index<LAYOUT>(job, X, orow) : 0;
                 if (valid && !PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) pi = 0;   // (checked build: reported)
-                float* const acc_p = valid ? job.buf + pi : nullptr;
                 V3 acc = v3(0.0f, 0.0f, 0.0f);
-                if (valid && job.accumulate) acc = v3(pt_px_ld(acc_p), pt_px_ld(acc_p + cs), pt_px_ld(acc_p + 2 * cs));
+                if (valid && job.accumulate) pt_px_ld3(job.buf, pxb, cs, pi, acc.x, acc.y, acc.z);
                 for (; fsky < S; ++fsky) {
                     uint32_t r;
                     V3 d;
@@ -1237,11 +1237,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
                         if (COUNT) ++n_seg, ++n_sky, ++n_esc;
                     }
                 }
-                if (fsky > 0 && valid) {   // (the pool's first chunk of the tile reads it back)
-                    pt_px_st(acc_p, acc.x);
-                    pt_px_st(acc_p + cs, acc.y);
-                    pt_px_st(acc_p + 2 * cs, acc.z);
-                }
+                if (fsky > 0 && valid) pt_px_st3(job.buf, pxb, cs, pi, acc.x, acc.y, acc.z);   // (the pool's first chunk reads it back)
                 if (fsky == S) {   // the whole tile: ~one pool iteration per frame (the schedule's cost)
                     if (rec_cost && lane == 0) pt_record_cost(job.cost, tile, ntiles, 1u + (uint32_t)fsky);
                     if (job.tile_epoch) pt_chain_publish(job.tile_epoch, tile, job.chain_seq, job.chain_delay, lane);
@@ -1276,10 +1272,9 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
             const int orow = LAYOUT == PT_LAYOUT_TILED_PLANAR8 ? job.row_start + pr * job.row_stride : pr;
             size_t pi = out_index<LAYOUT>(job, px, orow);
             if (!PT_GUARD(job.err, pi + 2 * cs < px_extent, PT_G_PIXEL, pi)) pi = 0;   // (checked build: reported)
-            float* const acc_p = job.buf + pi;
             V3 acc = v3(0.0f, 0.0f, 0.0f);
             if (first) {
-                if (job.accumulate) acc = v3(pt_px_ld(acc_p), pt_px_ld(acc_p + cs), pt_px_ld(acc_p + 2 * cs));   // (:1233: only to blend)
+                if (job.accumulate) pt_px_ld3(job.buf, pxb, cs, pi, acc.x, acc.y, acc.z);   // (:1233: only to blend)
             } else {
                 acc = v3(s_acc[wv][0][lane], s_acc[wv][1][lane], s_acc[wv][2][lane]);
             }
@@ -1302,9 +1297,7 @@ __global__ __launch_bounds__(64 * kWaves) PT_V4_CT_OCC void pt_v4_ct_kernel(PtV4
                 }
             }
             if (last) {
-                pt_px_st(acc_p, acc.x);
-                pt_px_st(acc_p + cs, acc.y);
-                pt_px_st(acc_p + 2 * cs, acc.z);
+                pt_px_st3(job.buf, pxb, cs, pi, acc.x, acc.y, acc.z);
             } else {
                 s_acc[wv][0][lane] = acc.x;
                 s_acc[wv][1][lane] = acc.y;

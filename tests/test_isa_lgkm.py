@@ -71,3 +71,20 @@ def test_no_inline_asm_touches_lds_or_waits():
             assert not re.search(r"\b(ds_|s_waitcnt|buffer_|global_|flat_|scratch_|s_load|s_store)", body), (f.name, body)
             assert body.startswith("v_mov_b32"), (f.name, body)
     assert seen >= 1
+
+
+def test_accumulator_buffer_accesses_are_whole_pixels():
+    """pt_chain.h's 96-bit sc1 buffer accesses of the accumulator: every buffer load / store in the
+    built library is a dwordx3 of the continuous-tiles pools (one 12-byte pixel).  An element-wise
+    bit cast of the intrinsic's u32 vector once made the compiler shrink the load to its first dword
+    (the other two channels then undefined) -- this catches that form."""
+    if not LIB.exists():
+        pytest.skip("libpt_mi355.so not built")
+    n = 0
+    for name, co in I.code_objects(LIB):
+        for f, ins in I.parse_functions(I.disassemble(co)).items():
+            for _, mn, ops, _ in ins:
+                if mn.startswith("buffer_"):
+                    n += 1
+                    assert mn in ("buffer_load_dwordx3", "buffer_store_dwordx3") and "sc1" in ops and "_ct_" in f, (f, mn, ops)
+    assert n >= 20
