@@ -91,11 +91,12 @@ def test_c2_chained_regime_matches_oracle(fresh):
 
 
 def test_c2_chained_whole_image_matches_oracle(fresh):
-    """configs[1] chained at the launch variant the timing picks for it (6 waves per SIMD, 45 % back
-    claims), 24 launches -- all but the first two continue the overlap: the whole image after 192
-    frames equals the oracle bit for bit (a stale accumulator read would show as scattered pixels)."""
+    """configs[1] chained at 6 waves per SIMD (the timing's pick for it), 24 launches -- all but the
+    first two continue the overlap, claiming their dynamic units cheapest-first (pt_capi.cpp
+    kChainBack): the whole image after 192 frames equals the oracle bit for bit (a stale accumulator
+    read would show as scattered pixels)."""
     W, H, B, S = 1920, 1080, 8, 8
-    fresh(B, PT_MI355_CT_WAVES="6", PT_MI355_BACK="45")
+    fresh(B, PT_MI355_CT_WAVES="6")
     img, frames, counts = _series(W, H, B, S, 24)
     assert counts["continued"] >= 21, counts
     ref = pyoracle.render(W, H, nframes=frames, num_bounces=B)
