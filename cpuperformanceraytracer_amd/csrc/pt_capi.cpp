@@ -193,6 +193,7 @@ struct State {
     int64_t test_bad_entry = -1;   // PT_MI355_TEST_BAD_ENTRY (test hook, pt_init)
     bool no_ct = false;   // PT_MI355_NO_CT=1 (read by pt_init): one-chunk launches on render_body (A/B)
     uint32_t test_chain_delay = 0;   // PT_MI355_TEST_CHAIN_DELAY=<us> (pt_init): chained launches publish late
+    uint32_t unit_mult = 2;          // PT_MI355_UNIT_MULT (pt_init, A/B): the diffuse CT schedule's unit multiple
 };
 
 State g;
@@ -664,7 +665,7 @@ int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls, uin
             // lanes no longer idle in a unit's tail while the dequeues still cost (A/B, 60 launches:
             // 1080p 8 spp 0.2497 vs 0.2525 ms, env 16 spp 0.4911 vs 0.4961, 4K 8 spp 0.8185 vs 0.8202;
             // 3x: 0.2513 / 0.4965 / 0.8356)
-            const uint32_t unit_mult = key.kind == 0 && !g.no_ct ? 2u : 1u;
+            const uint32_t unit_mult = key.kind == 0 && !g.no_ct ? g.unit_mult : 1u;
             hipError_t e = pt_launch_schedule(s->cost, s->order, s->units, s->units + 2 * s->key.ntiles + 1, s->key.ntiles,
                                               split, unit_mult, st, dv.derr);
             if (e != hipSuccess) return fail(PT_EHIP, "schedule launch failed: %s", hipGetErrorString(e));
@@ -1698,6 +1699,7 @@ int pt_init(const pt_config* cfg)
     g.ring_guard_cap = ~0u;
     g.no_ct = getenv("PT_MI355_NO_CT") && !strcmp(getenv("PT_MI355_NO_CT"), "1");
     g.test_chain_delay = getenv("PT_MI355_TEST_CHAIN_DELAY") ? (uint32_t)strtoul(getenv("PT_MI355_TEST_CHAIN_DELAY"), nullptr, 10) : 0u;
+    g.unit_mult = getenv("PT_MI355_UNIT_MULT") ? std::max<uint32_t>(1u, (uint32_t)strtoul(getenv("PT_MI355_UNIT_MULT"), nullptr, 10)) : 2u;
     g.v4_ct_force = getenv("PT_MI355_V4_CT") && !strcmp(getenv("PT_MI355_V4_CT"), "1");
     g.ct_back_pct = 20;
     g.back_set = false;
