@@ -704,8 +704,22 @@ def drive(args, wl, rank: int, world: int, ops, render_fn, count_fn, hooks: Hook
     left rank 0 waiting in its all-reduce: ADVICE round 5).  leg_workload: the strong leg's workload
     (default configs[4], c5_8k; tests pass a tiny one)."""
     from cpuperformanceraytracer_amd.shard import rows_of
-    res = run(args, wl, rank, world, ops, render_fn, count_fn, rehearse=rehearse, chain_counts=hooks.chain_counts)
-    hooks.check_errors()   # no launch of the run abandoned a tile (PT_EKERNEL otherwise)
+    from cpuperformanceraytracer_amd._native import PtError
+    try:
+        res = run(args, wl, rank, world, ops, render_fn, count_fn, rehearse=rehearse, chain_counts=hooks.chain_counts)
+        hooks.check_errors()   # no launch of the run abandoned a tile (PT_EKERNEL otherwise)
+    except PtError as e:
+        # A chained launch whose wait for its predecessor's tile ran out (guard PT_G_CHAIN_WAIT: the
+        # predecessor's waves stopped running -- DESIGN.md 3e, "Residency"): the run's accumulator is
+        # invalid and the error stands for it; the line is measured again with plain launches (one
+        # rank: N ranks would leave the others in the run's collectives), and says so.
+        if hooks.chain_counts is None or world > 1 or "guard 13 (chained launch" not in str(e):
+            raise
+        print(f"bench: chained run failed ({e}); measuring again with plain launches", file=sys.stderr)
+        res = run(args, wl, rank, world, ops, render_fn, count_fn, rehearse=rehearse, chain_counts=None)
+        hooks.check_errors()
+        if res is not None:
+            res["launch_chain"] = {"enabled": False, "chained_run_failed": str(e)[:400]}
     acc = None
     if res is not None:
         acc = res.pop("_accumulator")

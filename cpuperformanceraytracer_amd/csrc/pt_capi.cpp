@@ -345,7 +345,8 @@ const char* guard_name(uint32_t id)
         case PT_G_SCHED_UNIT: return "schedule builder: unit index out of range";
         case PT_G_RECORD: return "item record slot >= 64";
         case PT_G_QUEUE_GROUP: return "queue group out of range";
-        case PT_G_CHAIN_WAIT: return "chained launch: the previous launch's tile never became ready";
+        case PT_G_CHAIN_WAIT: return "chained launch: the previous launch's tile never became ready; value: the tile | its epoch's lag "
+                                     "<< 24 | bit 31 when an atomic read also lags (pt_chain.h)";
         default: return "unknown";
     }
 }
@@ -376,8 +377,8 @@ int sync_all()
         HIP_TRY(hipStreamSynchronize(dv.stream));
         if (guards)
             return fail(PT_EKERNEL, "device %d: %u kernel bounds guard failure(s), the first: guard %u (%s), value %u; "
-                        "the accumulator is invalid", dv.ordinal, guards, (uint32_t)(first >> 32),
-                        guard_name((uint32_t)(first >> 32)), (uint32_t)first);
+                        "pool guards: %u (first tile %u); the accumulator is invalid", dv.ordinal, guards,
+                        (uint32_t)(first >> 32), guard_name((uint32_t)(first >> 32)), (uint32_t)first, n, n ? tile : 0u);
         return fail(PT_EKERNEL, "device %d: a pool guard (ring iterations or continuous-tiles chunks) abandoned %u "
                     "tile(s) (first: tile %u of its launch); the accumulator is invalid", dv.ordinal, n, tile);
     }

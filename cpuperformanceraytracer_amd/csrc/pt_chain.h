@@ -96,18 +96,62 @@ __device__ __forceinline__ bool pt_chain_ready(const uint32_t* ep, uint32_t e, u
 
 // (the whole wave) before touching entry e's pixels: wait until the previous launch has published it.
 // Rare -- both launches take the tiles longest first, so a launch reaches a tile long after its
-// predecessor folded it.  Bounded: after ~1.3 s the wait is reported (guard PT_G_CHAIN_WAIT, every
-// build) instead of hanging the GPU; the host's stream gate makes that unreachable.
-__device__ __forceinline__ void pt_chain_wait(const uint32_t* ep, uint32_t e, uint32_t w, uint32_t* err, int lane)
+// predecessor folded it.  Bounded: after 2^21 polls (>= 2 s of the wave's own running time) the wait is
+// reported (guard PT_G_CHAIN_WAIT, every build) instead of hanging the GPU; the host's stream gate makes
+// that unreachable.  The bound counts polls, not wall-clock time: while the process's queues are
+// preempted the waves do not run, and a wall-clock bound (round 6's first form, 1.3 s of
+// s_memrealtime) would end every wait in progress when they resume.
+//
+// PT_CHAIN_DIAG=1 (a diagnostic build, scripts/build_variant.sh): words 34-36 of a continuing launch's
+// tile-queue block count its waves, the ones that ended and the ones waiting; a wait that runs out
+// (after 2^16 polls there) prints them for the launch and its predecessor.
+#ifndef PT_CHAIN_DIAG
+#define PT_CHAIN_DIAG 0
+#endif
+constexpr uint32_t kPtChainPolls = PT_CHAIN_DIAG ? 1u << 16 : 1u << 21;
+constexpr uint32_t kPtDiagWaves = 34, kPtDiagEnded = 35, kPtDiagWaiting = 36;
+// (diag) the tile-queue block of the chained launch before the one whose block is q (seq: its number)
+__device__ __forceinline__ unsigned* pt_chain_diag_prev(unsigned* q, uint32_t seq)
+{
+    return q - (size_t)(seq % 4u) * PT_QUEUE_WORDS + (size_t)((seq + 3u) % 4u) * PT_QUEUE_WORDS;
+}
+__device__ __forceinline__ void pt_chain_wait(const uint32_t* ep, uint32_t e, uint32_t w, uint32_t* err, int lane,
+                                              unsigned* qdiag = nullptr)
 {
     if (pt_chain_ready(ep, e, w)) return;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     bool ok = false;
+    uint32_t polls = 0;
+    if (PT_CHAIN_DIAG && qdiag && lane == 0) atomicAdd(qdiag + kPtDiagWaiting, 1u);
     do {
-        __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_s_sleep(8);   // (~0.2 us; a poll's sc1 loads take ~1-2 us more)
         ok = pt_chain_ready(ep, e, w);
-    } while (!ok && __builtin_amdgcn_s_memrealtime() - t0 < (1ull << 27));   // (100 MHz)
-    if (!ok && lane == 0) pt_guard_report(err, PT_G_CHAIN_WAIT, pt_entry_tile(e));
+    } while (!ok && ++polls < kPtChainPolls);
+    if (PT_CHAIN_DIAG && qdiag && lane == 0) atomicSub(qdiag + kPtDiagWaiting, 1u);
+#if PT_CHAIN_DIAG
+    if (!ok && lane == 0 && qdiag) {
+        unsigned* const qp = pt_chain_diag_prev(qdiag, w + 1u);
+        auto rd = [](unsigned* p) { return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+        const uint32_t t = pt_entry_tile(e);
+        printf("chain wait ran out: launch %u entry %u (tile %u) epochs %u %u | this launch: waves %u ended %u waiting %u "
+               "| previous: waves %u ended %u waiting %u | block %u wave %u\n",
+               w + 1u, e, t, rd(const_cast<uint32_t*>(ep + 2u * t)), rd(const_cast<uint32_t*>(ep + 2u * t + 1u)),
+               rd(qdiag + kPtDiagWaves), rd(qdiag + kPtDiagEnded), rd(qdiag + kPtDiagWaiting), rd(qp + kPtDiagWaves),
+               rd(qp + kPtDiagEnded), rd(qp + kPtDiagWaiting), blockIdx.x, threadIdx.x >> 6);
+    }
+#endif
+    if (!ok && lane == 0) {
+        // detail: the tile (bits 0-23); bits 24-30: how far the epoch is behind (an agent-scope atomic's
+        // read, capped at 127); bit 31: that read is behind too (clear: only the polls saw a stale value)
+        const uint32_t t = pt_entry_tile(e), part = pt_entry_part(e);
+        uint32_t m = ~0u;
+        if (part != 2u) m = __hip_atomic_fetch_add(const_cast<uint32_t*>(ep + 2u * t), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (part != 1u) {
+            const uint32_t b = __hip_atomic_fetch_add(const_cast<uint32_t*>(ep + 2u * t + 1u), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            m = b < m ? b : m;
+        }
+        const uint32_t behind = m >= w ? 0u : (w - m < 127u ? w - m : 127u);
+        pt_guard_report(err, PT_G_CHAIN_WAIT, (t & 0xffffffu) | (behind << 24) | (m < w ? 0x80000000u : 0u));
+    }
 }
 
 // (the whole wave) after entry e's last pixel store: publish sequence number seq for it.  delay: the

@@ -96,7 +96,7 @@ enum PtGuardId : uint32_t {
     PT_G_SCHED_UNIT = 10,   // the schedule builder: a unit index > 2 x tiles
     PT_G_RECORD = 11,       // a tile's item record slot >= 64
     PT_G_QUEUE_GROUP = 12,  // a queue group counter beyond PT_NQUEUES
-    PT_G_CHAIN_WAIT = 13,   // a chained launch waited > ~1.3 s for the previous launch's tile (every build)
+    PT_G_CHAIN_WAIT = 13,   // a chained launch polled 2^21 times (>= 2 s) for the previous launch's tile (every build)
 };
 
 // Tile queues: one counter per XCD group, 128 B apart (PT_QUEUE_WORDS u32 per launch).

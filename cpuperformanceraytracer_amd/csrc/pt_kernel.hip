@@ -1238,6 +1238,9 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     // chained launches: this block has started (the next launch's stream waits for every block of
     // this one: hipStreamWaitValue64 in pt_capi.cpp launch_chain)
     pt_chain_started(job.started);
+#if PT_CHAIN_DIAG
+    if (job.tile_epoch && blockIdx.x == 0 && threadIdx.x == 0) job.queue[kPtDiagWaves] = gridDim.x * (blockDim.x / 64u);
+#endif
     const PtScene* __restrict__ sc = job.scene;
     constexpr int kWavesPerBlock = waves_per_block<ENV>();
     constexpr bool QV = true;
@@ -1354,7 +1357,7 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
     // chained launches (pt_chain.h): before touching entry e's pixels, wait for the previous launch's
     // epoch; after e's last pixel store, publish this launch's
     auto chain_wait_tile = [&](uint32_t e) {
-        if (job.chain_wait != 0u) pt_chain_wait(job.tile_epoch, e, job.chain_wait, job.err, lane);
+        if (job.chain_wait != 0u) pt_chain_wait(job.tile_epoch, e, job.chain_wait, job.err, lane, PT_CHAIN_DIAG ? job.queue : nullptr);
     };
     auto chain_publish = [&](uint32_t e) {
         if (job.tile_epoch) pt_chain_publish(job.tile_epoch, e, job.chain_seq, job.chain_delay, lane);
@@ -1738,6 +1741,9 @@ __device__ __forceinline__ void render_body_ct(const PtJob& job)
         atomicMin(&job.err[1], pt_entry_tile(nitA > 0 ? ws_ld(kWsTcur) : (hasD ? ws_ld(kWsTD) : 0u)));
     }
     PtTileQueue<kWavesPerBlock>::restore(s_tq[wv]).report(job.err);   // (a schedule entry outside the launch)
+#if PT_CHAIN_DIAG
+    if (job.tile_epoch && lane == 0) atomicAdd(job.queue + kPtDiagEnded, 1u);
+#endif
 #if PT_DIAG
     if (job.counters && lane == 0) {
         unsigned long long* rec = job.counters + 32 + 4 * (size_t)(blockIdx.x * kWavesPerBlock + wv);

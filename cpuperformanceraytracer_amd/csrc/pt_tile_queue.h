@@ -61,6 +61,9 @@ __device__ __forceinline__ void pt_queue_zero_next(unsigned int* queue_next)
 {
     if (queue_next && blockIdx.x == 0 && threadIdx.x < PT_NQUEUES)
         *reinterpret_cast<unsigned long long*>(queue_next + threadIdx.x * 32u) = 0ull;
+#if PT_CHAIN_DIAG   // (pt_chain.h's diagnostic words 34-36)
+    if (queue_next && blockIdx.x == 0 && threadIdx.x >= 64 && threadIdx.x < 67) queue_next[34 + threadIdx.x - 64] = 0u;
+#endif
 }
 
 // A group's counter is 64 bits: dynamic units taken from the front (low word: longest first) and

@@ -342,3 +342,62 @@ def test_drive_completes_on_every_rank(world):
     assert ("cpu_baseline" in res) == (world == 1)
     if world > 1:
         assert res["configs4"]["verified"]["bit_exact"]
+
+
+def _worker_chain_fallback(port, q):
+    """bench.drive with chained steps whose run ends in a chained-launch wait error (guard 13): the line
+    is measured again with plain steps and says so."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import torch.distributed as dist
+    import bench
+    from cpuperformanceraytracer_amd._native import PtError
+    from cpuperformanceraytracer_amd.config import Workload
+    from oracle import pyoracle
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        wl = Workload("tiny", 64, 36, 3, 8, scaling="weak")
+        args = bench.parse(["--steps", "2", "--warmup", "1", "--device-warmup-ms", "0", "--no-configs4",
+                            "--no-cpu-baseline"])
+        modes, failed = [], []
+
+        def render_fn(buf, W, H, f, n, rs, st, nr, chain=False):
+            modes.append(chain)
+            pyoracle.render(W, H, frame_first=f, nframes=n, num_bounces=8, row_start=rs, row_stride=st, nrows=nr,
+                            nthreads=2, buf=buf.numpy())
+
+        def count_fn(buf, W, H, f, n, rs, st, nr):
+            render_fn(buf, W, H, f, n, rs, st, nr)
+            _, c = pyoracle.render_counted(W, H, frame_first=f, nframes=n, num_bounces=8, row_start=rs,
+                                           row_stride=st, nrows=nr)
+            return {"segments": c["segments"], "samples": c["samples"], "escaped": c["escaped"],
+                    "lane_slots": c["segments"], "primary": c["samples"]}
+
+        def check_errors():
+            if True in modes and not failed:
+                failed.append(1)
+                raise PtError(-5, "pt_check", "device 0: 9 kernel bounds guard failure(s), the first: guard 13 "
+                                              "(chained launch: the previous launch's tile never became ready)")
+
+        hooks = bench.Hooks(check_errors=check_errors, chain_counts=lambda: {"restarts": 0, "continued": 0})
+        out = bench.drive(args, wl, 0, 1, bench.HostOps(), render_fn, count_fn, hooks)
+        q.put((out["launch_chain"], sorted(set(modes))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_drive_measures_plain_steps_after_a_chain_wait_error():
+    """A chained run that ends in guard PT_G_CHAIN_WAIT (residency) is measured again with
+    plain launches: the line reports launch_chain.enabled false and the error."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker_chain_fallback, args=(_free_port(), q))
+    p.start()
+    chain, modes = q.get(timeout=240)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert chain["enabled"] is False and "guard 13" in chain["chained_run_failed"], chain
+    assert modes == [False, True]
