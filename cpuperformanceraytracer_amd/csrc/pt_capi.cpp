@@ -138,6 +138,9 @@ struct Dev {
         int area = 0;                      // slot area of the live chain's last launch (0: dct, 1: area1)
         int par = 0;                       // stream of the live chain's last launch
         unsigned long long restarts = 0, continued = 0;   // chained launches of each kind (pt_chain_counts)
+        // a chained launch's wait ran out on this device (guard PT_G_CHAIN_WAIT, reported by sync_all):
+        // chained calls are plain launches from then on ("Residency")
+        bool off = false;
     } chain;
 };
 
@@ -375,6 +378,7 @@ int sync_all()
         memcpy(dv.herr, init, sizeof(init));
         HIP_TRY(hipMemcpyAsync(dv.derr, dv.herr, sizeof(init), hipMemcpyHostToDevice, dv.stream));
         HIP_TRY(hipStreamSynchronize(dv.stream));
+        if (guards && (uint32_t)(first >> 32) == PT_G_CHAIN_WAIT) dv.chain.off = true;
         if (guards)
             return fail(PT_EKERNEL, "device %d: %u kernel bounds guard failure(s), the first: guard %u (%s), value %u; "
                         "pool guards: %u (first tile %u); the accumulator is invalid", dv.ordinal, guards,
@@ -982,6 +986,7 @@ int launch_chain(Dev& dv, Job j, hipStream_t s)
 {
     int rc;
     if ((rc = use_dev(dv))) return rc;
+    if (dv.chain.off) return chain_restart(dv, j, s, nullptr, nullptr);   // (a plain launch: use_sched joins the chain)
     const SchedKey key = chain_key(j);
     // (the continuous-tiles pool and a scheduled geometry: the tile epochs live in its schedule)
     Sched* sc = g.no_ct || j.ncols <= 0 || j.nrows <= 0 || j.nframes <= 0 ? nullptr : find_sched(dv, key, s);
@@ -1607,6 +1612,13 @@ int init_dev(Dev& dv, int32_t ordinal)
     if (hipMalloc(&dv.dscene, sizeof(PtScene)) != hipSuccess) return fail(PT_ENOMEM, "hipMalloc(scene) failed");
     HIP_TRY(hipEventCreateWithFlags(&dv.ev_gather, hipEventDisableTiming));
     HIP_TRY(hipMemcpy(dv.dscene, &g.scene, sizeof(PtScene), hipMemcpyHostToDevice));
+    {   // the chained-launch wait bound (pt_chain.h; test hook PT_MI355_TEST_CHAIN_POLLS, else the default --
+        // set on every init: the device symbols outlive pt_shutdown)
+        const char* tp = getenv("PT_MI355_TEST_CHAIN_POLLS");
+        const uint32_t polls = tp ? (uint32_t)strtoul(tp, nullptr, 10) : 0u;
+        HIP_TRY(pt_set_chain_polls(polls));
+        HIP_TRY(pt_v4_set_chain_polls(polls));
+    }
     return PT_OK;
 }
 

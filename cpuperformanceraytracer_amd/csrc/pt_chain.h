@@ -109,6 +109,9 @@ __device__ __forceinline__ bool pt_chain_ready(const uint32_t* ep, uint32_t e, u
 #define PT_CHAIN_DIAG 0
 #endif
 constexpr uint32_t kPtChainPolls = PT_CHAIN_DIAG ? 1u << 16 : 1u << 21;
+// the bound, per translation unit and device (test hook PT_MI355_TEST_CHAIN_POLLS: pt_set_chain_polls /
+// pt_v4_set_chain_polls), read only once a wait has begun
+static __device__ uint32_t pt_chain_polls_dev = kPtChainPolls;
 constexpr uint32_t kPtDiagWaves = 34, kPtDiagEnded = 35, kPtDiagWaiting = 36;
 // (diag) the tile-queue block of the chained launch before the one whose block is q (seq: its number)
 __device__ __forceinline__ unsigned* pt_chain_diag_prev(unsigned* q, uint32_t seq)
@@ -125,7 +128,7 @@ __device__ __forceinline__ void pt_chain_wait(const uint32_t* ep, uint32_t e, ui
     do {
         __builtin_amdgcn_s_sleep(8);   // (~0.2 us; a poll's sc1 loads take ~1-2 us more)
         ok = pt_chain_ready(ep, e, w);
-    } while (!ok && ++polls < kPtChainPolls);
+    } while (!ok && ++polls < pt_chain_polls_dev);
     if (PT_CHAIN_DIAG && qdiag && lane == 0) atomicSub(qdiag + kPtDiagWaiting, 1u);
 #if PT_CHAIN_DIAG
     if (!ok && lane == 0 && qdiag) {

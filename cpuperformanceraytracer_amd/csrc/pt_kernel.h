@@ -134,6 +134,9 @@ inline uint32_t pt_job_tiles(const PtJob& j)
 // cost: 2 x ntiles words (pt_record_cost), order: up to 2 x ntiles entries, units: 2 x ntiles + 1.
 // unit_mult: a multiple of the adaptive unit cost (the continuous-tiles pools: 2).
 // err: the device's error words (the checked build's guards; nullptr: none).
+// The chained-launch wait bound of this library's diffuse kernels on the current device (test hook:
+// pt_chain.h pt_chain_polls_dev; 0: the default)
+hipError_t pt_set_chain_polls(uint32_t polls);
 hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* units, uint32_t* nunits,
                               uint32_t ntiles, uint32_t split, uint32_t unit_mult, hipStream_t stream,
                               uint32_t* err = nullptr);

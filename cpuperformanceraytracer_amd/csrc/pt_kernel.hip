@@ -2088,6 +2088,12 @@ hipError_t pt_launch_schedule(const uint32_t* cost, uint32_t* order, uint32_t* u
     return hipGetLastError();
 }
 
+hipError_t pt_set_chain_polls(uint32_t polls)
+{
+    const uint32_t v = polls ? polls : kPtChainPolls;
+    return hipMemcpyToSymbol(HIP_SYMBOL(pt_chain_polls_dev), &v, sizeof(v));
+}
+
 uint32_t pt_ct_wave_floats() { return kCtWaveFloats; }
 
 int32_t pt_ct_env_waves() { return PT_ENV_WAVES; }

@@ -101,5 +101,7 @@ bool pt_v4_is_default_geometry(const PtV4Scene& s);                // geometry =
 // presenting configuration, pt_v4.hip pt_launch_v4 -- otherwise the caller converts separately)
 // *ct_blocks (optional): the grid of the continuous-tiles kernel it launched (0: the per-tile pool, or
 // nothing launched) -- a chained launch's gate waits for that many started blocks.
+// (as pt_set_chain_polls, for the v4 kernels)
+hipError_t pt_v4_set_chain_polls(uint32_t polls);
 hipError_t pt_launch_v4(const PtV4Job& job, const PtV4Scene& scene, hipStream_t stream, bool count,
                         bool* presented = nullptr, uint32_t* ct_blocks = nullptr);

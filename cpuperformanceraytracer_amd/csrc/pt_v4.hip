@@ -1545,6 +1545,12 @@ hipError_t launch_env(const PtV4Job& j, const PtV4Scene& sc, hipStream_t st, boo
 
 }  // namespace
 
+hipError_t pt_v4_set_chain_polls(uint32_t polls)
+{
+    const uint32_t v = polls ? polls : kPtChainPolls;
+    return hipMemcpyToSymbol(HIP_SYMBOL(pt_chain_polls_dev), &v, sizeof(v));
+}
+
 hipError_t pt_launch_v4(const PtV4Job& j_in, const PtV4Scene& sc, hipStream_t st, bool count, bool* presented,
                         uint32_t* ct_blocks)
 {

@@ -32,7 +32,8 @@ def fresh(monkeypatch):
         pt.init(num_bounces=B)
     yield init
     pt.shutdown()
-    for k in ("PT_MI355_CT_WAVES", "PT_MI355_BACK", "PT_MI355_TEST_CHAIN_DELAY", "PT_MI355_V4_CT"):
+    for k in ("PT_MI355_CT_WAVES", "PT_MI355_BACK", "PT_MI355_TEST_CHAIN_DELAY", "PT_MI355_V4_CT",
+              "PT_MI355_TEST_CHAIN_POLLS"):
         monkeypatch.delenv(k, raising=False)
 
 
@@ -142,6 +143,22 @@ def test_chained_launches_that_wait_match_oracle(fresh):
     fresh(B, PT_MI355_CT_WAVES="6", PT_MI355_TEST_CHAIN_DELAY="300")
     img, frames, counts = _series(W, H, B, S, 10)
     assert counts["continued"] >= 7, counts
+    ref = pyoracle.render(W, H, nframes=frames, num_bounces=B)
+    assert bits_equal(img, ref), mismatch_report(img, ref)
+
+
+def test_chain_wait_error_stops_chaining(fresh):
+    """A chained launch whose wait for its predecessor's tile runs out -- forced here: a 16-poll bound
+    (PT_MI355_TEST_CHAIN_POLLS) against ~2 ms publication delays -- is reported as guard 13
+    (PT_EKERNEL), never a hang, and the device stops chaining ("Residency"): the next
+    series of chained calls runs as plain launches (none continues) and equals the oracle."""
+    from cpuperformanceraytracer_amd._native import PtError
+    W, H, B, S = 320, 180, 8, 8
+    fresh(B, PT_MI355_CT_WAVES="6", PT_MI355_TEST_CHAIN_DELAY="2000", PT_MI355_TEST_CHAIN_POLLS="16")
+    with pytest.raises(PtError, match="guard 13"):
+        _series(W, H, B, S, 6)
+    img, frames, counts = _series(W, H, B, S, 6)
+    assert counts["continued"] == 0 and counts["restarts"] == 0, counts
     ref = pyoracle.render(W, H, nframes=frames, num_bounces=B)
     assert bits_equal(img, ref), mismatch_report(img, ref)
 
