@@ -78,7 +78,10 @@ constexpr int kSchedSlots = 16;
 constexpr int kBands = 4;   // PT_FLAG_PIN_HOST: row bands of a pipelined frame
 constexpr uint32_t kSchedMinTiles = 512;   // smaller jobs (e.g. one RenderTile) are not scheduled
 constexpr unsigned kQueueRing = 256;       // tile-queue ring slots (reuse across streams is event-ordered)
-constexpr unsigned long long kSchedRebuild = 64;
+// launches per schedule build (g.sched_rebuild; PT_MI355_SCHED_REBUILD): 256 -- a build restarts the
+// chained overlap and costs a one-workgroup kernel (~57 us at 1080p); 3-round A/B of chained steps vs 64
+// (profiles/r06/r06zl_*): c2 0.2160 vs 0.2189 ms, c4 0.4582 vs 0.4633, v4 0.3286 vs 0.3313
+constexpr unsigned long long kSchedRebuildDefault = 256;
 
 // One (logical) device: its streams, scene, tile queues, schedules, env map and the mirror of its
 // share of the caller's host accumulator.  Several logical devices may name the same HIP device
@@ -197,6 +200,7 @@ struct State {
     bool no_ct = false;   // PT_MI355_NO_CT=1 (read by pt_init): one-chunk launches on render_body (A/B)
     uint32_t test_chain_delay = 0;   // PT_MI355_TEST_CHAIN_DELAY=<us> (pt_init): chained launches publish late
     uint32_t unit_mult = 2;          // PT_MI355_UNIT_MULT (pt_init, A/B): the diffuse CT schedule's unit multiple
+    unsigned long long sched_rebuild = kSchedRebuildDefault;   // PT_MI355_SCHED_REBUILD (pt_init): launches per schedule build
 };
 
 State g;
@@ -663,9 +667,9 @@ int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls, uin
     if ((rc = chain_join(dv, st))) return rc;
     if (Sched* s = find_sched(dv, key, sched_st ? *sched_st : st)) {
         // (re)build the schedule from the last launch's costs on the 2nd launch of a geometry and
-        // then every kSchedRebuild launches (the costs of a fixed view barely change; the builder
+        // then every g.sched_rebuild launches (the costs of a fixed view barely change; the builder
         // is a one-workgroup kernel of ~57 us at 1080p)
-        if (s->have_cost && (!s->built || s->launches % kSchedRebuild == 0)) {
+        if (s->have_cost && (!s->built || s->launches % g.sched_rebuild == 0)) {
             // units of twice the adaptive cost for the diffuse kernels' continuous-tiles pool, whose
             // lanes no longer idle in a unit's tail while the dequeues still cost (A/B, 60 launches:
             // 1080p 8 spp 0.2497 vs 0.2525 ms, env 16 spp 0.4911 vs 0.4961, 4K 8 spp 0.8185 vs 0.8202;
@@ -686,7 +690,7 @@ int use_sched(Dev& dv, const SchedKey& key, hipStream_t st, LaunchSched* ls, uin
         }
         // the kernel records the tiles' costs only when the next launch builds from them (one 4-B
         // store per tile is a 32-B HBM write: ~1 MB per 1080p launch otherwise)
-        if (!s->built || (s->launches + 1) % kSchedRebuild == 0) {
+        if (!s->built || (s->launches + 1) % g.sched_rebuild == 0) {
             ls->cost = s->cost;
             s->have_cost = true;
         }
@@ -998,8 +1002,8 @@ int launch_chain(Dev& dv, Job j, hipStream_t s)
     // what the plain launch's use_sched would do for this launch: build the schedule (restart), record
     // the costs it is built from (a launch that records them may continue: the overlapped launches
     // before it do not write them, and the next launch, which builds from them, restarts)
-    const bool builds = sc->have_cost && (!sc->built || sc->launches % kSchedRebuild == 0);
-    const bool records = !sc->built || (sc->launches + 1) % kSchedRebuild == 0;
+    const bool builds = sc->have_cost && (!sc->built || sc->launches % g.sched_rebuild == 0);
+    const bool records = !sc->built || (sc->launches + 1) % g.sched_rebuild == 0;
     const bool cont = c.sched == sc && sc->built && !builds && chain_variant_fixed(j, *sc);
     const uint32_t seq = sc->chain_seq + 1;
     const int par = cont ? c.par ^ 1 : 0;
@@ -1712,6 +1716,8 @@ int pt_init(const pt_config* cfg)
     g.ring_guard_cap = ~0u;
     g.no_ct = getenv("PT_MI355_NO_CT") && !strcmp(getenv("PT_MI355_NO_CT"), "1");
     g.test_chain_delay = getenv("PT_MI355_TEST_CHAIN_DELAY") ? (uint32_t)strtoul(getenv("PT_MI355_TEST_CHAIN_DELAY"), nullptr, 10) : 0u;
+    g.sched_rebuild = getenv("PT_MI355_SCHED_REBUILD") ? std::max<unsigned long long>(2ull, strtoull(getenv("PT_MI355_SCHED_REBUILD"), nullptr, 10))
+                                                        : kSchedRebuildDefault;
     g.unit_mult = getenv("PT_MI355_UNIT_MULT") ? std::max<uint32_t>(1u, (uint32_t)strtoul(getenv("PT_MI355_UNIT_MULT"), nullptr, 10)) : 2u;
     g.v4_ct_force = getenv("PT_MI355_V4_CT") && !strcmp(getenv("PT_MI355_V4_CT"), "1");
     g.ct_back_pct = 20;

@@ -3,6 +3,7 @@ everything else runs on CPU (oracle vs golden fixtures, host logic, ABI exports,
 from __future__ import annotations
 
 import json
+import os
 import lzma
 import sys
 from pathlib import Path
@@ -14,6 +15,12 @@ ROOT = Path(__file__).resolve().parents[1]
 GOLDEN = ROOT / "tests" / "golden"
 if str(ROOT) not in sys.path:
     sys.path.insert(0, str(ROOT))
+
+
+# The suite's launches rebuild the tile schedule every 64 launches (the library's default is 256,
+# pt_capi.cpp kSchedRebuildDefault): the 66-70-launch series of test_gpu_regime / test_gpu_configs /
+# test_gpu_v4 / test_gpu_chain then cover a rebuild.  Set before any test initialises the library.
+os.environ.setdefault("PT_MI355_SCHED_REBUILD", "64")
 
 
 def pytest_configure(config):

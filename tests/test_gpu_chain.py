@@ -85,7 +85,7 @@ def test_c2_chained_regime_matches_oracle(fresh):
     warm-up): 40 rows spread over the image equal the oracle after 560 frames, and most launches
     overlapped."""
     W, H, B, S = 1920, 1080, 8, 8
-    fresh(B)
+    fresh(B)   # (conftest: a schedule rebuild every 64 launches, so one inside the 70)
     img, frames, counts = _series(W, H, B, S, 70, count_at=(5, 40), sync_at=(25,))
     assert counts["continued"] >= 30, counts
     _check_rows(img, W, H, frames, B, range(13, H, 27))

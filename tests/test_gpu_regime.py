@@ -27,7 +27,7 @@ from oracle import pyoracle
 
 pytestmark = pytest.mark.gpu
 
-K_SCHED_REBUILD = 64   # pt_capi.cpp kSchedRebuild
+K_SCHED_REBUILD = 64   # PT_MI355_SCHED_REBUILD as tests/conftest.py sets it (pt_capi.cpp)
 
 
 def _launch_series(W, H, B, S, launches, *, row_start=0, row_stride=1, nrows=None, env=False, count_at=(),
